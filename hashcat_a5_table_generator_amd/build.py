@@ -1,0 +1,64 @@
+"""Build liba5x.so (HIP kernels for gfx950 + C++ host) and the CLI replica in-tree.
+
+``python -m hashcat_a5_table_generator_amd.build`` or ``__graft_entry__.build()``.
+Outputs go to ``hashcat_a5_table_generator_amd/_build/`` (git-ignored, but they
+travel to the GPU box with the gpurun snapshot).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OUT = os.path.join(PKG, "_build")
+LIB = os.path.join(OUT, "liba5x.so")
+CLI = os.path.join(OUT, "a5x_generator")
+ARCH = os.environ.get("A5X_OFFLOAD_ARCH", "gfx950")
+
+LIB_SRCS = ["a5x_kernels.hip", "a5x_host.cpp"]
+HEADERS = ["a5x_format.h", "a5x_gosem.h", "a5x_launch.h"]
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm is required to build liba5x)")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    hipcc = _hipcc()
+    srcs = [os.path.join(CSRC, s) for s in LIB_SRCS]
+    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "a5x.h")]
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    if force or _stale(LIB, deps):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-fvisibility=hidden", *inc, *srcs, "-o", LIB + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(LIB + ".tmp", LIB)
+    cli_src = os.path.join(CSRC, "a5x_cli.cpp")
+    if os.path.exists(cli_src) and (force or _stale(CLI, [cli_src, LIB])):
+        cmd = [hipcc, "-O2", "-std=c++17", *inc, cli_src, "-o", CLI, "-L", OUT, "-la5x",
+               "-Wl,-rpath,$ORIGIN"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

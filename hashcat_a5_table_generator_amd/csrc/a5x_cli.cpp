@@ -1,0 +1,147 @@
+// a5x_cli.cpp -- `a5x_generator`: C++ replica of the reference CLI (main.go:17-100)
+// on top of liba5x.  Same flags (main.go:18-26, kong conventions), same
+// "cand\n" stdout format (main.go:66).  Used by tests and benchmarks because the
+// Go toolchain is absent here; the Go CLI itself binds liba5x through the cgo
+// stub shown in INTEGRATION.md.
+//
+//   a5x_generator <dict-file> -t <table> [-t <table> ...] [-m N] [-x N]
+//                 [--threads N] [-s] [-r] [--device N]
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "a5x.h"
+
+static void usage(FILE* f) {
+  fprintf(f,
+          "Usage: a5_generator --table-files=TABLE-FILES,... <dict-file> [flags]\n\n"
+          "Generates word variations based on a substitution table. v0.2\n\n"
+          "Arguments:\n  <dict-file>    Path to dictionary file\n\n"
+          "Flags:\n"
+          "  -h, --help                        Show context-sensitive help.\n"
+          "  -t, --table-files=TABLE-FILES,... Path to substitution table (multiple possible, sequential)\n"
+          "  -m, --table-min=0                 Minimum substitutions\n"
+          "  -x, --table-max=15                Maximum substitutions\n"
+          "      --threads=-1                  Number of threads (accepted; the GPU needs none)\n"
+          "  -s, --substitute-all              Substitution Cipher, see Transliteration Attack\n"
+          "  -r, --reverse-sub                 Reverse substitution direction\n"
+          "      --device=0                    GPU ordinal (a5x extension)\n");
+}
+
+static int sink_stdout(void* user, const uint8_t* data, size_t len) {
+  (void)user;
+  return fwrite(data, 1, len, stdout) == len ? 0 : 1;
+}
+
+static bool parse_int(const char* s, int* out) {
+  char* e;
+  long v = strtol(s, &e, 10);
+  if (!*s || *e) return false;
+  *out = (int)v;
+  return true;
+}
+
+int main(int argc, char** argv) {
+  std::vector<std::string> tables;
+  std::string dict;
+  int tmin = 0, tmax = 15, threads = -1, device = 0;
+  bool suball = false, rev = false;
+  auto need = [&](int& i, const char* flag) -> const char* {
+    if (i + 1 >= argc) {
+      fprintf(stderr, "a5_generator: error: %s: expected value\n", flag);
+      usage(stderr);
+      exit(80);
+    }
+    return argv[++i];
+  };
+  auto add_tables = [&](const char* v) {  // kong []string flags split on ','
+    std::string s(v);
+    size_t p = 0;
+    while (true) {
+      size_t q = s.find(',', p);
+      tables.push_back(s.substr(p, q == std::string::npos ? std::string::npos : q - p));
+      if (q == std::string::npos) break;
+      p = q + 1;
+    }
+  };
+  for (int i = 1; i < argc; i++) {
+    const char* a = argv[i];
+    std::string s(a);
+    auto val_of = [&](const char* flag) -> const char* {
+      size_t eq = s.find('=');
+      if (eq != std::string::npos) return a + eq + 1;
+      return need(i, flag);
+    };
+    int v;
+    if (s == "-h" || s == "--help") { usage(stdout); return 0; }
+    else if (s == "-t" || s.rfind("--table-files", 0) == 0) add_tables(val_of("--table-files"));
+    else if (s == "-m" || s.rfind("--table-min", 0) == 0) {
+      if (!parse_int(val_of("--table-min"), &v)) { fprintf(stderr, "a5_generator: error: --table-min: bad int\n"); return 80; }
+      tmin = v;
+    } else if (s == "-x" || s.rfind("--table-max", 0) == 0) {
+      if (!parse_int(val_of("--table-max"), &v)) { fprintf(stderr, "a5_generator: error: --table-max: bad int\n"); return 80; }
+      tmax = v;
+    } else if (s.rfind("--threads", 0) == 0) {
+      if (!parse_int(val_of("--threads"), &v)) { fprintf(stderr, "a5_generator: error: --threads: bad int\n"); return 80; }
+      threads = v;
+    } else if (s.rfind("--device", 0) == 0) {
+      if (!parse_int(val_of("--device"), &v)) { fprintf(stderr, "a5_generator: error: --device: bad int\n"); return 80; }
+      device = v;
+    } else if (s == "--substitute-all") suball = true;
+    else if (s == "--reverse-sub") rev = true;
+    else if (s.size() > 1 && s[0] == '-' && s[1] != '-') {
+      bool ok = true;  // combined boolean shorts, e.g. -sr
+      for (size_t k = 1; k < s.size(); k++) {
+        if (s[k] == 's') suball = true;
+        else if (s[k] == 'r') rev = true;
+        else ok = false;
+      }
+      if (!ok) { fprintf(stderr, "a5_generator: error: unknown flag %s\n", a); usage(stderr); return 80; }
+    } else if (dict.empty()) dict = s;
+    else { fprintf(stderr, "a5_generator: error: unexpected argument %s\n", a); usage(stderr); return 80; }
+  }
+  (void)threads;
+  if (tables.empty()) { fprintf(stderr, "a5_generator: error: missing flags: --table-files=TABLE-FILES,...\n"); usage(stderr); return 80; }
+  if (dict.empty()) { fprintf(stderr, "a5_generator: error: expected \"<dict-file>\"\n"); usage(stderr); return 80; }
+
+  a5x_ctx* ctx = nullptr;
+  int rc = a5x_create(device, &ctx);
+  if (rc) { fprintf(stderr, "a5_generator: no usable GPU (a5x_create=%d)\n", rc); return 1; }
+  for (auto& t : tables) {
+    rc = a5x_load_table_file(ctx, t.c_str());
+    if (rc) { fprintf(stderr, "%s\n", a5x_last_error(ctx)); a5x_destroy(ctx); return 1; }  // log.Fatal
+  }
+  FILE* f = fopen(dict.c_str(), "rb");
+  if (!f) { perror(dict.c_str()); a5x_destroy(ctx); return 1; }
+  std::vector<uint8_t> data;
+  {
+    uint8_t buf[1 << 16];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof buf, f)) > 0) data.insert(data.end(), buf, buf + r);
+    fclose(f);
+  }
+  uint64_t n = 0;
+  a5x_split_words(data.data(), data.size(), nullptr, nullptr, 0, &n);
+  std::vector<uint8_t> words(data.size() + 16);
+  std::vector<uint64_t> off(n + 2);
+  a5x_split_words(data.data(), data.size(), words.data(), off.data(), off.size(), &n);
+  static char obuf[1 << 22];
+  setvbuf(stdout, obuf, _IOFBF, sizeof obuf);
+  const int mode = (suball ? A5X_MODE_SUBALL : A5X_MODE_DEFAULT) + (rev ? 1 : 0);
+  const uint64_t B = 1u << 22;
+  std::vector<uint64_t> sub;
+  for (uint64_t b0 = 0; b0 < n && rc == 0; b0 += B) {
+    const uint64_t b1 = b0 + B < n ? b0 + B : n;
+    sub.resize(b1 - b0 + 1);
+    for (uint64_t i = b0; i <= b1; i++) sub[i - b0] = off[i] - off[b0];
+    rc = a5x_expand(ctx, words.data() + off[b0], sub.data(), b1 - b0, mode, tmin, tmax, sink_stdout, nullptr,
+                    nullptr);
+  }
+  fflush(stdout);
+  if (rc) fprintf(stderr, "a5_generator: %s\n", a5x_last_error(ctx));
+  a5x_destroy(ctx);
+  return rc ? 2 : 0;
+}

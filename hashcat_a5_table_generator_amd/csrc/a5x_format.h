@@ -1,0 +1,78 @@
+// a5x_format.h -- layouts shared by the host compiler of substitution tables
+// (a5x_host.cpp) and the HIP kernels (a5x_kernels.hip).
+//
+// The merged Go map[string][]string of main.go:40-50 is compiled into one flat
+// "device table" blob that every workgroup copies into LDS once:
+//
+//   A5xTableHdr                                   (64 B)
+//   u16 bucket[257]  keys whose first byte is b are [bucket[b], bucket[b+1])
+//   A5xKey  keys[nkeys]                           (16 B each, 16-B aligned)
+//   A5xChoice choices[nchoices]                   (8 B each)
+//   u8 blob[blob_bytes]                           (key + value bytes, 8-B padded)
+//
+// Choice 0 of key k (choices[k.choice_base]) is the key itself (the "keep"
+// branch); choice 1+v is value v in (-t file, line) order (main.go:141, 48).
+#pragma once
+#include <stdint.h>
+
+#define A5X_TABLE_MAGIC 0x58354131u  // "1A5X"
+
+struct A5xTableHdr {
+  uint32_t magic;
+  uint32_t total_bytes;   // whole blob, multiple of 16
+  uint32_t nkeys;         // keys with length >= 1 (an empty key never matches in
+                          // processWord / processWordReverse: keyLength >= 1)
+  uint32_t nchoices;
+  uint32_t off_bucket;    // byte offsets inside the blob
+  uint32_t off_keys;
+  uint32_t off_choices;
+  uint32_t off_blob;
+  uint32_t blob_bytes;
+  uint32_t max_klen;
+  uint32_t max_vlen;
+  uint32_t has_empty_key; // the map has "" (matters for -s only, main.go:315)
+  uint32_t pad[4];
+};
+
+struct A5xKey {
+  uint16_t klen;
+  uint16_t nvals;
+  uint32_t choice_base;   // choices[choice_base] = key, [choice_base+1+v] = value v
+  uint32_t sumlen;        // sum of value lengths (byte DP)
+  int16_t maxdelta;       // max(|v|) - klen
+  uint16_t pad;
+};
+
+struct A5xChoice {
+  uint32_t first4;        // first min(len,4) bytes, little-endian, zero padded
+  uint16_t len;
+  uint16_t blob_off;      // offset in blob (valid for any len)
+};
+
+static_assert(sizeof(A5xTableHdr) == 64, "hdr");
+static_assert(sizeof(A5xKey) == 16, "key");
+static_assert(sizeof(A5xChoice) == 8, "choice");
+
+// Per-word class flags written by the keyspace pass (u32 per word).
+enum : uint32_t {
+  A5X_WF_RADIX = 1u << 0,   // disjoint single matches, free count window: mixed radix
+  A5X_WF_BIN = 1u << 1,     // ... and every slot has exactly one value (radix 2)
+  A5X_WF_GENERAL = 1u << 2, // overlapping / multi matches or capped: DP walk
+  A5X_WF_BIG = 1u << 3,     // does not fit the pass-A wave budget: pass B
+  A5X_WF_DEFER = 1u << 4,   // keyspace needs the wave-level DP kernel
+  A5X_WF_ERR_OVF = 1u << 8, // count/bytes overflow u64
+  A5X_WF_ERR_BIG = 1u << 9, // exceeds pass-B limits
+};
+
+// Limits of the expansion passes (documented in DESIGN.md).
+#define A5X_WAVE 64
+#define A5X_LMAX_A 64          // pass A: word bytes (one lane per position)
+#define A5X_DPENT_A 256        // pass A: DP table entries (G and H each), (events+1) x W
+#define A5X_MLMAX_A 128        // pass A: total key matches in a word
+#define A5X_RING_A 4096        // pass A: staging ring bytes per wave
+#define A5X_LMAX_B 2048        // pass B (one wave per workgroup)
+#define A5X_DPENT_B 4096
+#define A5X_MLMAX_B 4096
+#define A5X_RING_B 16384
+#define A5X_CMAX 63            // max DP columns-1 (count window)
+#define A5X_TABLE_LDS_MAX 32768

@@ -1,0 +1,782 @@
+// a5x_host.cpp -- host side of liba5x: the C ABI declared in include/a5x.h.
+//
+//   * substitution tables: Go-exact parser (readSubstitutionTable, main.go:108-144;
+//     decodeHexNotation, main.go:147-162) and the -t merge (main.go:40-50), then
+//     compiled into the flat LDS-resident device table of a5x_format.h;
+//   * dictionary splitting with bufio.ScanLines semantics (main.go:72-74);
+//   * the per-batch device pipeline (keyspace -> scans -> plan -> expand) on one
+//     HIP stream, replacing the goroutine-per-word dispatch and the single
+//     channel writer of main.go:58-98;
+//   * host-buffer convenience calls (a5x_keyspace, a5x_expand) that stage words
+//     into HBM and stream the expanded bytes back to a sink.
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "a5x.h"
+#include "a5x_format.h"
+#include "a5x_gosem.h"
+#include "a5x_launch.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// the merged map[string][]string (keys in first-appearance order)
+// ---------------------------------------------------------------------------
+struct Table {
+  std::vector<std::string> keys;
+  std::vector<std::vector<std::string>> vals;
+  std::unordered_map<std::string, uint32_t> index;
+
+  void add(const std::string& k, const std::string& v) {
+    auto it = index.find(k);
+    uint32_t i;
+    if (it == index.end()) {
+      i = (uint32_t)keys.size();
+      index.emplace(k, i);
+      keys.push_back(k);
+      vals.emplace_back();
+    } else {
+      i = it->second;
+    }
+    vals[i].push_back(v);
+  }
+  void clear() { keys.clear(); vals.clear(); index.clear(); }
+  size_t nvals() const {
+    size_t n = 0;
+    for (auto& v : vals) n += v.size();
+    return n;
+  }
+};
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+};
+
+}  // namespace
+
+struct a5x_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::string devname;
+  int cus = 0;
+
+  Table table;
+  bool table_dirty = true;
+  std::vector<uint8_t> blob;
+  uint8_t* d_table = nullptr;
+  size_t d_table_cap = 0;
+  uint32_t table_bytes = 0;
+
+  DevBuf<uint64_t> count, bytes, cand_off, byte_off, scan_tmp, locate;
+  DevBuf<uint32_t> flags, defer, chunk_w0, chunk_big;
+  uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] pad
+  uint32_t* h_scalars = nullptr;  // pinned
+  uint64_t* h_totals = nullptr;   // pinned [0] cands [1] bytes [2..3] locate
+
+  // host-API staging
+  DevBuf<uint8_t> s_words, s_out;
+  DevBuf<uint64_t> s_woff;
+  uint8_t* h_out = nullptr;
+  size_t h_out_cap = 0;
+
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t chunk = 1024;      // candidates per expand wave
+  uint32_t waves_per_block = 4;
+};
+
+namespace {
+
+int fail(a5x_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHK(c, x)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess) return fail((c), A5X_E_HIP, "%s failed: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+template <typename T>
+int grow(a5x_ctx* c, DevBuf<T>& b, size_t n) {
+  if (n <= b.cap) return A5X_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t want = n + n / 8 + 64;
+  hipError_t e = hipMalloc((void**)&b.p, want * sizeof(T));
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    return fail(c, A5X_E_NOMEM, "hipMalloc(%zu bytes) failed: %s", want * sizeof(T), hipGetErrorString(e));
+  }
+  b.cap = want;
+  return A5X_OK;
+}
+
+template <typename T>
+void release(DevBuf<T>& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
+// readSubstitutionTable on one file's bytes, merged into t (main.go:108-144 + 40-50)
+int parse_table_into(a5x_ctx* c, Table& t, const uint8_t* d, size_t n) {
+  using namespace a5x::gosem;
+  Table ft;  // the file's own map, then appended per key like main.go:47-49
+  size_t pos = 0;
+  const uint8_t* line;
+  size_t len;
+  int r;
+  while ((r = scan_line(d, n, &pos, &line, &len)) == 1) {
+    const uint8_t* s = line;
+    size_t m = len;
+    trim_space(&s, &m);
+    if (m == 0 || s[0] == '#') continue;
+    const uint8_t* eq = (const uint8_t*)memchr(s, '=', m);
+    if (!eq) continue;
+    std::string k, v;
+    const size_t kn = (size_t)(eq - s);
+    if (!decode_hex_notation(s, kn, &k)) {
+      fprintf(stderr, "Error decoding hex notation in key: %.*s\n", (int)m, (const char*)s);
+      continue;
+    }
+    if (!decode_hex_notation(eq + 1, m - kn - 1, &v)) {
+      fprintf(stderr, "Error decoding hex notation in value: %.*s\n", (int)m, (const char*)s);
+      continue;
+    }
+    ft.add(k, v);
+  }
+  if (r < 0) return fail(c, A5X_E_TOOLONG, "bufio.Scanner: token too long");
+  for (size_t i = 0; i < ft.keys.size(); i++)
+    for (auto& v : ft.vals[i]) t.add(ft.keys[i], v);
+  return A5X_OK;
+}
+
+// Compile the map into the device table blob of a5x_format.h.
+int compile_table(a5x_ctx* c) {
+  const Table& t = c->table;
+  std::vector<uint32_t> order;
+  for (uint32_t i = 0; i < t.keys.size(); i++)
+    if (!t.keys[i].empty()) order.push_back(i);
+  // bucket by first byte, longest key first inside a bucket
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    const uint8_t fa = (uint8_t)t.keys[a][0], fb = (uint8_t)t.keys[b][0];
+    if (fa != fb) return fa < fb;
+    return t.keys[a].size() > t.keys[b].size();
+  });
+  if (order.size() > 65535) return fail(c, A5X_E_UNSUPPORTED, "table has %zu keys (max 65535)", order.size());
+  std::vector<uint16_t> bucket(257, 0);
+  for (uint32_t i : order) bucket[(uint8_t)t.keys[i][0] + 1]++;
+  for (int b = 0; b < 256; b++) bucket[b + 1] += bucket[b];
+
+  std::vector<A5xKey> keys;
+  std::vector<A5xChoice> ch;
+  std::vector<uint8_t> blob;
+  uint32_t max_klen = 0, max_vlen = 0;
+  auto add_choice = [&](const std::string& s) -> int {
+    A5xChoice x;
+    memset(&x, 0, sizeof x);
+    if (s.size() > 65535) return -1;
+    x.len = (uint16_t)s.size();
+    for (size_t i = 0; i < s.size() && i < 4; i++) x.first4 |= (uint32_t)(uint8_t)s[i] << (8 * i);
+    if (blob.size() + s.size() > 65535) return -1;
+    x.blob_off = (uint16_t)blob.size();
+    blob.insert(blob.end(), s.begin(), s.end());
+    ch.push_back(x);
+    return 0;
+  };
+  for (uint32_t i : order) {
+    const std::string& k = t.keys[i];
+    const auto& vs = t.vals[i];
+    if (k.size() > 65535 || vs.size() > 65535)
+      return fail(c, A5X_E_UNSUPPORTED, "table key/value list too large for the device table");
+    A5xKey key;
+    memset(&key, 0, sizeof key);
+    key.klen = (uint16_t)k.size();
+    key.nvals = (uint16_t)vs.size();
+    key.choice_base = (uint32_t)ch.size();
+    int maxd = -65536;
+    if (add_choice(k)) return fail(c, A5X_E_UNSUPPORTED, "device table blob exceeds 64 KiB");
+    for (auto& v : vs) {
+      if (add_choice(v)) return fail(c, A5X_E_UNSUPPORTED, "device table blob exceeds 64 KiB");
+      key.sumlen += (uint32_t)v.size();
+      maxd = std::max(maxd, (int)v.size() - (int)k.size());
+      max_vlen = std::max(max_vlen, (uint32_t)v.size());
+    }
+    key.maxdelta = (int16_t)std::max(-32768, std::min(32767, maxd));
+    max_klen = std::max(max_klen, (uint32_t)k.size());
+    keys.push_back(key);
+  }
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  A5xTableHdr h;
+  memset(&h, 0, sizeof h);
+  h.magic = A5X_TABLE_MAGIC;
+  h.nkeys = (uint32_t)keys.size();
+  h.nchoices = (uint32_t)ch.size();
+  h.off_bucket = sizeof(A5xTableHdr);
+  h.off_keys = (uint32_t)al16(h.off_bucket + 257 * sizeof(uint16_t));
+  h.off_choices = (uint32_t)al16(h.off_keys + keys.size() * sizeof(A5xKey));
+  h.off_blob = (uint32_t)al16(h.off_choices + ch.size() * sizeof(A5xChoice));
+  h.blob_bytes = (uint32_t)blob.size();
+  h.total_bytes = (uint32_t)al16(h.off_blob + blob.size() + 8);  // 8 B tail for 4-byte reads
+  h.max_klen = max_klen;
+  h.max_vlen = max_vlen;
+  h.has_empty_key = t.index.count(std::string()) ? 1u : 0u;
+  if (h.total_bytes > A5X_TABLE_LDS_MAX)
+    return fail(c, A5X_E_UNSUPPORTED, "device table is %u bytes (LDS staging max %u)", h.total_bytes,
+                (unsigned)A5X_TABLE_LDS_MAX);
+  c->blob.assign(h.total_bytes, 0);
+  memcpy(c->blob.data(), &h, sizeof h);
+  memcpy(c->blob.data() + h.off_bucket, bucket.data(), 257 * sizeof(uint16_t));
+  if (!keys.empty()) memcpy(c->blob.data() + h.off_keys, keys.data(), keys.size() * sizeof(A5xKey));
+  if (!ch.empty()) memcpy(c->blob.data() + h.off_choices, ch.data(), ch.size() * sizeof(A5xChoice));
+  if (!blob.empty()) memcpy(c->blob.data() + h.off_blob, blob.data(), blob.size());
+  c->table_bytes = h.total_bytes;
+  return A5X_OK;
+}
+
+int upload_table(a5x_ctx* c) {
+  if (c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (c->table.keys.empty()) return fail(c, A5X_E_NOTABLE, "no substitution table loaded");
+  if (!c->table_dirty) return A5X_OK;
+  int rc = compile_table(c);
+  if (rc) return rc;
+  if (c->d_table_cap < c->blob.size()) {
+    if (c->d_table) (void)hipFree(c->d_table);
+    c->d_table = nullptr;
+    HIPCHK(c, hipMalloc((void**)&c->d_table, c->blob.size()));
+    c->d_table_cap = c->blob.size();
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_table, c->blob.data(), c->blob.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->table_dirty = false;
+  return A5X_OK;
+}
+
+int check_mode(a5x_ctx* c, int mode) {
+  if (mode < 0 || mode > 3) return fail(c, A5X_E_ARG, "bad mode %d", mode);
+  if (mode != A5X_MODE_DEFAULT)
+    return fail(c, A5X_E_UNSUPPORTED,
+                "mode %d (-r/-s) is not implemented on the device in this build; only processWord (default)",
+                mode);
+  return A5X_OK;
+}
+
+int decode_dev_err(a5x_ctx* c, uint32_t e) {
+  if (!e) return A5X_OK;
+  if (e & 2u) return fail(c, A5X_E_OVERFLOW, "a word's keyspace overflows 64 bits");
+  if (e & 16u) return fail(c, A5X_E_OVERFLOW, "batch keyspace overflows 64 bits");
+  if (e & 4u)
+    return fail(c, A5X_E_UNSUPPORTED,
+                "a word with candidates exceeds the device limits (length %d B, %d matches, DP (events+1) x "
+                "(min(max,matches)+1) <= %d)", A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B);
+  return fail(c, A5X_E_HIP, "device consistency error 0x%x", e);
+}
+
+struct Batch {  // device-side per-batch state after keyspace
+  uint64_t total_cands = 0, total_bytes = 0;
+  uint32_t nbig = 0;
+  const uint64_t* cand_off = nullptr;
+  const uint64_t* byte_off = nullptr;
+};
+
+// keyspace -> flags, per-word counts/bytes, exclusive scans (synchronises once)
+int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mn, int mx,
+                 uint64_t* d_cand_off, uint64_t* d_byte_off, hipStream_t st, Batch* B, bool timed) {
+  int rc;
+  if ((rc = upload_table(c))) return rc;
+  if (nw > 0xffffffffull) return fail(c, A5X_E_ARG, "batch of %llu words (max 2^32-1)", (unsigned long long)nw);
+  if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
+      (rc = grow(c, c->defer, nw + 1)) || (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)))
+    return rc;
+  if (!d_cand_off) {
+    if ((rc = grow(c, c->cand_off, nw + 1))) return rc;
+    d_cand_off = c->cand_off.p;
+  }
+  if (!d_byte_off) {
+    if ((rc = grow(c, c->byte_off, nw + 1))) return rc;
+    d_byte_off = c->byte_off.p;
+  }
+  if (timed) HIPCHK(c, hipEventRecord(c->ev[0], st));
+  HIPCHK(c, hipMemsetAsync(c->d_scalars, 0, 16, st));
+  if (nw > 0) {
+    A5xKsLaunch K;
+    K.table = c->d_table; K.table_bytes = c->table_bytes; K.words = d_words; K.woff = d_woff; K.nw = nw;
+    K.mn = mn; K.mx = mx; K.count = c->count.p; K.bytes = c->bytes.p; K.flags = c->flags.p;
+    K.defer_list = c->defer.p; K.defer_n = c->d_scalars; K.nbig = c->d_scalars + 1; K.err = c->d_scalars + 2;
+    K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nw, (uint64_t)c->cus * 4));
+    HIPCHK(c, a5x_launch_keyspace(K, st));
+    HIPCHK(c, a5x_launch_scan(c->count.p, c->bytes.p, nw, d_cand_off, d_byte_off, c->scan_tmp.p,
+                              c->d_scalars + 2, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_totals, d_cand_off + nw, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_totals + 1, d_byte_off + nw, 8, hipMemcpyDeviceToHost, st));
+  } else {
+    HIPCHK(c, hipMemsetAsync(d_cand_off, 0, 8, st));
+    HIPCHK(c, hipMemsetAsync(d_byte_off, 0, 8, st));
+    c->h_totals[0] = c->h_totals[1] = 0;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if ((rc = decode_dev_err(c, c->h_scalars[2]))) {
+    // name the first offending word (diagnostics)
+    std::vector<uint32_t> fl(nw);
+    std::vector<uint64_t> wo(nw + 1);
+    if (nw && hipMemcpy(fl.data(), c->flags.p, nw * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+        hipMemcpy(wo.data(), d_woff, (nw + 1) * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      for (uint64_t i = 0; i < nw; i++)
+        if (fl[i] & (A5X_WF_ERR_BIG | A5X_WF_ERR_OVF)) {
+          std::string w((size_t)(wo[i + 1] - wo[i]), '\0');
+          (void)hipMemcpy(&w[0], d_words + wo[i], w.size(), hipMemcpyDeviceToHost);
+          char tail[160];
+          snprintf(tail, sizeof tail, " [word %llu len %zu flags 0x%08x: %.40s]", (unsigned long long)i, w.size(),
+                   fl[i], w.c_str());
+          c->err += tail;
+          break;
+        }
+    }
+    return rc;
+  }
+  B->total_cands = nw ? c->h_totals[0] : 0;
+  B->total_bytes = nw ? c->h_totals[1] : 0;
+  B->nbig = c->h_scalars[1];
+  B->cand_off = d_cand_off;
+  B->byte_off = d_byte_off;
+  return A5X_OK;
+}
+
+A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mn, int mx,
+                        const Batch& B) {
+  A5xExpLaunch E;
+  memset(&E, 0, sizeof E);
+  E.table = c->d_table; E.table_bytes = c->table_bytes; E.words = d_words; E.woff = d_woff; E.nw = nw;
+  E.cand_off = B.cand_off; E.byte_off = B.byte_off; E.flags = c->flags.p; E.chunk_w0 = c->chunk_w0.p;
+  E.chunk_big = c->chunk_big.p; E.CH = c->chunk; E.mn = mn; E.mx = mx; E.err = c->d_scalars + 2;
+  E.waves_per_block = c->waves_per_block;
+  return E;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int a5x_abi_version(void) { return A5X_ABI_VERSION; }
+
+int a5x_create(int device, a5x_ctx** out) {
+  if (!out) return A5X_E_ARG;
+  *out = nullptr;
+  if (device == -1) {  // host-only context: tables, splitting, export (no GPU needed)
+    a5x_ctx* c = new a5x_ctx();
+    c->device = -1;
+    *out = c;
+    return A5X_OK;
+  }
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return A5X_E_HIP;
+  if (device < 0 || device >= n) return A5X_E_ARG;
+  a5x_ctx* c = new a5x_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return A5X_E_HIP;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+    c->devname = std::string(prop.name) + " (" + prop.gcnArchName + ")";
+    c->cus = prop.multiProcessorCount;
+  }
+  if (c->cus <= 0) c->cus = 256;
+  bool ok = hipMalloc((void**)&c->d_scalars, 64) == hipSuccess &&
+            hipHostMalloc((void**)&c->h_scalars, 64, 0) == hipSuccess &&
+            hipHostMalloc((void**)&c->h_totals, 64, 0) == hipSuccess && a5x_set_kernel_attrs() == hipSuccess;
+  for (int i = 0; i < 4 && ok; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  if (!ok) {
+    a5x_destroy(c);
+    return A5X_E_HIP;
+  }
+  if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
+  if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
+  *out = c;
+  return A5X_OK;
+}
+
+void a5x_destroy(a5x_ctx* c) {
+  if (!c) return;
+  if (c->device < 0) { delete c; return; }
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  release(c->count); release(c->bytes); release(c->cand_off); release(c->byte_off); release(c->scan_tmp);
+  release(c->locate); release(c->flags); release(c->defer); release(c->chunk_w0); release(c->chunk_big);
+  release(c->s_words); release(c->s_out); release(c->s_woff);
+  if (c->d_table) (void)hipFree(c->d_table);
+  if (c->d_scalars) (void)hipFree(c->d_scalars);
+  if (c->h_scalars) (void)hipHostFree(c->h_scalars);
+  if (c->h_totals) (void)hipHostFree(c->h_totals);
+  if (c->h_out) (void)hipHostFree(c->h_out);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* a5x_last_error(const a5x_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int a5x_device_info(a5x_ctx* c, char* name, size_t cap, int* cu_count) {
+  if (!c) return A5X_E_ARG;
+  if (name && cap) {
+    strncpy(name, c->devname.c_str(), cap - 1);
+    name[cap - 1] = 0;
+  }
+  if (cu_count) *cu_count = c->cus;
+  return A5X_OK;
+}
+
+int a5x_load_table_file(a5x_ctx* c, const char* path) {
+  if (!c || !path) return A5X_E_ARG;
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail(c, A5X_E_IO, "open %s: %s", path, strerror(errno));
+  std::vector<uint8_t> d;
+  uint8_t buf[65536];
+  size_t r;
+  while ((r = fread(buf, 1, sizeof buf, f)) > 0) d.insert(d.end(), buf, buf + r);
+  const bool err = ferror(f);
+  fclose(f);
+  if (err) return fail(c, A5X_E_IO, "read %s failed", path);
+  return a5x_parse_table(c, d.data(), d.size());
+}
+
+int a5x_parse_table(a5x_ctx* c, const uint8_t* data, size_t len) {
+  if (!c || (!data && len)) return A5X_E_ARG;
+  Table t = c->table;
+  int rc = parse_table_into(c, t, data, len);
+  if (rc) return rc;
+  c->table = std::move(t);
+  c->table_dirty = true;
+  return A5X_OK;
+}
+
+int a5x_set_table(a5x_ctx* c, const uint8_t* kb, const uint64_t* koff, uint32_t nk, const uint8_t* vb,
+                  const uint64_t* voff, const uint32_t* vkey, uint32_t nv) {
+  if (!c || (nk && !koff) || (nv && (!voff || !vkey))) return A5X_E_ARG;
+  Table t;
+  for (uint32_t i = 0; i < nk; i++) {
+    if (koff[i + 1] < koff[i]) return fail(c, A5X_E_ARG, "key offsets not monotone");
+    std::string k((const char*)kb + koff[i], (size_t)(koff[i + 1] - koff[i]));
+    if (t.index.count(k)) return fail(c, A5X_E_ARG, "duplicate key %u", i);
+    t.index.emplace(k, (uint32_t)t.keys.size());
+    t.keys.push_back(k);
+    t.vals.emplace_back();
+  }
+  for (uint32_t j = 0; j < nv; j++) {
+    if (vkey[j] >= nk || voff[j + 1] < voff[j]) return fail(c, A5X_E_ARG, "bad value %u", j);
+    t.vals[vkey[j]].emplace_back((const char*)vb + voff[j], (size_t)(voff[j + 1] - voff[j]));
+  }
+  c->table = std::move(t);
+  c->table_dirty = true;
+  return A5X_OK;
+}
+
+int a5x_clear_table(a5x_ctx* c) {
+  if (!c) return A5X_E_ARG;
+  c->table.clear();
+  c->table_dirty = true;
+  return A5X_OK;
+}
+
+int a5x_table_export(const a5x_ctx* c, uint32_t* n_keys, uint32_t* n_vals, uint64_t* key_bytes, uint64_t* val_bytes,
+                     uint8_t* ko, uint64_t* koff, uint8_t* vo, uint64_t* voff, uint32_t* vkey) {
+  if (!c) return A5X_E_ARG;
+  const Table& t = c->table;
+  uint64_t kbt = 0, vbt = 0, nv = 0;
+  if (koff) koff[0] = 0;
+  if (voff) voff[0] = 0;
+  for (uint32_t i = 0; i < t.keys.size(); i++) {
+    if (ko) memcpy(ko + kbt, t.keys[i].data(), t.keys[i].size());
+    kbt += t.keys[i].size();
+    if (koff) koff[i + 1] = kbt;
+    for (auto& v : t.vals[i]) {
+      if (vo) memcpy(vo + vbt, v.data(), v.size());
+      vbt += v.size();
+      if (vkey) vkey[nv] = i;
+      nv++;
+      if (voff) voff[nv] = vbt;
+    }
+  }
+  if (n_keys) *n_keys = (uint32_t)t.keys.size();
+  if (n_vals) *n_vals = (uint32_t)nv;
+  if (key_bytes) *key_bytes = kbt;
+  if (val_bytes) *val_bytes = vbt;
+  return A5X_OK;
+}
+
+int a5x_split_words(const uint8_t* data, size_t len, uint8_t* words_out, uint64_t* off_out, uint64_t off_cap,
+                    uint64_t* n_words) {
+  if ((!data && len) || !n_words) return A5X_E_ARG;
+  size_t pos = 0, wb = 0;
+  uint64_t n = 0;
+  const uint8_t* line;
+  size_t l;
+  if (off_out && off_cap) off_out[0] = 0;
+  while (a5x::gosem::scan_line(data, len, &pos, &line, &l) == 1) {  // ErrTooLong: silently stop
+    if (words_out) {
+      if (!off_out || n + 1 >= off_cap) return A5X_E_ARG;
+      memcpy(words_out + wb, line, l);
+    }
+    wb += l;
+    n++;
+    if (words_out) off_out[n] = wb;
+  }
+  *n_words = n;
+  return A5X_OK;
+}
+
+int a5x_keyspace_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn,
+                        int mx, uint64_t* d_cand_off, uint64_t* d_byte_off, uint64_t* tc, uint64_t* tb,
+                        void* stream) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!d_words || !d_woff))) return A5X_E_ARG;
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  Batch B;
+  if ((rc = run_keyspace(c, d_words, d_woff, nw, mn, mx, d_cand_off, d_byte_off, st, &B, false))) return rc;
+  if (tc) *tc = B.total_cands;
+  if (tb) *tb = B.total_bytes;
+  return A5X_OK;
+}
+
+int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn,
+                      int mx, uint64_t cand_begin, uint64_t cand_end, uint8_t* d_out, uint64_t out_cap,
+                      uint64_t* d_cand_off, uint64_t* d_byte_off, a5x_stats* stats, void* stream) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!d_words || !d_woff))) return A5X_E_ARG;
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  Batch B;
+  if ((rc = run_keyspace(c, d_words, d_woff, nw, mn, mx, d_cand_off, d_byte_off, st, &B, true))) return rc;
+  const uint64_t cb = std::min(cand_begin, B.total_cands);
+  const uint64_t ce = std::min(cand_end, B.total_cands);
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->words = nw;
+  }
+  if (ce <= cb) return A5X_OK;
+  A5xExpLaunch E = exp_launch(c, d_words, d_woff, nw, mn, mx, B);
+  E.cand_begin = cb;
+  E.cand_end = ce;
+  // byte range of [cb, ce)
+  uint64_t b0 = 0, b1 = B.total_bytes;
+  if (cb > 0 || ce < B.total_cands) {
+    if ((rc = grow(c, c->locate, 4))) return rc;
+    uint64_t hc[2] = {cb, ce};
+    HIPCHK(c, hipMemcpyAsync(c->locate.p, hc, 16, hipMemcpyHostToDevice, st));
+    HIPCHK(c, a5x_launch_locate(E, c->locate.p, 2, c->locate.p + 2, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_totals + 2, c->locate.p + 2, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+    b0 = c->h_totals[2];
+    b1 = c->h_totals[3];
+  }
+  if (stats) {
+    stats->candidates = ce - cb;
+    stats->bytes = b1 - b0;
+  }
+  if (b1 - b0 > out_cap || (!d_out && b1 > b0))
+    return fail(c, A5X_E_CAPACITY, "output needs %llu bytes, buffer has %llu", (unsigned long long)(b1 - b0),
+                (unsigned long long)out_cap);
+  E.out = d_out;
+  E.out_base = b0;
+  const uint64_t nchunks = (B.total_cands + c->chunk - 1) / c->chunk;
+  if ((rc = grow(c, c->chunk_w0, nchunks + 1)) || (rc = grow(c, c->chunk_big, nchunks + 1))) return rc;
+  E.chunk_w0 = c->chunk_w0.p;
+  E.chunk_big = c->chunk_big.p;
+  if (B.nbig) HIPCHK(c, hipMemsetAsync(c->chunk_big.p, 0, (nchunks + 1) * 4, st));
+  HIPCHK(c, a5x_launch_plan(B.cand_off, c->flags.p, nw, c->chunk, c->chunk_w0.p, B.nbig ? c->chunk_big.p : nullptr,
+                            st));
+  HIPCHK(c, hipEventRecord(c->ev[1], st));
+  HIPCHK(c, a5x_launch_expand(E, 0, st));
+  if (B.nbig) HIPCHK(c, a5x_launch_expand(E, 1, st));
+  HIPCHK(c, hipEventRecord(c->ev[2], st));
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+  if (stats) {
+    float a = 0, b = 0, t = 0;
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    HIPCHK(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[2]));
+    stats->ms_keyspace = a;
+    stats->ms_expand = b;
+    stats->ms_total = t;
+    stats->words_pass_b = B.nbig;
+    stats->expand_launches = B.nbig ? 2 : 1;
+    stats->pad = 0;
+  }
+  return A5X_OK;
+}
+
+int a5x_digest_device(a5x_ctx* c, const uint8_t* d_out, const uint64_t* d_byte_off, uint64_t out_base, uint64_t nw,
+                      uint64_t* d_digest, void* stream) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!d_byte_off || !d_digest))) return A5X_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (nw) HIPCHK(c, a5x_launch_digest(d_out, d_byte_off, out_base, nw, d_digest, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  return A5X_OK;
+}
+
+int a5x_keyspace(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
+                 uint64_t* out_count, uint64_t* out_bytes) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!words || !woff))) return A5X_E_ARG;
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t wbytes = nw ? woff[nw] : 0;
+  if ((rc = grow(c, c->s_words, wbytes + 16)) || (rc = grow(c, c->s_woff, nw + 1))) return rc;
+  if (wbytes) HIPCHK(c, hipMemcpyAsync(c->s_words.p, words, wbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->s_woff.p, woff, (nw + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  Batch B;
+  if ((rc = run_keyspace(c, c->s_words.p, c->s_woff.p, nw, mn, mx, nullptr, nullptr, c->stream, &B, false)))
+    return rc;
+  if (out_count && nw) HIPCHK(c, hipMemcpyAsync(out_count, c->count.p, nw * 8, hipMemcpyDeviceToHost, c->stream));
+  if (out_bytes && nw) HIPCHK(c, hipMemcpyAsync(out_bytes, c->bytes.p, nw * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return A5X_OK;
+}
+
+int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
+               a5x_sink_fn sink, void* user, a5x_stats* stats) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || !sink || (nw && (!words || !woff))) return A5X_E_ARG;
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t wbytes = nw ? woff[nw] : 0;
+  if ((rc = grow(c, c->s_words, wbytes + 16)) || (rc = grow(c, c->s_woff, nw + 1))) return rc;
+  if (wbytes) HIPCHK(c, hipMemcpyAsync(c->s_words.p, words, wbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->s_woff.p, woff, (nw + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  uint64_t tc = 0, tb = 0;
+  if ((rc = a5x_keyspace_device(c, c->s_words.p, c->s_woff.p, nw, mode, mn, mx, nullptr, nullptr, &tc, &tb,
+                                c->stream)))
+    return rc;
+  // stream the output through a bounded device buffer, in candidate ranges
+  size_t cap = (size_t)1 << 28;
+  if (const char* e = getenv("A5X_HOST_CHUNK_BYTES")) cap = std::max<size_t>(4096, strtoull(e, nullptr, 10));
+  if ((rc = grow(c, c->s_out, cap))) return rc;
+  if (c->h_out_cap < cap) {
+    if (c->h_out) (void)hipHostFree(c->h_out);
+    c->h_out = nullptr;
+    HIPCHK(c, hipHostMalloc((void**)&c->h_out, cap, 0));
+    c->h_out_cap = cap;
+  }
+  a5x_stats total;
+  memset(&total, 0, sizeof total);
+  total.words = nw;
+  uint64_t g = 0, step = std::max<uint64_t>(1, cap / 32);
+  while (g < tc) {
+    const uint64_t ge = std::min(tc, g + step);
+    a5x_stats s;
+    rc = a5x_expand_device(c, c->s_words.p, c->s_woff.p, nw, mode, mn, mx, g, ge, c->s_out.p, cap, nullptr,
+                           nullptr, &s, c->stream);
+    if (rc == A5X_E_CAPACITY) {
+      if (ge - g == 1) return rc;  // one candidate larger than the buffer
+      step = std::max<uint64_t>(1, (ge - g) / 2);
+      continue;
+    }
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_out, c->s_out.p, s.bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (s.bytes && sink(user, c->h_out, s.bytes)) return fail(c, A5X_E_SINK, "sink returned non-zero");
+    total.candidates += s.candidates;
+    total.bytes += s.bytes;
+    total.ms_keyspace += s.ms_keyspace;
+    total.ms_expand += s.ms_expand;
+    total.ms_total += s.ms_total;
+    g = ge;
+    if (s.bytes < cap / 4) step *= 2;  // adapt the range to the buffer
+  }
+  if (stats) *stats = total;
+  return A5X_OK;
+}
+
+int a5x_partition(const uint64_t* prefix, uint64_t n, uint32_t parts, uint64_t* split) {
+  if (!prefix || !split || parts == 0) return A5X_E_ARG;
+  const uint64_t total = prefix[n];
+  split[0] = 0;
+  for (uint32_t r = 1; r < parts; r++) {
+    const unsigned __int128 target = (unsigned __int128)total * r / parts;
+    // first word i whose start offset >= target
+    uint64_t lo = split[r - 1], hi = n;
+    while (lo < hi) {
+      const uint64_t mid = lo + (hi - lo) / 2;
+      if ((unsigned __int128)prefix[mid] < target) lo = mid + 1; else hi = mid;
+    }
+    split[r] = lo;
+  }
+  split[parts] = n;
+  return A5X_OK;
+}
+
+int a5x_dev_alloc(a5x_ctx* c, void** p, size_t bytes) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || !p) return A5X_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+  if (e != hipSuccess) return fail(c, A5X_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  return A5X_OK;
+}
+int a5x_dev_free(a5x_ctx* c, void* p) {
+  if (!c) return A5X_E_ARG;
+  if (p) HIPCHK(c, hipFree(p));
+  return A5X_OK;
+}
+int a5x_memcpy_h2d(a5x_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c) return A5X_E_ARG;
+  HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return A5X_OK;
+}
+int a5x_memcpy_d2h(a5x_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c) return A5X_E_ARG;
+  HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return A5X_OK;
+}
+int a5x_synchronize(a5x_ctx* c) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c) return A5X_E_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return A5X_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,1151 @@
+// a5x_kernels.hip -- CDNA4 (gfx950) kernels for hashcat -a 5 table expansion.
+//
+// Hot path = processWord (/root/reference/main.go:168-205): for every word, every
+// set of non-overlapping key matches (byte positions of the ORIGINAL word) with
+// max(1,min) <= |set| <= max, times every choice of one value per match, spliced
+// in and written as "cand\n" (main.go:66).  The candidate multiset per word is the
+// contract (the reference's output order is nondeterministic, main.go:77).
+//
+// Pipeline (one HIP stream, see a5x_host.cpp):
+//   k_keyspace_thread  one lane per word: matching + closed-form mixed-radix
+//                      count/bytes for words whose matches are disjoint single
+//                      keys (SURVEY 8(a) fast path); everything else deferred.
+//   k_keyspace_wave    one wave per deferred word: interval DP G[p][c] (counts)
+//                      and H[p][c] (bytes) in LDS, lanes over the count column c.
+//   k_scan_*           exclusive scan of (count, bytes) -> global candidate and
+//                      byte offsets per word.
+//   k_plan             chunk -> first word map (chunks of CH candidates).
+//   k_expand<A|B>      one wave per chunk: per-word setup in LDS, each lane unranks
+//                      one candidate (mixed radix or DP walk), wave scan of
+//                      lengths, bytes OR-ed into a per-wave LDS ring at their
+//                      final offsets, complete 16-B blocks streamed to HBM with
+//                      global_store_dwordx4 (1 KiB per wave instruction).
+//   k_digest           per-word order-independent multiset digest of the output
+//                      (verification only).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "a5x_format.h"
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef int64_t i64;
+
+#define WAVE_SYNC()                                          \
+  do {                                                       \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+    __builtin_amdgcn_wave_barrier();                         \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+  } while (0)
+
+enum : u32 {
+  A5X_DERR_TABLE = 1u << 0,   // table blob does not fit LDS / bad magic
+  A5X_DERR_OVF = 1u << 1,     // u64 overflow in a keyspace
+  A5X_DERR_BIG = 1u << 2,     // a word beyond pass-B limits has candidates
+  A5X_DERR_STATE = 1u << 3,   // internal consistency (keyspace vs expand)
+  A5X_DERR_SCANOVF = 1u << 4, // prefix sum overflow
+};
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u32 lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ u64 shfl_u64(u64 v, int src) {
+  u32 lo = __shfl((int)(u32)v, src), hi = __shfl((int)(u32)(v >> 32), src);
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 shfl_up_u64(u64 v, int d) {
+  u32 lo = __shfl_up((int)(u32)v, d), hi = __shfl_up((int)(u32)(v >> 32), d);
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 shfl_xor_u64(u64 v, int m) {
+  u32 lo = __shfl_xor((int)(u32)v, m), hi = __shfl_xor((int)(u32)(v >> 32), m);
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u32 wave_incl_scan_u32(u32 x) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    u32 y = __shfl_up((int)x, d);
+    if ((int)lane_id() >= d) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ u64 wave_sum_u64(u64 x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += shfl_xor_u64(x, m);
+  return x;
+}
+__device__ __forceinline__ i64 wave_sum_i64(i64 x) { return (i64)wave_sum_u64((u64)x); }
+__device__ __forceinline__ u32 wave_max_u32(u32 x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x = max(x, (u32)__shfl_xor((int)x, m));
+  return x;
+}
+__device__ __forceinline__ u32 wave_or_u32(u32 x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x |= (u32)__shfl_xor((int)x, m);
+  return x;
+}
+__device__ __forceinline__ u32 uniform(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ u64 uniform64(u64 x) {
+  return ((u64)__builtin_amdgcn_readfirstlane((u32)(x >> 32)) << 32) | __builtin_amdgcn_readfirstlane((u32)x);
+}
+
+// a*b with overflow flag
+__device__ __forceinline__ u64 mul_ovf(u64 a, u64 b, bool& ovf) {
+  u64 r;
+  ovf |= __builtin_mul_overflow(a, b, &r);
+  return r;
+}
+__device__ __forceinline__ u64 add_ovf(u64 a, u64 b, bool& ovf) {
+  u64 r = a + b;
+  ovf |= r < a;
+  return r;
+}
+
+__device__ __forceinline__ u32 keep_bytes(u32 v, u32 n) { return n >= 4 ? v : (v & ((1u << (8 * n)) - 1u)); }
+
+// unaligned 4-byte read from LDS (base must have 8 readable bytes past off)
+__device__ __forceinline__ u32 lds_ld4(const uint8_t* base, u32 off) {
+  const u32* p = (const u32*)(base + (off & ~3u));
+  u32 lo = p[0], hi = p[1];
+  return __builtin_amdgcn_alignbyte(hi, lo, off & 3u);
+}
+
+// ---------------------------------------------------------------------------
+// the device table (see a5x_format.h), viewed in LDS
+// ---------------------------------------------------------------------------
+struct Tab {
+  const A5xTableHdr* hdr;
+  const uint16_t* bucket;
+  const A5xKey* keys;
+  const A5xChoice* ch;
+  const uint8_t* blob;
+};
+
+__device__ __forceinline__ Tab tab_view(const uint8_t* base) {
+  Tab t;
+  t.hdr = (const A5xTableHdr*)base;
+  t.bucket = (const uint16_t*)(base + t.hdr->off_bucket);
+  t.keys = (const A5xKey*)(base + t.hdr->off_keys);
+  t.ch = (const A5xChoice*)(base + t.hdr->off_choices);
+  t.blob = base + t.hdr->off_blob;
+  return t;
+}
+
+// whole workgroup copies the table blob (multiple of 16 B) into LDS
+__device__ __forceinline__ void load_table(uint8_t* dst, const uint8_t* src, u32 bytes) {
+  const uint4* s = (const uint4*)src;
+  uint4* d = (uint4*)dst;
+  for (u32 i = threadIdx.x; i < bytes / 16; i += blockDim.x) d[i] = s[i];
+}
+
+// does key k match the word (global bytes) at p?  caller checked p+klen <= L
+__device__ __forceinline__ bool key_match_global(const uint8_t* wp, u32 p, const A5xKey& key, const Tab& T) {
+  const A5xChoice c0 = T.ch[key.choice_base];
+  u32 kl = key.klen;
+  for (u32 i = 1; i < kl; i++) {  // byte 0 matched by the bucket
+    u32 kb = i < 4 ? ((c0.first4 >> (8 * i)) & 255u) : T.blob[c0.blob_off + i];
+    if (wp[p + i] != kb) return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Keyspace, one lane per word (radix fast path; SURVEY 8(a) closed form)
+// ---------------------------------------------------------------------------
+struct KsArgs {
+  const uint8_t* table;
+  u32 table_bytes;
+  const uint8_t* words;
+  const u64* woff;
+  u64 nw;
+  int mn, mx;
+  u64* count;
+  u64* bytes;
+  u32* flags;
+  u32* defer_list;
+  u32* defer_n;
+  u32* nbig;
+  u32* err;
+};
+
+__global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < a.nw; w += stride) {
+    const u64 s = a.woff[w], e = a.woff[w + 1];
+    const u64 L64 = e - s;
+    if (a.mx < 1 || L64 == 0) {  // processWord emits nothing
+      a.count[w] = 0; a.bytes[w] = 0; a.flags[w] = A5X_WF_RADIX;
+      continue;
+    }
+    if (L64 > A5X_LMAX_A) {  // long words: the wave kernel (loops over positions)
+      a.flags[w] = A5X_WF_DEFER;
+      a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
+      continue;
+    }
+    const u32 L = (u32)L64;
+    const uint8_t* wp = a.words + s;
+    u32 nmatch = 0, last_end = 0, maxl = L + 1;
+    bool conflict = false, bin = true, ovf = false;
+    u64 P = 1, Dp = 0, Dn = 0;
+    for (u32 p = 0; p < L; p++) {
+      const u32 b = wp[p];
+      const u32 ks = T.bucket[b], ke = T.bucket[b + 1];
+      for (u32 k = ks; k < ke; k++) {
+        const A5xKey key = T.keys[k];
+        if (p + key.klen > L || !key_match_global(wp, p, key, T)) continue;
+        nmatch++;
+        if (p < last_end) conflict = true;  // overlaps a previous match or 2nd match at p
+        last_end = max(last_end, p + (u32)key.klen);
+        const u64 R = (u64)key.nvals + 1;
+        // sum over this slot's values of (|v| - klen), split by sign
+        u64 spos = 0, sneg = 0;
+        for (u32 v = 0; v < key.nvals; v++) {
+          const int d = (int)T.ch[key.choice_base + 1 + v].len - (int)key.klen;
+          if (d > 0) spos += (u64)d; else sneg += (u64)(-d);
+        }
+        Dp = add_ovf(mul_ovf(Dp, R, ovf), mul_ovf(P, spos, ovf), ovf);
+        Dn = add_ovf(mul_ovf(Dn, R, ovf), mul_ovf(P, sneg, ovf), ovf);
+        P = mul_ovf(P, R, ovf);
+        if (key.nvals != 1) bin = false;
+        if (key.maxdelta > 0) maxl += (u32)key.maxdelta;
+      }
+    }
+    const bool freew = (a.mn <= 1) && ((i64)nmatch <= (i64)a.mx);
+    if (nmatch == 0) {
+      a.count[w] = 0; a.bytes[w] = 0; a.flags[w] = A5X_WF_RADIX;
+    } else if (!conflict && freew && !ovf && P <= (1ull << 32) && maxl <= A5X_RING_A - 16) {
+      bool o2 = false;
+      const u64 cnt = P - 1;
+      u64 byt = add_ovf(mul_ovf(cnt, (u64)L + 1, o2), Dp, o2);
+      if (byt < Dn) o2 = true;
+      byt -= Dn;
+      if (o2) {
+        a.flags[w] = A5X_WF_ERR_OVF; a.count[w] = 0; a.bytes[w] = 0;
+        atomicOr(a.err, A5X_DERR_OVF);
+      } else {
+        a.count[w] = cnt; a.bytes[w] = byt;
+        a.flags[w] = A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u);
+      }
+    } else {
+      a.flags[w] = A5X_WF_DEFER;
+      a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-level word setup shared by k_keyspace_wave and k_expand
+// ---------------------------------------------------------------------------
+struct Slot {            // radix slot (one disjoint single-key match)
+  uint16_t pos, klen;
+  u32 R;                 // nvals + 1
+  u32 choice_base;       // choices[cb] = key ("keep"), [cb + d] = value d-1
+  u32 magic, shift;      // branch-free u32 division by R (libdivide form)
+  int delta1;            // |value 0| - klen (radix-2 words)
+  u64 Q;                 // product of R over earlier slots (digit weight)
+};
+
+// Key matches are kept per "event" = a position where at least one key matches.
+// Between events every position is a forced keep, so the DP runs over events
+// only: (events+1) x W entries instead of (L+1) x W.
+template <int LMAX, int MLMAX, int DPENT>
+struct WaveLds {
+  static constexpr int SMAX = LMAX < MLMAX ? LMAX : MLMAX;
+  uint8_t wbuf[LMAX + 16];
+  uint16_t evidx[LMAX + 2];    // number of events at positions < p, p in [0, L]
+  uint16_t evpos[SMAX + 1];    // event -> position; evpos[m] = L
+  u32 evm[SMAX];               // event -> (mstart << 8) | match count
+  uint16_t mlist[MLMAX];       // matching key ids, grouped by event
+  union {
+    Slot slots[SMAX];
+    struct { u64 G[DPENT]; u64 H[DPENT]; } dp;
+  };
+};
+
+struct WordInfo {
+  u32 L, nmatch, nslots;
+  u32 cls;         // A5X_WF_RADIX [| A5X_WF_BIN] or A5X_WF_GENERAL; 0 = no candidates
+  u32 fits;        // 1: the word's setup fit this pass's LDS budget
+  u32 freew, W, Cc;
+  int lo;
+  u32 maxlen;      // upper bound on (candidate length + 1)
+  int udelta;      // radix-2: common |v|-klen of all slots, or INT_MIN
+  u64 count, bytes;
+  u32 ovf;
+  u32 nev;         // events (positions with a key match)
+  u32 why;         // diagnostics when !fits: 1 long, 2 matches, 3 columns, 4 DP size
+};
+
+__device__ __forceinline__ void divmagic(u32 d, u32& magic, u32& shift) {
+  // libdivide u32 branchfree: l = ceil(log2 d), M = floor(2^32 (2^l - d) / d) + 1
+  u32 l = 32 - __clz(d - 1);
+  u64 m = (((u64)1 << 32) * (((u64)1 << l) - d)) / d + 1;
+  magic = (u32)m;
+  shift = l - 1;
+}
+__device__ __forceinline__ u32 fastdiv(u32 n, u32 magic, u32 shift) {
+  u32 q = __umulhi(n, magic);
+  return (q + ((n - q) >> 1)) >> shift;
+}
+
+// One wave sets up word w: bytes -> wbuf, key matches grouped by event, class,
+// and either radix slots or the event DP tables.  Returned fields are uniform.
+template <int LMAX, int MLMAX, int DPENT>
+__device__ WordInfo wave_setup(WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, const uint8_t* words,
+                               const u64* woff, u64 w, int mn, int mx) {
+  typedef WaveLds<LMAX, MLMAX, DPENT> LdsT;
+  WordInfo I;
+  const u32 lane = lane_id();
+  const u64 s = woff[w];
+  const u64 L64 = woff[w + 1] - s;
+  I.L = (u32)min(L64, (u64)0xffffffffu);
+  I.cls = 0; I.fits = 1; I.nslots = 0; I.count = 0; I.bytes = 0; I.ovf = 0; I.nev = 0;
+  I.maxlen = 0; I.udelta = INT32_MIN; I.freew = 1; I.W = 2; I.Cc = 1; I.lo = 1; I.nmatch = 0; I.why = 0;
+  if (mx < 1 || L64 == 0) return I;
+  const u32 L = I.L;
+  const bool stored = L64 <= (u64)LMAX;
+  const uint8_t* wp = words + s;
+  if (stored) {
+    for (u32 p = lane; p < L + 16 && p < LMAX + 16; p += 64) S.wbuf[p] = p < L ? wp[p] : 0;
+  }
+  WAVE_SYNC();
+  // ---- matches: positions in chunks of 64 lanes ----
+  u32 base = 0, evbase = 0, prev_end = 0;  // running matches / events / max match end
+  bool conflict = false, multi = false, room = true;
+  u32 maxadd = 0;
+  for (u32 p0 = 0; p0 < L; p0 += 64) {
+    const u32 p = p0 + lane;
+    u32 nm = 0, kmax = 0, dmax = 0;
+    if (p < L) {
+      const u32 b = stored ? S.wbuf[p] : wp[p];
+      const u32 ks = T.bucket[b], ke = T.bucket[b + 1];
+      for (u32 k = ks; k < ke; k++) {
+        const A5xKey key = T.keys[k];
+        if (p + key.klen > L || !key_match_global(wp, p, key, T)) continue;
+        nm++;
+        kmax = max(kmax, (u32)key.klen);
+        if (key.maxdelta > 0) dmax = max(dmax, (u32)key.maxdelta);
+      }
+    }
+    // overlap: a match at p conflicts if an earlier match (any position < p) ends after p
+    const u32 endp = nm ? p + kmax : 0;
+    u32 pre = endp;  // inclusive max-scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      u32 y = __shfl_up((int)pre, d);
+      if ((int)lane >= d) pre = max(pre, y);
+    }
+    u32 before = __shfl_up((int)pre, 1);
+    if (lane == 0) before = 0;
+    before = max(before, prev_end);
+    if (nm && before > p) conflict = true;
+    if (nm > 1) multi = true;
+    const u32 incl = wave_incl_scan_u32(nm);
+    const u32 mstart = base + incl - nm;
+    const u64 bal = __ballot(nm > 0);
+    const u32 ev = evbase + (u32)__popcll(bal & ((1ull << lane) - 1ull));
+    const u32 nev_after = evbase + (u32)__popcll(bal);
+    const u32 nm_after = base + __shfl((int)incl, 63);
+    if (stored && nev_after <= (u32)LdsT::SMAX && nm_after <= (u32)MLMAX) {
+      if (p < L) S.evidx[p] = (uint16_t)ev;
+      if (nm) {
+        S.evpos[ev] = (uint16_t)p;
+        S.evm[ev] = (mstart << 8) | min(nm, 255u);
+        const u32 b = S.wbuf[p];
+        const u32 ks = T.bucket[b], ke = T.bucket[b + 1];
+        u32 j = 0;
+        for (u32 k = ks; k < ke; k++) {
+          const A5xKey key = T.keys[k];
+          if (p + key.klen > L || !key_match_global(wp, p, key, T)) continue;
+          S.mlist[mstart + j++] = (uint16_t)k;
+        }
+      }
+    } else {
+      room = false;
+    }
+    maxadd += (u32)wave_sum_u64(dmax);
+    base = nm_after;
+    evbase = nev_after;
+    prev_end = max(prev_end, (u32)__shfl((int)pre, 63));
+  }
+  conflict = wave_or_u32(conflict) != 0;
+  multi = wave_or_u32(multi) != 0;
+  I.nmatch = base;
+  I.nev = evbase;
+  I.maxlen = L + 1 + maxadd;
+  if (base == 0) return I;                                  // no candidates
+  I.freew = (mn <= 1) && ((i64)base <= (i64)mx);
+  I.lo = mn <= 1 ? 1 : mn;
+  if (!stored || !room) { I.fits = 0; I.why = stored ? 2 : 1; I.cls = A5X_WF_GENERAL; return I; }
+  if (lane == 0) { S.evidx[L] = (uint16_t)evbase; S.evpos[evbase] = (uint16_t)L; }
+  WAVE_SYNC();
+  const u32 m = evbase;
+
+  if (!conflict && !multi && I.freew) {
+    // ---- radix slots: one per event, digit weights Q ----
+    for (u32 i = lane; i < m; i += 64) {
+      const A5xKey key = T.keys[S.mlist[S.evm[i] >> 8]];
+      Slot sl;
+      sl.pos = S.evpos[i]; sl.klen = key.klen; sl.R = (u32)key.nvals + 1u;
+      sl.choice_base = key.choice_base;
+      divmagic(sl.R, sl.magic, sl.shift);
+      sl.delta1 = (int)T.ch[key.choice_base + 1].len - (int)key.klen;
+      sl.Q = 0;
+      S.slots[i] = sl;
+    }
+    I.nslots = m;
+    WAVE_SYNC();
+    // digit weights (serial; nslots is small) and P
+    u64 P = 1;
+    bool ovf = false, bin = true;
+    int ud = S.slots[0].delta1;
+    for (u32 i = 0; i < m; i++) {
+      const u32 R = S.slots[i].R;
+      if (lane == 0) S.slots[i].Q = P;
+      P = mul_ovf(P, R, ovf);
+      if (R != 2) bin = false;
+      if (S.slots[i].delta1 != ud) ud = INT32_MIN;
+    }
+    WAVE_SYNC();
+    if (!ovf && P <= (1ull << 32)) {
+      // bytes = (P-1)(L+1) + sum_slots (P/R) sum_v delta   (lanes over slots)
+      i64 part = 0;
+      for (u32 i = lane; i < m; i += 64) {
+        const Slot sl = S.slots[i];
+        i64 sd = 0;
+        for (u32 v = 1; v < sl.R; v++) sd += (i64)T.ch[sl.choice_base + v].len - (i64)sl.klen;
+        part += (i64)(P / sl.R) * sd;
+      }
+      const i64 dsum = wave_sum_i64(part);
+      I.cls = A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u);
+      I.count = P - 1;
+      I.bytes = (P - 1) * (u64)(L + 1) + (u64)dsum;
+      I.udelta = bin ? ud : INT32_MIN;
+      return I;
+    }
+    I.nslots = 0;
+    // overflowing radix words go through the DP (same counts, u64 walk)
+  }
+  // ---- general: DP over events with a count window ----
+  // G[e][c]: completions from event e having made c substitutions (c clamped to 1 in
+  // the free window); H[e][c]: their bytes from position evpos[e] on, newline incl.
+  I.cls = A5X_WF_GENERAL;
+  u32 C = I.freew ? 1u : (u32)min((i64)mx, (i64)base);
+  I.Cc = C;
+  I.W = C + 1;
+  if (I.W > 64 || (u64)(m + 1) * I.W > (u64)DPENT) { I.fits = 0; I.why = I.W > 64 ? 3 : 4; return I; }
+  const u32 W = I.W, c = lane;
+  bool ovf = false;
+  for (int e = (int)m; e >= 0; --e) {
+    if (c < W) {
+      u64 g, h;
+      if (e == (int)m) {
+        g = I.freew ? (c == 1 ? 1u : 0u) : ((int)c >= I.lo ? 1u : 0u);
+        h = g;
+      } else {
+        const u32 q = S.evpos[e], qn = S.evpos[e + 1];
+        g = S.dp.G[(e + 1) * W + c];
+        h = add_ovf(S.dp.H[(e + 1) * W + c], mul_ovf(g, qn - q, ovf), ovf);
+        const u32 em = S.evm[e], ms = em >> 8, mc = em & 255u;
+        const u32 nc = I.freew ? 1u : c + 1u;
+        if (nc <= C) {
+          for (u32 j = 0; j < mc; j++) {
+            const A5xKey key = T.keys[S.mlist[ms + j]];
+            const u32 p2 = q + key.klen, e2 = S.evidx[p2], lit = S.evpos[e2] - p2;
+            const u64 gs = S.dp.G[e2 * W + nc];
+            const u64 hs = S.dp.H[e2 * W + nc];
+            g = add_ovf(g, mul_ovf(gs, key.nvals, ovf), ovf);
+            const u64 per = (u64)key.sumlen + (u64)key.nvals * lit;
+            h = add_ovf(h, add_ovf(mul_ovf(hs, key.nvals, ovf), mul_ovf(gs, per, ovf), ovf), ovf);
+          }
+        }
+      }
+      S.dp.G[e * W + c] = g;
+      S.dp.H[e * W + c] = h;
+    }
+    WAVE_SYNC();
+  }
+  I.ovf = wave_or_u32(ovf) != 0;
+  I.count = S.dp.G[0];
+  bool o2 = false;
+  I.bytes = add_ovf(S.dp.H[0], mul_ovf(S.dp.G[0], S.evpos[0], o2), o2);  // + literal prefix
+  if (o2) I.ovf = 1;
+  return I;
+}
+
+// ---------------------------------------------------------------------------
+// Keyspace for deferred words: one wave per word (pass-B budget)
+// ---------------------------------------------------------------------------
+typedef WaveLds<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B> LdsB;
+typedef WaveLds<A5X_LMAX_A, A5X_MLMAX_A, A5X_DPENT_A> LdsA;
+
+__global__ void __launch_bounds__(64) k_keyspace_wave(KsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  LdsB& S = *(LdsB*)(smem + ((a.table_bytes + 15u) & ~15u));
+  const u32 n = *a.defer_n;
+  for (u32 i = blockIdx.x; i < n; i += gridDim.x) {
+    const u32 w = a.defer_list[i];
+    WordInfo I = wave_setup<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>(S, T, a.words, a.woff, w, a.mn, a.mx);
+    if (lane_id() == 0) {
+      u32 f = I.cls ? I.cls : (u32)A5X_WF_RADIX;
+      // would pass A (smaller LDS budget) handle it?
+      bool fitsA = I.L <= A5X_LMAX_A && I.nmatch <= A5X_MLMAX_A && I.maxlen <= A5X_RING_A - 16 &&
+                   (I.cls != A5X_WF_GENERAL || (u64)(I.nev + 1) * I.W <= A5X_DPENT_A);
+      if (I.cls && !fitsA) { f |= A5X_WF_BIG; atomicAdd(a.nbig, 1u); }
+      if (I.cls && (!I.fits || I.maxlen > A5X_RING_B - 16)) {
+        f |= A5X_WF_ERR_BIG | ((I.fits ? 5u : I.why) << 16) | (min(I.W, 255u) << 24);
+        atomicOr(a.err, A5X_DERR_BIG);
+      }
+      if (I.ovf) { f |= A5X_WF_ERR_OVF; atomicOr(a.err, A5X_DERR_OVF); }
+      const bool bad = (f & (A5X_WF_ERR_BIG | A5X_WF_ERR_OVF)) != 0;
+      a.count[w] = bad ? 0 : I.count;
+      a.bytes[w] = bad ? 0 : I.bytes;
+      a.flags[w] = f;
+    }
+    WAVE_SYNC();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Exclusive scan of (count, bytes) pairs: n -> n+1 entries (last = totals)
+// ---------------------------------------------------------------------------
+#define SCAN_ITEMS 8
+#define SCAN_BLOCK 256
+#define SCAN_TILE (SCAN_ITEMS * SCAN_BLOCK)
+
+__device__ __forceinline__ void block_excl_scan2(u64& a, u64& b, u64& ta, u64& tb, u32* errp) {
+  __shared__ u64 sa[SCAN_BLOCK / 64], sb[SCAN_BLOCK / 64];
+  const u32 lane = lane_id(), wv = threadIdx.x / 64;
+  u64 ia = a, ib = b;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    u64 ya = shfl_up_u64(ia, d), yb = shfl_up_u64(ib, d);
+    if ((int)lane >= d) { ia += ya; ib += yb; }
+  }
+  if (lane == 63) { sa[wv] = ia; sb[wv] = ib; }
+  __syncthreads();
+  u64 oa = 0, ob = 0;
+  for (u32 k = 0; k < wv; k++) { oa += sa[k]; ob += sb[k]; }
+  ta = 0; tb = 0;
+  for (u32 k = 0; k < SCAN_BLOCK / 64; k++) { ta += sa[k]; tb += sb[k]; }
+  a = oa + ia - a;
+  b = ob + ib - b;
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(SCAN_BLOCK) k_scan_reduce(const u64* ca, const u64* cb, u64 n, u64* sa, u64* sb,
+                                                             u32* err) {
+  const u64 base = (u64)blockIdx.x * SCAN_TILE;
+  u64 a = 0, b = 0;
+  for (u32 j = 0; j < SCAN_ITEMS; j++) {
+    const u64 i = base + (u64)j * SCAN_BLOCK + threadIdx.x;
+    if (i < n) {
+      const u64 x = ca[i], y = cb[i];
+      a += x; b += y;
+      if (a < x || b < y) atomicOr(err, A5X_DERR_SCANOVF);
+    }
+  }
+  u64 ta, tb;
+  block_excl_scan2(a, b, ta, tb, err);
+  if (threadIdx.x == 0) { sa[blockIdx.x] = ta; sb[blockIdx.x] = tb; }
+}
+
+// out[i] = exclusive prefix (+ block offset); out[n] = total when this block is last
+__global__ void __launch_bounds__(SCAN_BLOCK) k_scan_down(const u64* ca, const u64* cb, u64 n, const u64* oa,
+                                                           const u64* ob, u64* outa, u64* outb, u32* err) {
+  __shared__ u64 la[SCAN_TILE], lb[SCAN_TILE];
+  const u64 base = (u64)blockIdx.x * SCAN_TILE;
+  for (u32 j = 0; j < SCAN_ITEMS; j++) {
+    const u32 t = j * SCAN_BLOCK + threadIdx.x;
+    const u64 i = base + t;
+    la[t] = i < n ? ca[i] : 0;
+    lb[t] = i < n ? cb[i] : 0;
+  }
+  __syncthreads();
+  u64 a = 0, b = 0;
+  for (u32 j = 0; j < SCAN_ITEMS; j++) { a += la[threadIdx.x * SCAN_ITEMS + j]; b += lb[threadIdx.x * SCAN_ITEMS + j]; }
+  u64 ta, tb;
+  u64 ea = a, eb = b;
+  block_excl_scan2(ea, eb, ta, tb, err);
+  u64 ra = (oa ? oa[blockIdx.x] : 0) + ea, rb = (ob ? ob[blockIdx.x] : 0) + eb;
+  for (u32 j = 0; j < SCAN_ITEMS; j++) {
+    const u32 t = threadIdx.x * SCAN_ITEMS + j;
+    const u64 x = la[t], y = lb[t];
+    la[t] = ra; lb[t] = rb;
+    ra += x; rb += y;
+  }
+  // totals: the thread holding element n-1 (tile-local) ends with the inclusive sum
+  // (items past n are zero-padded); read before anything is overwritten in place.
+  const bool last_blk = base + SCAN_TILE >= n;
+  if (last_blk && threadIdx.x == (u32)((n - 1 - base) / SCAN_ITEMS)) {
+    outa[n] = ra; outb[n] = rb;
+  }
+  __syncthreads();
+  for (u32 j = 0; j < SCAN_ITEMS; j++) {
+    const u32 t = j * SCAN_BLOCK + threadIdx.x;
+    const u64 i = base + t;
+    if (i < n) { outa[i] = la[t]; outb[i] = lb[t]; }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Chunk planner: chunk c covers global candidates [c*CH, (c+1)*CH)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_plan(const u64* cand_off, const u32* flags, u64 nw, u64 CH, u32* chunk_w0,
+                                              u32* chunk_big) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+    const u64 a = cand_off[w], b = cand_off[w + 1];
+    if (b <= a) continue;
+    for (u64 c = (a + CH - 1) / CH; c * CH < b; c++) chunk_w0[c] = (u32)w;
+    if (flags[w] & A5X_WF_BIG)
+      for (u64 c = a / CH; c * CH < b; c++) chunk_big[c] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Expansion
+// ---------------------------------------------------------------------------
+struct ExpArgs {
+  const uint8_t* table;
+  u32 table_bytes;
+  const uint8_t* words;
+  const u64* woff;
+  u64 nw;
+  const u64* cand_off;   // n+1, exclusive prefix of counts
+  const u64* byte_off;   // n+1, exclusive prefix of bytes
+  const u32* flags;
+  const u32* chunk_w0;
+  const u32* chunk_big;
+  u64 cand_begin, cand_end;  // global candidate range of this call
+  u64 CH;
+  uint8_t* out;
+  u64 out_base;          // byte_off value that maps to out[0]
+  int mn, mx;
+  u32* err;
+};
+
+// Per-lane byte emitter: bytes are OR-ed into an all-zero LDS ring at their
+// final positions (ring index = byte offset relative to the run base).
+struct Emit {
+  u64 acc;
+  u32 n;   // pending bytes in acc
+  u32 dw;  // dword index (relative to run base) of acc's low dword
+};
+
+template <u32 RING>
+__device__ __forceinline__ void em_put(Emit& e, u32* ring, u32 piece, u32 plen) {
+  e.acc |= (u64)piece << (8u * e.n);
+  e.n += plen;
+  if (e.n >= 4) {
+    atomicOr(&ring[e.dw & (RING / 4 - 1)], (u32)e.acc);
+    e.dw++;
+    e.acc >>= 32;
+    e.n -= 4;
+  }
+}
+template <u32 RING>
+__device__ __forceinline__ void em_bytes(Emit& e, u32* ring, const uint8_t* src, u32 off, u32 len) {
+  for (u32 k = 0; k < len; k += 4) {
+    const u32 m = min(4u, len - k);
+    em_put<RING>(e, ring, keep_bytes(lds_ld4(src, off + k), m), m);
+  }
+}
+template <u32 RING>
+__device__ __forceinline__ void em_choice(Emit& e, u32* ring, const Tab& T, u32 ci) {
+  const A5xChoice c = T.ch[ci];
+  if (c.len <= 4) em_put<RING>(e, ring, c.first4, c.len);
+  else em_bytes<RING>(e, ring, T.blob, c.blob_off, c.len);
+}
+template <u32 RING>
+__device__ __forceinline__ void em_finish(Emit& e, u32* ring) {
+  if (e.n) atomicOr(&ring[e.dw & (RING / 4 - 1)], (u32)e.acc);
+}
+
+// Global byte range of one "run" (contiguous output) staged through the ring.
+struct Run {
+  u64 base;     // 16-aligned global byte position (relative to out_base) of ring origin
+  u64 lo;       // first byte owned by this wave
+  u64 pos;      // next byte to be produced
+  u64 flushed;  // bytes < flushed are in HBM (16-aligned, >= base)
+  bool open;
+};
+
+template <u32 RING>
+__device__ __forceinline__ void store_block(uint8_t* out, u64 X, uint4 v, u64 lo, u64 hi) {
+  // block [X, X+16) restricted to bytes [lo, hi)
+  if (X >= lo && X + 16 <= hi) {
+    *(uint4*)(out + X) = v;
+  } else {
+    const u32 wv[4] = {v.x, v.y, v.z, v.w};
+    for (u32 b = 0; b < 16; b++) {
+      const u64 Y = X + b;
+      if (Y >= lo && Y < hi) out[Y] = (uint8_t)(wv[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+}
+
+// stream complete blocks [flushed, upto) (upto 16-aligned) and zero them in the ring
+template <u32 RING>
+__device__ __forceinline__ void run_flush(Run& R, u32* ring, uint8_t* out, u64 upto, u64 hi) {
+  const u32 lane = lane_id();
+  const u64 nb = (upto - R.flushed) / 16;
+  for (u64 b = lane; b < nb; b += 64) {
+    const u64 X = R.flushed + b * 16;
+    uint4* rp = (uint4*)ring + (((X - R.base) / 16) & (RING / 16 - 1));
+    const uint4 v = *rp;
+    *rp = make_uint4(0, 0, 0, 0);
+    store_block<RING>(out, X, v, R.lo, hi);
+  }
+  R.flushed = upto;
+  WAVE_SYNC();
+}
+
+template <u32 RING>
+__device__ __forceinline__ void run_close(Run& R, u32* ring, uint8_t* out) {
+  if (!R.open) return;
+  const u64 full = R.pos & ~15ull;
+  if (full > R.flushed) run_flush<RING>(R, ring, out, full, R.pos);
+  if (R.pos > R.flushed) run_flush<RING>(R, ring, out, R.flushed + 16, R.pos);  // partial tail block
+  R.open = false;
+}
+
+template <u32 RING>
+__device__ __forceinline__ void run_open(Run& R, u64 pos) {
+  R.base = pos & ~15ull;
+  R.lo = pos;
+  R.pos = pos;
+  R.flushed = R.base;
+  R.open = true;
+}
+
+// prefix bytes of candidates [0, r) of a radix word (candidate r <-> idx r+1)
+template <int LMAX, int MLMAX, int DPENT>
+__device__ u64 radix_prefix_bytes(const WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, const WordInfo& I, u64 r) {
+  if (r == 0) return 0;
+  const u64 Y = r + 1;  // idx in [0, Y) minus idx 0
+  i64 part = 0;
+  for (u32 i = lane_id(); i < I.nslots; i += 64) {
+    const Slot sl = S.slots[i];
+    const u64 QR = sl.Q * sl.R, full = Y / QR, rem = Y % QR;
+    for (u32 v = 1; v < sl.R; v++) {
+      const u64 lo = (u64)v * sl.Q;
+      const u64 cnt = full * sl.Q + (rem > lo ? min(sl.Q, rem - lo) : 0);
+      part += ((i64)T.ch[sl.choice_base + v].len - (i64)sl.klen) * (i64)cnt;
+    }
+  }
+  return (u64)((i64)(r * (u64)(I.L + 1)) + wave_sum_i64(part));
+}
+
+// General DP walk for candidate rank r: returns length (incl. newline); emits if EMIT.
+template <bool EMIT, u32 RING, int LMAX, int MLMAX, int DPENT>
+__device__ u32 dp_walk(const WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, const WordInfo& I, u64 r, Emit& e,
+                       u32* ring) {
+  const u32 W = I.W, m = I.nev;
+  u32 p = 0, c = 0, len = 1;
+  for (;;) {
+    const u32 ev = S.evidx[p], q = S.evpos[ev];
+    if (q > p) {  // forced keeps up to the next event
+      if (EMIT) em_bytes<RING>(e, ring, S.wbuf, p, q - p);
+      len += q - p;
+    }
+    if (ev >= m) break;
+    const u64 gk = S.dp.G[(ev + 1) * W + c];
+    if (r < gk) {
+      if (EMIT) em_put<RING>(e, ring, S.wbuf[q], 1);
+      len++;
+      p = q + 1;
+      continue;
+    }
+    r -= gk;
+    const u32 em = S.evm[ev], ms = em >> 8, mc = em & 255u;
+    const u32 nc = I.freew ? 1u : c + 1u;
+    u32 choice = 0, kl = 1;
+    for (u32 j = 0; j < mc && nc <= I.Cc; j++) {
+      const A5xKey key = T.keys[S.mlist[ms + j]];
+      const u64 gs = S.dp.G[S.evidx[q + key.klen] * W + nc];
+      if (gs == 0) continue;
+      u64 qv;
+      if (key.nvals <= 8) {
+        qv = 0;
+        while (qv < key.nvals && r >= gs) { r -= gs; qv++; }
+        if (qv < key.nvals) { choice = key.choice_base + 1 + (u32)qv; kl = key.klen; break; }
+      } else {
+        qv = r / gs;
+        if (qv < key.nvals) { r -= qv * gs; choice = key.choice_base + 1 + (u32)qv; kl = key.klen; break; }
+        r -= gs * key.nvals;
+      }
+    }
+    // choice == 0 cannot happen for r < G[ev][c]
+    if (EMIT) em_choice<RING>(e, ring, T, choice);
+    len += T.ch[choice].len;
+    p = q + kl;
+    c = nc;
+  }
+  if (EMIT) em_put<RING>(e, ring, '\n', 1);
+  return len;
+}
+
+// byte offset of candidate r inside its word's output (general words; any lane)
+template <int LMAX, int MLMAX, int DPENT>
+__device__ u64 dp_prefix_bytes(const WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, const WordInfo& I, u64 r) {
+  const u32 W = I.W, m = I.nev;
+  u32 p = 0, c = 0;
+  u64 pl = 0, acc = 0;
+  for (;;) {
+    const u32 ev = S.evidx[p], q = S.evpos[ev];
+    pl += q - p;
+    if (ev >= m) break;
+    const u32 qn = S.evpos[ev + 1];
+    const u64 gk = S.dp.G[(ev + 1) * W + c];
+    if (r < gk) { pl++; p = q + 1; continue; }
+    r -= gk;
+    acc += S.dp.H[(ev + 1) * W + c] + (pl + (qn - q)) * gk;
+    const u32 em = S.evm[ev], ms = em >> 8, mc = em & 255u;
+    const u32 nc = I.freew ? 1u : c + 1u;
+    u32 choice = 0, kl = 1;
+    for (u32 j = 0; j < mc && nc <= I.Cc; j++) {
+      const A5xKey key = T.keys[S.mlist[ms + j]];
+      const u32 p2 = q + key.klen, e2 = S.evidx[p2], lit = S.evpos[e2] - p2;
+      const u64 gs = S.dp.G[e2 * W + nc];
+      const u64 hs = S.dp.H[e2 * W + nc];
+      bool found = false;
+      for (u32 v = 0; v < key.nvals; v++) {
+        const u32 ci = key.choice_base + 1 + v;
+        if (r < gs) { choice = ci; kl = key.klen; found = true; break; }
+        r -= gs;
+        acc += hs + (pl + T.ch[ci].len + lit) * gs;
+      }
+      if (found) break;
+    }
+    pl += T.ch[choice].len;
+    p = q + kl;
+    c = nc;
+  }
+  return acc;
+}
+
+template <int LMAX, int MLMAX, int DPENT, u32 RING, bool PASSB>
+__device__ void expand_chunk(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab& T, const ExpArgs& a, u64 chunk) {
+  const u32 lane = lane_id();
+  const u64 g0 = max(a.cand_begin, chunk * a.CH);
+  const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
+  if (g0 >= g1) return;
+  u64 w = a.chunk_w0[chunk];
+  // the chunk map gives the word holding chunk*CH; advance to the one holding g0
+  while (a.cand_off[w + 1] <= g0) w++;
+  u64 r = g0 - a.cand_off[w];
+  u64 g = g0;
+  Run R;
+  R.open = false;
+  while (g < g1) {
+    const u64 cnt = a.cand_off[w + 1] - a.cand_off[w];
+    if (cnt == 0) { w++; continue; }
+    const u64 nhere = min(cnt - r, g1 - g);
+    const u32 fl = a.flags[w];
+    const bool mine = PASSB ? (fl & A5X_WF_BIG) != 0 : (fl & A5X_WF_BIG) == 0;
+    if (!mine) {
+      run_close<RING>(R, ring, a.out);
+      g += nhere; w++; r = 0;
+      continue;
+    }
+    WordInfo I = wave_setup<LMAX, MLMAX, DPENT>(S, T, a.words, a.woff, w, a.mn, a.mx);
+    if (!I.fits || I.count != cnt || I.maxlen > RING - 16) {
+      if (lane == 0) atomicOr(a.err, A5X_DERR_STATE);
+      run_close<RING>(R, ring, a.out);
+      return;
+    }
+    u64 pos = a.byte_off[w] - a.out_base;
+    if (r) {
+      if (I.cls & A5X_WF_RADIX) pos += radix_prefix_bytes(S, T, I, r);
+      else pos += uniform64(dp_prefix_bytes(S, T, I, r));
+    }
+    if (!R.open || R.pos != pos) {
+      run_close<RING>(R, ring, a.out);
+      run_open<RING>(R, pos);
+    }
+    // lanes per round: the ring holds at most RING-16 unflushed bytes
+    const u32 nl = min(64u, (RING - 16) / I.maxlen);
+    const u64 rend = r + nhere;
+    for (u64 rr = r; rr < rend; rr += nl) {
+      const bool act = lane < nl && rr + lane < rend;
+      const u64 rk = rr + lane;
+      u32 len = 0;
+      Emit e;
+      if (I.cls & A5X_WF_RADIX) {
+        const u32 idx = (u32)(rk + 1);
+        if (act) {
+          if (I.cls & A5X_WF_BIN) {
+            if (I.udelta != INT32_MIN) {
+              len = I.L + 1 + (u32)((int)__popc(idx) * I.udelta);
+            } else {
+              int l = (int)I.L + 1;
+              for (u32 i = 0; i < I.nslots; i++) l += ((idx >> i) & 1u) ? S.slots[i].delta1 : 0;
+              len = (u32)l;
+            }
+          } else {
+            int l = (int)I.L + 1;
+            u32 n = idx;
+            for (u32 i = 0; i < I.nslots; i++) {
+              const Slot& sl = S.slots[i];
+              const u32 q = fastdiv(n, sl.magic, sl.shift);
+              const u32 d = n - q * sl.R;
+              n = q;
+              if (d) l += (int)T.ch[sl.choice_base + d].len - (int)sl.klen;
+            }
+            len = (u32)l;
+          }
+        }
+        const u32 incl = wave_incl_scan_u32(len);
+        const u32 tot = __shfl((int)incl, 63);
+        const u64 off = R.pos + incl - len - R.base;
+        if (act) {
+          e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
+          u32 prev = 0, n = idx;
+          for (u32 i = 0; i < I.nslots; i++) {
+            const Slot& sl = S.slots[i];
+            u32 d;
+            if (I.cls & A5X_WF_BIN) d = (idx >> i) & 1u;
+            else { const u32 q = fastdiv(n, sl.magic, sl.shift); d = n - q * sl.R; n = q; }
+            if (sl.pos > prev) em_bytes<RING>(e, ring, S.wbuf, prev, sl.pos - prev);
+            em_choice<RING>(e, ring, T, sl.choice_base + d);
+            prev = sl.pos + sl.klen;
+          }
+          if (I.L > prev) em_bytes<RING>(e, ring, S.wbuf, prev, I.L - prev);
+          em_put<RING>(e, ring, '\n', 1);
+          em_finish<RING>(e, ring);
+        }
+        R.pos += tot;
+      } else {
+        if (act) len = dp_walk<false, RING>(S, T, I, rk, e, ring);
+        const u32 incl = wave_incl_scan_u32(len);
+        const u32 tot = __shfl((int)incl, 63);
+        const u64 off = R.pos + incl - len - R.base;
+        if (act) {
+          e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
+          dp_walk<true, RING>(S, T, I, rk, e, ring);
+          em_finish<RING>(e, ring);
+        }
+        R.pos += tot;
+      }
+      WAVE_SYNC();
+      const u64 full = R.pos & ~15ull;
+      if (full > R.flushed) run_flush<RING>(R, ring, a.out, full, R.pos);
+    }
+    g += nhere; w++; r = 0;
+    WAVE_SYNC();
+  }
+  run_close<RING>(R, ring, a.out);
+}
+
+template <int LMAX, int MLMAX, int DPENT, u32 RING, bool PASSB>
+__device__ void expand_body(const ExpArgs& a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  load_table(smem, a.table, a.table_bytes);
+  const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
+  const u32 tb = (a.table_bytes + 15u) & ~15u;
+  const u32 per = (u32)((sizeof(WaveLds<LMAX, MLMAX, DPENT>) + RING + 15u) & ~15u);
+  uint8_t* mine = smem + tb + wv * per;
+  u32* ring = (u32*)mine;
+  WaveLds<LMAX, MLMAX, DPENT>& S = *(WaveLds<LMAX, MLMAX, DPENT>*)(mine + RING);
+  for (u32 i = lane_id(); i < RING / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  const u64 c0 = a.cand_begin / a.CH;
+  const u64 chunk = c0 + (u64)blockIdx.x * nwv + wv;
+  if (chunk * a.CH >= a.cand_end) return;
+  if (PASSB && !a.chunk_big[chunk]) return;
+  expand_chunk<LMAX, MLMAX, DPENT, RING, PASSB>(S, ring, T, a, chunk);
+}
+
+__global__ void __launch_bounds__(256) k_expand_a(ExpArgs a) {
+  expand_body<A5X_LMAX_A, A5X_MLMAX_A, A5X_DPENT_A, A5X_RING_A, false>(a);
+}
+__global__ void __launch_bounds__(64) k_expand_b(ExpArgs a) {
+  expand_body<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B, A5X_RING_B, true>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Locate: global byte offset of candidate indices (range starts for partial calls)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_locate(ExpArgs a, const u64* cands, u32 n, u64* out_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  LdsB& S = *(LdsB*)(smem + ((a.table_bytes + 15u) & ~15u));
+  for (u32 i = 0; i < n; i++) {
+    const u64 g = cands[i];
+    if (g >= a.cand_off[a.nw]) { if (lane_id() == 0) out_bytes[i] = a.byte_off[a.nw]; continue; }
+    // largest w with cand_off[w] <= g (that word has count > 0)
+    u64 lo = 0, hi = a.nw;  // invariant cand_off[lo] <= g < cand_off[hi]
+    while (hi - lo > 1) {
+      const u64 mid = (lo + hi) / 2;
+      if (a.cand_off[mid] <= g) lo = mid; else hi = mid;
+    }
+    const u64 w = lo, r = g - a.cand_off[w];
+    u64 pos = a.byte_off[w];
+    if (r) {
+      WordInfo I = wave_setup<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>(S, T, a.words, a.woff, w, a.mn, a.mx);
+      if (!I.fits) { if (lane_id() == 0) atomicOr(a.err, A5X_DERR_STATE); return; }
+      if (I.cls & A5X_WF_RADIX) pos += radix_prefix_bytes(S, T, I, r);
+      else pos += uniform64(dp_prefix_bytes(S, T, I, r));
+    }
+    if (lane_id() == 0) out_bytes[i] = pos;
+    WAVE_SYNC();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Verification digest: per word {count, bytes, sum h, sum h^2}, h = fmix64(fnv1a64)
+// (same definition as oracle/a5_oracle.c a5o_cand_hash).  One lane per word.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u64 fmix64(u64 k) {
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+__global__ void __launch_bounds__(256) k_digest(const uint8_t* out, const u64* byte_off, u64 out_base, u64 nw,
+                                                u64* dig) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+    const u64 s = byte_off[w] - out_base, e = byte_off[w + 1] - out_base;
+    u64 cnt = 0, hs = 0, hq = 0, h = 1469598103934665603ULL;
+    for (u64 i = s; i < e; i++) {
+      const u32 b = out[i];
+      if (b == '\n') {
+        const u64 f = fmix64(h);
+        cnt++; hs += f; hq += f * f;
+        h = 1469598103934665603ULL;
+      } else {
+        h ^= b; h *= 1099511628211ULL;
+      }
+    }
+    dig[4 * w + 0] = cnt; dig[4 * w + 1] = e - s; dig[4 * w + 2] = hs; dig[4 * w + 3] = hq;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-visible launch helpers (C++ linkage; used by a5x_host.cpp)
+// ---------------------------------------------------------------------------
+#include "a5x_launch.h"
+
+static inline u32 blocks_for(u64 n, u32 bs, u32 cap) {
+  u64 b = (n + bs - 1) / bs;
+  if (b < 1) b = 1;
+  return (u32)(b < cap ? b : cap);
+}
+
+hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
+  KsArgs a;
+  a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
+  a.mn = L.mn; a.mx = L.mx; a.count = L.count; a.bytes = L.bytes; a.flags = L.flags;
+  a.defer_list = L.defer_list; a.defer_n = L.defer_n; a.nbig = L.nbig; a.err = L.err;
+  hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, 256, 65536)), dim3(256), L.table_bytes, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t lds = ((L.table_bytes + 15u) & ~15u) + sizeof(LdsB);
+  hipLaunchKernelGGL(k_keyspace_wave, dim3(L.defer_blocks), dim3(64), lds, st, a);
+  return hipGetLastError();
+}
+
+size_t a5x_keyspace_wave_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + sizeof(LdsB); }
+
+// recursive exclusive scan of pairs; tmp must hold a5x_scan_tmp_elems(n) u64
+u64 a5x_scan_tmp_elems(u64 n) {
+  u64 t = 0;
+  while (n > SCAN_TILE) { n = (n + SCAN_TILE - 1) / SCAN_TILE; t += 2 * (n + 1); }
+  return t + 2;
+}
+
+hipError_t a5x_launch_scan(const u64* ca, const u64* cb, u64 n, u64* outa, u64* outb, u64* tmp, u32* err,
+                           hipStream_t st) {
+  if (n <= SCAN_TILE) {
+    hipLaunchKernelGGL(k_scan_down, dim3(1), dim3(SCAN_BLOCK), 0, st, ca, cb, n, (const u64*)nullptr,
+                       (const u64*)nullptr, outa, outb, err);
+    return hipGetLastError();
+  }
+  const u64 nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  u64* sa = tmp;
+  u64* sb = tmp + (nb + 1);
+  hipLaunchKernelGGL(k_scan_reduce, dim3((u32)nb), dim3(SCAN_BLOCK), 0, st, ca, cb, n, sa, sb, err);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // scan the block sums in place (into the same arrays, n+1 layout)
+  e = a5x_launch_scan(sa, sb, nb, sa, sb, tmp + 2 * (nb + 1), err, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_scan_down, dim3((u32)nb), dim3(SCAN_BLOCK), 0, st, ca, cb, n, (const u64*)sa,
+                     (const u64*)sb, outa, outb, err);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_plan(const u64* cand_off, const u32* flags, u64 nw, u64 CH, u32* chunk_w0, u32* chunk_big,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_plan, dim3(blocks_for(nw, 256, 65536)), dim3(256), 0, st, cand_off, flags, nw, CH, chunk_w0,
+                     chunk_big);
+  return hipGetLastError();
+}
+
+static ExpArgs exp_args(const A5xExpLaunch& L) {
+  ExpArgs a;
+  a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
+  a.cand_off = L.cand_off; a.byte_off = L.byte_off; a.flags = L.flags; a.chunk_w0 = L.chunk_w0;
+  a.chunk_big = L.chunk_big; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.out = L.out;
+  a.out_base = L.out_base; a.mn = L.mn; a.mx = L.mx; a.err = L.err;
+  return a;
+}
+
+size_t a5x_expand_lds(u32 table_bytes, int passb, u32 waves) {
+  const size_t tb = (table_bytes + 15u) & ~15u;
+  if (passb) return tb + ((sizeof(LdsB) + A5X_RING_B + 15u) & ~(size_t)15u);
+  return tb + waves * ((sizeof(LdsA) + A5X_RING_A + 15u) & ~(size_t)15u);
+}
+
+hipError_t a5x_launch_expand(const A5xExpLaunch& L, int passb, hipStream_t st) {
+  ExpArgs a = exp_args(L);
+  const u64 c0 = L.cand_begin / L.CH, c1 = (L.cand_end + L.CH - 1) / L.CH;
+  const u64 nchunks = c1 - c0;
+  if (nchunks == 0) return hipSuccess;
+  if (!passb) {
+    const u32 waves = L.waves_per_block;
+    const u64 nb = (nchunks + waves - 1) / waves;
+    hipLaunchKernelGGL(k_expand_a, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);
+  } else {
+    hipLaunchKernelGGL(k_expand_b, dim3((u32)nchunks), dim3(64), a5x_expand_lds(L.table_bytes, 1, 1), st, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_locate(const A5xExpLaunch& L, const u64* cands, u32 n, u64* out_bytes, hipStream_t st) {
+  ExpArgs a = exp_args(L);
+  hipLaunchKernelGGL(k_locate, dim3(1), dim3(64), a5x_keyspace_wave_lds(L.table_bytes), st, a, cands, n, out_bytes);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_digest(const uint8_t* out, const u64* byte_off, u64 out_base, u64 nw, u64* dig,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_digest, dim3(blocks_for(nw, 256, 65536)), dim3(256), 0, st, out, byte_off, out_base, nw, dig);
+  return hipGetLastError();
+}
+
+hipError_t a5x_set_kernel_attrs() {
+  hipError_t e = hipFuncSetAttribute((const void*)k_expand_b, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_keyspace_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_locate, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_expand_a, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}

@@ -1,0 +1,57 @@
+// a5x_launch.h -- host-side launch interface of a5x_kernels.hip (internal to liba5x).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+struct A5xKsLaunch {
+  const uint8_t* table;
+  uint32_t table_bytes;
+  const uint8_t* words;
+  const uint64_t* woff;
+  uint64_t nw;
+  int mn, mx;
+  uint64_t* count;
+  uint64_t* bytes;
+  uint32_t* flags;
+  uint32_t* defer_list;
+  uint32_t* defer_n;
+  uint32_t* nbig;
+  uint32_t* err;
+  uint32_t defer_blocks;
+};
+
+struct A5xExpLaunch {
+  const uint8_t* table;
+  uint32_t table_bytes;
+  const uint8_t* words;
+  const uint64_t* woff;
+  uint64_t nw;
+  const uint64_t* cand_off;
+  const uint64_t* byte_off;
+  const uint32_t* flags;
+  const uint32_t* chunk_w0;
+  const uint32_t* chunk_big;
+  uint64_t cand_begin, cand_end;
+  uint64_t CH;
+  uint8_t* out;
+  uint64_t out_base;
+  int mn, mx;
+  uint32_t* err;
+  uint32_t waves_per_block;
+};
+
+hipError_t a5x_set_kernel_attrs();
+hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st);
+size_t a5x_keyspace_wave_lds(uint32_t table_bytes);
+uint64_t a5x_scan_tmp_elems(uint64_t n);
+hipError_t a5x_launch_scan(const uint64_t* ca, const uint64_t* cb, uint64_t n, uint64_t* outa, uint64_t* outb,
+                           uint64_t* tmp, uint32_t* err, hipStream_t st);
+hipError_t a5x_launch_plan(const uint64_t* cand_off, const uint32_t* flags, uint64_t nw, uint64_t CH,
+                           uint32_t* chunk_w0, uint32_t* chunk_big, hipStream_t st);
+size_t a5x_expand_lds(uint32_t table_bytes, int passb, uint32_t waves);
+hipError_t a5x_launch_expand(const A5xExpLaunch& L, int passb, hipStream_t st);
+hipError_t a5x_launch_locate(const A5xExpLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out_bytes,
+                             hipStream_t st);
+hipError_t a5x_launch_digest(const uint8_t* out, const uint64_t* byte_off, uint64_t out_base, uint64_t nw,
+                             uint64_t* dig, hipStream_t st);

@@ -1,0 +1,74 @@
+"""Seeded synthetic word lists for the BASELINE.json configs.
+
+``greek-dictionary.txt`` is missing from the reference snapshot
+(``.MISSING_LARGE_BLOBS:1``), and there is no network, so every benchmark and
+scale test runs on these generators (numpy PCG64, fixed seeds).
+Output layout = the ABI batch layout: contiguous bytes (+16 B pad) and n+1
+u64 offsets.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+
+GREEK = np.array([0x3B1 + i for i in range(25)], dtype=np.int64)  # α..ω
+
+
+def _pack(lengths: np.ndarray, data: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    offs = np.zeros(len(lengths) + 1, dtype=np.uint64)
+    np.cumsum(lengths, out=offs[1:])
+    out = np.zeros(len(data) + 16, dtype=np.uint8)
+    out[: len(data)] = data
+    return out, offs
+
+
+def words_from_alphabet(n: int, lmin: int, lmax: int, alphabet: bytes, seed: int) -> Tuple[np.ndarray, np.ndarray]:
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(lmin, lmax + 1, size=n, dtype=np.int64)
+    alpha = np.frombuffer(alphabet, dtype=np.uint8)
+    data = alpha[rng.integers(0, len(alpha), size=int(lengths.sum()), dtype=np.int64)]
+    return _pack(lengths, data)
+
+
+def words_az(n: int, lmin: int = 6, lmax: int = 12, seed: int = 0x5A5) -> Tuple[np.ndarray, np.ndarray]:
+    """[a-z] words, length U[lmin, lmax] (C3, C4 with lmin=lmax=10, C2 ASCII variant)."""
+    return words_from_alphabet(n, lmin, lmax, b"abcdefghijklmnopqrstuvwxyz", seed)
+
+
+def words_az09(n: int, lmin: int = 6, lmax: int = 12, seed: int = 0x5A5) -> Tuple[np.ndarray, np.ndarray]:
+    """[a-z0-9] words (C1)."""
+    return words_from_alphabet(n, lmin, lmax, b"abcdefghijklmnopqrstuvwxyz0123456789", seed)
+
+
+def words_greek(n: int, lmin: int = 6, lmax: int = 12, seed: int = 0x5A5) -> Tuple[np.ndarray, np.ndarray]:
+    """Greek [α-ω] words of lmin..lmax letters (2 UTF-8 bytes each; C2, C5)."""
+    rng = np.random.default_rng(seed)
+    letters = rng.integers(lmin, lmax + 1, size=n, dtype=np.int64)
+    cps = GREEK[rng.integers(0, len(GREEK), size=int(letters.sum()), dtype=np.int64)]
+    b0 = (0xC0 | (cps >> 6)).astype(np.uint8)
+    b1 = (0x80 | (cps & 0x3F)).astype(np.uint8)
+    data = np.stack([b0, b1], axis=1).reshape(-1)
+    return _pack(letters * 2, data)
+
+
+CONFIGS = {
+    # name: (tables, generator, kwargs, description)
+    "c1": (["qwerty-azerty"], words_az09, {"lmin": 6, "lmax": 12},
+           "qwerty-azerty x 10k [a-z0-9] words len U[6,12] (configs[0], CPU plumbing)"),
+    "c2": (["qwerty-greek"], words_greek, {"lmin": 6, "lmax": 12},
+           "qwerty-greek x synthetic Greek words len U[6,12] (configs[1]; 0 candidates: keys are ASCII)"),
+    "c2a": (["qwerty-greek"], words_az, {"lmin": 6, "lmax": 12},
+            "qwerty-greek x [a-z] words len U[6,12] (configs[1] ASCII variant, multi-byte output)"),
+    "c3": (["czech", "german"], words_az, {"lmin": 6, "lmax": 12},
+           "czech+german x synthetic [a-z] words len U[6,12] (configs[2])"),
+    "c4": (["qwerty-cyrillic"], words_az, {"lmin": 10, "lmax": 10},
+           "qwerty-cyrillic x synthetic [a-z] words len 10 (configs[3], 1023 cand/word)"),
+    "c5": (["greek-hebrew"], words_greek, {"lmin": 6, "lmax": 12},
+           "greek-hebrew x synthetic Greek words len U[6,12] (configs[4] expansion stage)"),
+}
+
+
+def config_words(name: str, n: int, seed: int = 0x5A5):
+    tables, gen, kw, _ = CONFIGS[name]
+    return tables, gen(n, seed=seed, **kw)
