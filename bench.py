@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""bench.py -- candidates/s of the hashcat -a 5 table expansion hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3] [--words N]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One "step" = one full pass of the hot path over one batch already resident in HBM:
+keyspace (k_keyspace_*) -> prefix scans -> chunk plan -> expansion (k_expand_a[/b])
+into an HBM output buffer, i.e. a5x_expand_device() of include/a5x.h.  The default
+workload is BASELINE.json configs[2]: czech.table + german.table over a synthetic
+10M-word [a-z] list (len U[6,12]) per GPU.  Multi-GPU = weak scaling: every rank
+expands its own 10M-word shard (independent words, no data-path collective);
+the only collectives are the barrier and the max/sum reductions of the timing.
+
+Prints ONE JSON line (rank 0) with the driver's fields plus "roofline" (expansion
+kernel: algorithmic bytes = sum(len(cand)+1) per launch / average launch time from
+HIP events on the library stream) and "cpu_baseline" (oracle/a5_oracle.c run with
+the reference's goroutine/channel/writer structure on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c3", help="c1 c2 c2a c3 c4 c5 (hashcat_a5_table_generator_amd/synth.py)")
+    ap.add_argument("--words", type=int, default=10_000_000, help="words per GPU")
+    ap.add_argument("--min", type=int, default=0)
+    ap.add_argument("--max", type=int, default=15)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-words", type=int, default=50_000)
+    ap.add_argument("--verify", action="store_true", help="digest-check the last step against the C oracle")
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self, n_gpus: int):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.dist, self.torch = dist, torch
+        if n_gpus != self.world and self.rank == 0:
+            log(f"note: --gpus {n_gpus} but WORLD_SIZE={self.world}; using WORLD_SIZE")
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+            self.torch.cuda.synchronize()
+
+    def reduce(self, x: float, op: str) -> float:
+        if not self.dist:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def latest_profile_traffic(workload: str):
+    """HBM bytes per expansion launch from the committed rocprofv3 --pmc pass (or None)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+            if d.get("workload") == workload and d.get("bytes_per_launch"):
+                return d
+        except Exception:
+            continue
+    return None
+
+
+def cpu_baseline(tables, args):
+    """The reference algorithm restated in C (oracle/a5_oracle.c), main.go:58-98 structure."""
+    from oracle import c_oracle as co
+    from hashcat_a5_table_generator_amd import synth
+    t = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", x + ".table") for x in tables])
+    fd = os.open(os.devnull, os.O_WRONLY)
+    best = None
+    for th in sorted({1, min(16, os.cpu_count() or 1)}):
+        nwords = args.cpu_sample_words if th == 1 else max(1000, args.cpu_sample_words // 5)
+        _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
+        t0 = time.perf_counter()
+        c, b = t.run_pipeline(data, offs, 0, args.min, args.max, th, fd)
+        dt = time.perf_counter() - t0
+        r = {"value": c / dt, "unit": "candidates/s", "cores": th, "kind": "port",
+             "sample": f"{nwords} words of workload {args.workload} (seed 0xC0FFEE): {c} candidates, "
+                       f"{b} bytes to /dev/null in {dt:.2f} s; C restatement of main.go with {th} worker thread(s), "
+                       f"a 1000-slot channel and one 4 KiB writer (best of 1 and {min(16, os.cpu_count() or 1)} "
+                       f"threads)"}
+        log(f"cpu baseline threads={th}: {c / dt / 1e6:.2f} Mcand/s ({dt:.2f} s)")
+        if best is None or r["value"] > best["value"]:
+            best = r
+    os.close(fd)
+    return best
+
+
+def main():
+    args = parse()
+    D = Dist(args.gpus)
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
+
+    tables, (data, offs) = synth.config_words(args.workload, args.words, seed=0x5A5 + 7919 * D.rank)
+    n = len(offs) - 1
+    ctx = Context(D.local)
+    ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
+    dw = DeviceBuffer.from_array(ctx, data)
+    do = DeviceBuffer.from_array(ctx, offs)
+    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, 0, args.min, args.max)
+    log(f"rank {D.rank}: {ctx.device_name}: {n} words -> {tc} candidates, {tb / 1e9:.2f} GB")
+    out = DeviceBuffer(ctx, max(tb, 16))
+    boff = DeviceBuffer(ctx, (n + 1) * 8)
+
+    def step():
+        return ctx.expand_device(dw.ptr, do.ptr, n, out.ptr, tb, 0, args.min, args.max, d_byte_off=boff.ptr)
+
+    for _ in range(args.warmup):
+        step()
+    D.barrier()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        stats.append(step())
+    D.barrier()
+    dt = time.perf_counter() - t0
+    dt_max = D.reduce(dt, "max")
+    cands_all = D.reduce(float(tc) * args.steps, "sum")
+    ms_exp = float(np.mean([s["ms_expand"] for s in stats]))
+    ms_ks = float(np.mean([s["ms_keyspace"] for s in stats]))
+    launches = stats[-1]["expand_launches"]
+    ms_exp_max = D.reduce(ms_exp, "max")
+
+    if args.verify:
+        from oracle import c_oracle as co
+        dig = DeviceBuffer(ctx, n * 32)
+        ctx.digest_device(out.ptr, boff.ptr, 0, n, dig.ptr)
+        got = dig.to_array(np.uint64).reshape(n, 4)
+        want = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables]
+                         ).digest_batch(data, offs, 0, args.min, args.max)
+        bad = int((got != want).any(axis=1).sum())
+        log(f"verify: {bad} mismatching words of {n}")
+        if bad:
+            raise SystemExit(f"verification failed on {bad} words")
+
+    if D.rank == 0:
+        achieved = tb / (ms_exp * 1e-3) / 1e9  # GB/s, algorithmic bytes per launch / launch time
+        prof = latest_profile_traffic(args.workload)
+        traffic = None
+        if prof:
+            traffic = prof["bytes_per_launch"]
+        desc = synth.CONFIGS[args.workload][3]
+        res = {
+            "metric": "candidates/sec (whole node) at 1/2/4/8 MI355X + % HBM write roofline",
+            "value": cands_all / dt_max,
+            "unit": "candidates/s",
+            "n_gpus": D.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.workload}: {desc}",
+                "tables": tables,
+                "words_per_gpu": n,
+                "candidates_per_gpu_step": tc,
+                "bytes_per_gpu_step": tb,
+                "table_min": args.min,
+                "table_max": args.max,
+                "mode": "processWord (default)",
+                "parallelism": f"weak: {D.world} x independent word shards, no data-path collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_expand_a" + ("+k_expand_b" if launches > 1 else ""),
+                "ms_per_launch": ms_exp,
+                "ms_per_launch_max_rank": ms_exp_max,
+                "ms_keyspace_scan_plan": ms_ks,
+                "algorithmic_bytes_per_launch": tb,
+            },
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(tables, args)
+        print(json.dumps(res), flush=True)
+    D.barrier()
+    for b in (out, boff, dw, do):
+        b.free()
+    ctx.close()
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -6,7 +6,7 @@
 //
 //   A5xTableHdr                                   (64 B)
 //   u16 bucket[257]  keys whose first byte is b are [bucket[b], bucket[b+1])
-//   A5xKey  keys[nkeys]                           (16 B each, 16-B aligned)
+//   A5xKey  keys[nkeys]                           (32 B each, 16-B aligned)
 //   A5xChoice choices[nchoices]                   (8 B each)
 //   u8 blob[blob_bytes]                           (key + value bytes, 8-B padded)
 //
@@ -40,7 +40,11 @@ struct A5xKey {
   uint32_t choice_base;   // choices[choice_base] = key, [choice_base+1+v] = value v
   uint32_t sumlen;        // sum of value lengths (byte DP)
   int16_t maxdelta;       // max(|v|) - klen
-  uint16_t pad;
+  uint16_t maxclen;       // max(klen, max |v|): longest choice
+  uint32_t magic;         // branch-free u32 division by R = nvals + 1 (libdivide form)
+  uint32_t shift;
+  uint32_t sum_dpos;      // sum over values of max(|v| - klen, 0)
+  uint32_t sum_dneg;      // sum over values of max(klen - |v|, 0)
 };
 
 struct A5xChoice {
@@ -50,7 +54,7 @@ struct A5xChoice {
 };
 
 static_assert(sizeof(A5xTableHdr) == 64, "hdr");
-static_assert(sizeof(A5xKey) == 16, "key");
+static_assert(sizeof(A5xKey) == 32, "key");
 static_assert(sizeof(A5xChoice) == 8, "choice");
 
 // Per-word class flags written by the keyspace pass (u32 per word).
@@ -60,9 +64,13 @@ enum : uint32_t {
   A5X_WF_GENERAL = 1u << 2, // overlapping / multi matches or capped: DP walk
   A5X_WF_BIG = 1u << 3,     // does not fit the pass-A wave budget: pass B
   A5X_WF_DEFER = 1u << 4,   // keyspace needs the wave-level DP kernel
+  A5X_WF_FAST = 1u << 5,    // radix, <= 64 B, fanout <= 3, choices <= 4 B, <= 32 pieces: k_expand_fast
   A5X_WF_ERR_OVF = 1u << 8, // count/bytes overflow u64
   A5X_WF_ERR_BIG = 1u << 9, // exceeds pass-B limits
 };
+
+// bits 16..23 of a RADIX word's flags: its slot count (<= 64); bits 24..29 of a
+// FAST word: its piece count (<= 32), see fast_piece_count() in a5x_kernels.hip
 
 // Limits of the expansion passes (documented in DESIGN.md).
 #define A5X_WAVE 64

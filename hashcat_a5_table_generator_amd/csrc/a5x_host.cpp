@@ -80,8 +80,8 @@ struct a5x_ctx {
   uint32_t table_bytes = 0;
 
   DevBuf<uint64_t> count, bytes, cand_off, byte_off, scan_tmp, locate;
-  DevBuf<uint32_t> flags, defer, chunk_w0, chunk_big;
-  uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] pad
+  DevBuf<uint32_t> flags, defer, chunk_w0, chunk_kind;
+  uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] nslow, [16..31] guard record
   uint32_t* h_scalars = nullptr;  // pinned
   uint64_t* h_totals = nullptr;   // pinned [0] cands [1] bytes [2..3] locate
 
@@ -224,6 +224,20 @@ int compile_table(a5x_ctx* c) {
       max_vlen = std::max(max_vlen, (uint32_t)v.size());
     }
     key.maxdelta = (int16_t)std::max(-32768, std::min(32767, maxd));
+    {
+      size_t mc = k.size();
+      for (auto& v : vs) mc = std::max(mc, v.size());
+      key.maxclen = (uint16_t)std::min<size_t>(mc, 65535);
+    }
+    for (auto& v : vs) {
+      const long d = (long)v.size() - (long)k.size();
+      if (d > 0) key.sum_dpos += (uint32_t)d; else key.sum_dneg += (uint32_t)(-d);
+    }
+    {  // libdivide u32 branch-free magic for R = nvals + 1 (>= 2)
+      const uint32_t R = (uint32_t)vs.size() + 1, l = 32 - __builtin_clz(R - 1);
+      key.magic = (uint32_t)(((((uint64_t)1) << 32) * ((((uint64_t)1) << l) - R)) / R + 1);
+      key.shift = l - 1;
+    }
     max_klen = std::max(max_klen, (uint32_t)k.size());
     keys.push_back(key);
   }
@@ -284,6 +298,15 @@ int check_mode(a5x_ctx* c, int mode) {
 
 int decode_dev_err(a5x_ctx* c, uint32_t e) {
   if (!e) return A5X_OK;
+  if (e & 32u) {
+    uint64_t d[8] = {0};
+    (void)hipMemcpy(d, c->d_scalars + 16, sizeof d, hipMemcpyDeviceToHost);
+    return fail(c, A5X_E_HIP,
+                "device bounds guard tripped: code %llu ctx {%llu, %llu, %llu, %llu} block %llu thread %llu",
+                (unsigned long long)d[0], (unsigned long long)d[1], (unsigned long long)d[2],
+                (unsigned long long)d[3], (unsigned long long)d[4], (unsigned long long)d[5],
+                (unsigned long long)d[6]);
+  }
   if (e & 2u) return fail(c, A5X_E_OVERFLOW, "a word's keyspace overflows 64 bits");
   if (e & 16u) return fail(c, A5X_E_OVERFLOW, "batch keyspace overflows 64 bits");
   if (e & 4u)
@@ -295,7 +318,7 @@ int decode_dev_err(a5x_ctx* c, uint32_t e) {
 
 struct Batch {  // device-side per-batch state after keyspace
   uint64_t total_cands = 0, total_bytes = 0;
-  uint32_t nbig = 0;
+  uint32_t nbig = 0, nslow = 0;
   const uint64_t* cand_off = nullptr;
   const uint64_t* byte_off = nullptr;
 };
@@ -318,12 +341,13 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
     d_byte_off = c->byte_off.p;
   }
   if (timed) HIPCHK(c, hipEventRecord(c->ev[0], st));
-  HIPCHK(c, hipMemsetAsync(c->d_scalars, 0, 16, st));
+  HIPCHK(c, hipMemsetAsync(c->d_scalars, 0, 128, st));  // scalars + guard debug record
   if (nw > 0) {
     A5xKsLaunch K;
     K.table = c->d_table; K.table_bytes = c->table_bytes; K.words = d_words; K.woff = d_woff; K.nw = nw;
     K.mn = mn; K.mx = mx; K.count = c->count.p; K.bytes = c->bytes.p; K.flags = c->flags.p;
     K.defer_list = c->defer.p; K.defer_n = c->d_scalars; K.nbig = c->d_scalars + 1; K.err = c->d_scalars + 2;
+    K.nslow = c->d_scalars + 3;
     K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nw, (uint64_t)c->cus * 4));
     HIPCHK(c, a5x_launch_keyspace(K, st));
     HIPCHK(c, a5x_launch_scan(c->count.p, c->bytes.p, nw, d_cand_off, d_byte_off, c->scan_tmp.p,
@@ -359,6 +383,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   B->total_cands = nw ? c->h_totals[0] : 0;
   B->total_bytes = nw ? c->h_totals[1] : 0;
   B->nbig = c->h_scalars[1];
+  B->nslow = c->h_scalars[3];
   B->cand_off = d_cand_off;
   B->byte_off = d_byte_off;
   return A5X_OK;
@@ -370,7 +395,8 @@ A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   memset(&E, 0, sizeof E);
   E.table = c->d_table; E.table_bytes = c->table_bytes; E.words = d_words; E.woff = d_woff; E.nw = nw;
   E.cand_off = B.cand_off; E.byte_off = B.byte_off; E.flags = c->flags.p; E.chunk_w0 = c->chunk_w0.p;
-  E.chunk_big = c->chunk_big.p; E.CH = c->chunk; E.mn = mn; E.mx = mx; E.err = c->d_scalars + 2;
+  E.chunk_kind = c->chunk_kind.p; E.CH = c->chunk; E.mn = mn; E.mx = mx; E.err = c->d_scalars + 2;
+  E.dbg = (uint64_t*)(c->d_scalars + 16);
   E.waves_per_block = c->waves_per_block;
   return E;
 }
@@ -408,8 +434,8 @@ int a5x_create(int device, a5x_ctx** out) {
     c->cus = prop.multiProcessorCount;
   }
   if (c->cus <= 0) c->cus = 256;
-  bool ok = hipMalloc((void**)&c->d_scalars, 64) == hipSuccess &&
-            hipHostMalloc((void**)&c->h_scalars, 64, 0) == hipSuccess &&
+  bool ok = hipMalloc((void**)&c->d_scalars, 256) == hipSuccess &&
+            hipHostMalloc((void**)&c->h_scalars, 256, 0) == hipSuccess &&
             hipHostMalloc((void**)&c->h_totals, 64, 0) == hipSuccess && a5x_set_kernel_attrs() == hipSuccess;
   for (int i = 0; i < 4 && ok; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   if (!ok) {
@@ -428,7 +454,7 @@ void a5x_destroy(a5x_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   release(c->count); release(c->bytes); release(c->cand_off); release(c->byte_off); release(c->scan_tmp);
-  release(c->locate); release(c->flags); release(c->defer); release(c->chunk_w0); release(c->chunk_big);
+  release(c->locate); release(c->flags); release(c->defer); release(c->chunk_w0); release(c->chunk_kind);
   release(c->s_words); release(c->s_out); release(c->s_woff);
   if (c->d_table) (void)hipFree(c->d_table);
   if (c->d_scalars) (void)hipFree(c->d_scalars);
@@ -612,16 +638,18 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
                 (unsigned long long)out_cap);
   E.out = d_out;
   E.out_base = b0;
+  E.out_cap = out_cap;
   const uint64_t nchunks = (B.total_cands + c->chunk - 1) / c->chunk;
-  if ((rc = grow(c, c->chunk_w0, nchunks + 1)) || (rc = grow(c, c->chunk_big, nchunks + 1))) return rc;
+  if ((rc = grow(c, c->chunk_w0, nchunks + 1)) || (rc = grow(c, c->chunk_kind, nchunks + 1))) return rc;
   E.chunk_w0 = c->chunk_w0.p;
-  E.chunk_big = c->chunk_big.p;
-  if (B.nbig) HIPCHK(c, hipMemsetAsync(c->chunk_big.p, 0, (nchunks + 1) * 4, st));
-  HIPCHK(c, a5x_launch_plan(B.cand_off, c->flags.p, nw, c->chunk, c->chunk_w0.p, B.nbig ? c->chunk_big.p : nullptr,
-                            st));
+  E.chunk_kind = c->chunk_kind.p;
+  const bool other = B.nbig || B.nslow;
+  if (other) HIPCHK(c, hipMemsetAsync(c->chunk_kind.p, 0, (nchunks + 1) * 4, st));
+  HIPCHK(c, a5x_launch_plan(B.cand_off, c->flags.p, nw, c->chunk, c->chunk_w0.p, c->chunk_kind.p, st));
   HIPCHK(c, hipEventRecord(c->ev[1], st));
   HIPCHK(c, a5x_launch_expand(E, 0, st));
-  if (B.nbig) HIPCHK(c, a5x_launch_expand(E, 1, st));
+  if (B.nslow) HIPCHK(c, a5x_launch_expand(E, 1, st));
+  if (B.nbig) HIPCHK(c, a5x_launch_expand(E, 2, st));
   HIPCHK(c, hipEventRecord(c->ev[2], st));
   HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
@@ -635,7 +663,7 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     stats->ms_expand = b;
     stats->ms_total = t;
     stats->words_pass_b = B.nbig;
-    stats->expand_launches = B.nbig ? 2 : 1;
+    stats->expand_launches = 1 + (B.nslow ? 1 : 0) + (B.nbig ? 1 : 0);
     stats->pad = 0;
   }
   return A5X_OK;

@@ -44,6 +44,7 @@ enum : u32 {
   A5X_DERR_BIG = 1u << 2,     // a word beyond pass-B limits has candidates
   A5X_DERR_STATE = 1u << 3,   // internal consistency (keyspace vs expand)
   A5X_DERR_SCANOVF = 1u << 4, // prefix sum overflow
+  A5X_DERR_GUARD = 1u << 5,   // a device bounds guard tripped (see the debug record)
 };
 
 // ---------------------------------------------------------------------------
@@ -87,9 +88,10 @@ __device__ __forceinline__ u32 wave_or_u32(u32 x) {
   for (int m = 32; m >= 1; m >>= 1) x |= (u32)__shfl_xor((int)x, m);
   return x;
 }
-__device__ __forceinline__ u32 uniform(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
+// readfirstlane returns int: convert through u32 so nothing sign-extends
+__device__ __forceinline__ u32 uniform(u32 x) { return (u32)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ u64 uniform64(u64 x) {
-  return ((u64)__builtin_amdgcn_readfirstlane((u32)(x >> 32)) << 32) | __builtin_amdgcn_readfirstlane((u32)x);
+  return ((u64)uniform((u32)(x >> 32)) << 32) | (u64)uniform((u32)x);
 }
 
 // a*b with overflow flag
@@ -152,6 +154,13 @@ __device__ __forceinline__ bool key_match_global(const uint8_t* wp, u32 p, const
   return true;
 }
 
+// Pieces of a FAST word (k_expand_fast emits one <= 4-byte piece per step): the
+// literal run before a slot merges with the slot's choice when run + longest
+// choice <= 4, else it is cut into 4-byte literal pieces; the tail + '\n' is cut
+// the same way.  Both the keyspace pass and the window setup use this rule.
+__device__ __forceinline__ u32 lit_pieces(u32 m) { return (m + 3) / 4; }
+__device__ __forceinline__ u32 slot_pieces(u32 run, u32 maxclen) { return run + maxclen <= 4 ? 1u : lit_pieces(run) + 1u; }
+
 // ---------------------------------------------------------------------------
 // Keyspace, one lane per word (radix fast path; SURVEY 8(a) closed form)
 // ---------------------------------------------------------------------------
@@ -168,6 +177,7 @@ struct KsArgs {
   u32* defer_list;
   u32* defer_n;
   u32* nbig;
+  u32* nslow;
   u32* err;
 };
 
@@ -181,7 +191,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     const u64 s = a.woff[w], e = a.woff[w + 1];
     const u64 L64 = e - s;
     if (a.mx < 1 || L64 == 0) {  // processWord emits nothing
-      a.count[w] = 0; a.bytes[w] = 0; a.flags[w] = A5X_WF_RADIX;
+      a.count[w] = 0; a.bytes[w] = 0; a.flags[w] = A5X_WF_RADIX | A5X_WF_FAST;
       continue;
     }
     if (L64 > A5X_LMAX_A) {  // long words: the wave kernel (loops over positions)
@@ -191,7 +201,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     }
     const u32 L = (u32)L64;
     const uint8_t* wp = a.words + s;
-    u32 nmatch = 0, last_end = 0, maxl = L + 1;
+    u32 nmatch = 0, last_end = 0, maxl = L + 1, maxnv = 0, maxcl = 0, npiece = 0, pend = 0;
     bool conflict = false, bin = true, ovf = false;
     u64 P = 1, Dp = 0, Dn = 0;
     for (u32 p = 0; p < L; p++) {
@@ -205,21 +215,21 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
         last_end = max(last_end, p + (u32)key.klen);
         const u64 R = (u64)key.nvals + 1;
         // sum over this slot's values of (|v| - klen), split by sign
-        u64 spos = 0, sneg = 0;
-        for (u32 v = 0; v < key.nvals; v++) {
-          const int d = (int)T.ch[key.choice_base + 1 + v].len - (int)key.klen;
-          if (d > 0) spos += (u64)d; else sneg += (u64)(-d);
-        }
+        const u64 spos = key.sum_dpos, sneg = key.sum_dneg;
         Dp = add_ovf(mul_ovf(Dp, R, ovf), mul_ovf(P, spos, ovf), ovf);
         Dn = add_ovf(mul_ovf(Dn, R, ovf), mul_ovf(P, sneg, ovf), ovf);
         P = mul_ovf(P, R, ovf);
         if (key.nvals != 1) bin = false;
         if (key.maxdelta > 0) maxl += (u32)key.maxdelta;
+        maxnv = max(maxnv, (u32)key.nvals);
+        maxcl = max(maxcl, (u32)key.maxclen);
+        npiece += slot_pieces(p - pend, key.maxclen);  // meaningful only without conflicts
+        pend = p + key.klen;
       }
     }
     const bool freew = (a.mn <= 1) && ((i64)nmatch <= (i64)a.mx);
     if (nmatch == 0) {
-      a.count[w] = 0; a.bytes[w] = 0; a.flags[w] = A5X_WF_RADIX;
+      a.count[w] = 0; a.bytes[w] = 0; a.flags[w] = A5X_WF_RADIX | A5X_WF_FAST;
     } else if (!conflict && freew && !ovf && P <= (1ull << 32) && maxl <= A5X_RING_A - 16) {
       bool o2 = false;
       const u64 cnt = P - 1;
@@ -231,7 +241,11 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
         atomicOr(a.err, A5X_DERR_OVF);
       } else {
         a.count[w] = cnt; a.bytes[w] = byt;
-        a.flags[w] = A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u);
+        npiece += lit_pieces(L - pend + 1);  // tail + '\n'
+        const bool fast = maxnv <= 3 && maxcl <= 4 && npiece <= 32;
+        if (!fast) atomicAdd(a.nslow, 1u);
+        a.flags[w] = A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u) | (fast ? A5X_WF_FAST : 0u) | (nmatch << 16) |
+                     (fast ? npiece << 24 : 0u);
       }
     } else {
       a.flags[w] = A5X_WF_DEFER;
@@ -497,11 +511,12 @@ __global__ void __launch_bounds__(64) k_keyspace_wave(KsArgs a) {
     const u32 w = a.defer_list[i];
     WordInfo I = wave_setup<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>(S, T, a.words, a.woff, w, a.mn, a.mx);
     if (lane_id() == 0) {
-      u32 f = I.cls ? I.cls : (u32)A5X_WF_RADIX;
+      u32 f = I.cls ? I.cls : (u32)(A5X_WF_RADIX | A5X_WF_FAST);
       // would pass A (smaller LDS budget) handle it?
       bool fitsA = I.L <= A5X_LMAX_A && I.nmatch <= A5X_MLMAX_A && I.maxlen <= A5X_RING_A - 16 &&
                    (I.cls != A5X_WF_GENERAL || (u64)(I.nev + 1) * I.W <= A5X_DPENT_A);
       if (I.cls && !fitsA) { f |= A5X_WF_BIG; atomicAdd(a.nbig, 1u); }
+      else if (I.cls) atomicAdd(a.nslow, 1u);
       if (I.cls && (!I.fits || I.maxlen > A5X_RING_B - 16)) {
         f |= A5X_WF_ERR_BIG | ((I.fits ? 5u : I.why) << 16) | (min(I.W, 255u) << 24);
         atomicOr(a.err, A5X_DERR_BIG);
@@ -601,15 +616,19 @@ __global__ void __launch_bounds__(SCAN_BLOCK) k_scan_down(const u64* ca, const u
 // ---------------------------------------------------------------------------
 // Chunk planner: chunk c covers global candidates [c*CH, (c+1)*CH)
 // ---------------------------------------------------------------------------
+// chunk_kind[c] bit 0: the chunk holds candidates of a slow (non-FAST) word,
+// bit 1: of a BIG word.  Only written when such words exist (host zeroes it).
 __global__ void __launch_bounds__(256) k_plan(const u64* cand_off, const u32* flags, u64 nw, u64 CH, u32* chunk_w0,
-                                              u32* chunk_big) {
+                                              u32* chunk_kind) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
     const u64 a = cand_off[w], b = cand_off[w + 1];
     if (b <= a) continue;
     for (u64 c = (a + CH - 1) / CH; c * CH < b; c++) chunk_w0[c] = (u32)w;
-    if (flags[w] & A5X_WF_BIG)
-      for (u64 c = a / CH; c * CH < b; c++) chunk_big[c] = 1;
+    const u32 f = flags[w];
+    const u32 kind = (f & A5X_WF_BIG) ? 2u : ((f & A5X_WF_FAST) ? 0u : 1u);
+    if (kind)
+      for (u64 c = a / CH; c * CH < b; c++) atomicOr(&chunk_kind[c], kind);
   }
 }
 
@@ -626,14 +645,28 @@ struct ExpArgs {
   const u64* byte_off;   // n+1, exclusive prefix of bytes
   const u32* flags;
   const u32* chunk_w0;
-  const u32* chunk_big;
+  const u32* chunk_kind;
   u64 cand_begin, cand_end;  // global candidate range of this call
   u64 CH;
   uint8_t* out;
   u64 out_base;          // byte_off value that maps to out[0]
+  u64 out_cap;           // bytes writable at out
   int mn, mx;
   u32* err;
+  u64* dbg;              // 8-word debug record of the first tripped guard
 };
+
+// Record the first tripped guard (code + context) and flag the call as failed.
+// Takes the two pointers (not the argument struct) so the kernel arguments are
+// never spilled to scratch.
+__device__ __forceinline__ void guard_trip2(u32* err, u64* dbg, u64 code, u64 x0, u64 x1, u64 x2, u64 x3) {
+  atomicOr(err, A5X_DERR_GUARD);
+  if (atomicCAS((unsigned long long*)dbg, 0ull, (unsigned long long)code) == 0ull) {
+    dbg[1] = x0; dbg[2] = x1; dbg[3] = x2; dbg[4] = x3;
+    dbg[5] = blockIdx.x; dbg[6] = threadIdx.x;
+  }
+}
+#define guard_trip(A, code, x0, x1, x2, x3) guard_trip2((A).err, (A).dbg, code, x0, x1, x2, x3)
 
 // Per-lane byte emitter: bytes are OR-ed into an all-zero LDS ring at their
 // final positions (ring index = byte offset relative to the run base).
@@ -681,23 +714,26 @@ struct Run {
   bool open;
 };
 
-template <u32 RING>
-__device__ __forceinline__ void store_block(uint8_t* out, u64 X, uint4 v, u64 lo, u64 hi) {
-  // block [X, X+16) restricted to bytes [lo, hi)
+__device__ __forceinline__ void store_block(const ExpArgs& a, u64 X, uint4 v, u64 lo, u64 hi) {
+  // block [X, X+16) restricted to bytes [lo, hi); never beyond out_cap
+  if (hi > a.out_cap || X + 16 <= lo) {
+    guard_trip(a, 1, X, lo, hi, a.out_cap);
+    return;
+  }
   if (X >= lo && X + 16 <= hi) {
-    *(uint4*)(out + X) = v;
+    *(uint4*)(a.out + X) = v;
   } else {
     const u32 wv[4] = {v.x, v.y, v.z, v.w};
     for (u32 b = 0; b < 16; b++) {
       const u64 Y = X + b;
-      if (Y >= lo && Y < hi) out[Y] = (uint8_t)(wv[b >> 2] >> (8 * (b & 3)));
+      if (Y >= lo && Y < hi) a.out[Y] = (uint8_t)(wv[b >> 2] >> (8 * (b & 3)));
     }
   }
 }
 
 // stream complete blocks [flushed, upto) (upto 16-aligned) and zero them in the ring
 template <u32 RING>
-__device__ __forceinline__ void run_flush(Run& R, u32* ring, uint8_t* out, u64 upto, u64 hi) {
+__device__ __forceinline__ void run_flush(Run& R, u32* ring, const ExpArgs& a, u64 upto, u64 hi) {
   const u32 lane = lane_id();
   const u64 nb = (upto - R.flushed) / 16;
   for (u64 b = lane; b < nb; b += 64) {
@@ -705,18 +741,18 @@ __device__ __forceinline__ void run_flush(Run& R, u32* ring, uint8_t* out, u64 u
     uint4* rp = (uint4*)ring + (((X - R.base) / 16) & (RING / 16 - 1));
     const uint4 v = *rp;
     *rp = make_uint4(0, 0, 0, 0);
-    store_block<RING>(out, X, v, R.lo, hi);
+    store_block(a, X, v, R.lo, hi);
   }
   R.flushed = upto;
   WAVE_SYNC();
 }
 
 template <u32 RING>
-__device__ __forceinline__ void run_close(Run& R, u32* ring, uint8_t* out) {
+__device__ __forceinline__ void run_close(Run& R, u32* ring, const ExpArgs& a) {
   if (!R.open) return;
   const u64 full = R.pos & ~15ull;
-  if (full > R.flushed) run_flush<RING>(R, ring, out, full, R.pos);
-  if (R.pos > R.flushed) run_flush<RING>(R, ring, out, R.flushed + 16, R.pos);  // partial tail block
+  if (full > R.flushed) run_flush<RING>(R, ring, a, full, R.pos);
+  if (R.pos > R.flushed) run_flush<RING>(R, ring, a, R.flushed + 16, R.pos);  // partial tail block
   R.open = false;
 }
 
@@ -835,144 +871,452 @@ __device__ u64 dp_prefix_bytes(const WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& 
   return acc;
 }
 
-template <int LMAX, int MLMAX, int DPENT, u32 RING, bool PASSB>
-__device__ void expand_chunk(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab& T, const ExpArgs& a, u64 chunk) {
+// One word (any class) through the per-word path: wave_setup in LDS, then rounds of
+// up to 64 candidates (radix digits or the DP walk).  Candidates [r, r+nhere).
+template <int LMAX, int MLMAX, int DPENT, u32 RING>
+__device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab& T, const ExpArgs& a, Run& R,
+                            u64 w, u64 r, u64 nhere, u64 cnt) {
+  const u32 lane = lane_id();
+  WordInfo I = wave_setup<LMAX, MLMAX, DPENT>(S, T, a.words, a.woff, w, a.mn, a.mx);
+  if (!I.fits || I.count != cnt || I.maxlen > RING - 16) {
+    if (lane == 0) atomicOr(a.err, A5X_DERR_STATE);
+    return false;
+  }
+  u64 pos = a.byte_off[w] - a.out_base;
+  if (r) {
+    if (I.cls & A5X_WF_RADIX) pos += radix_prefix_bytes(S, T, I, r);
+    else pos += uniform64(dp_prefix_bytes(S, T, I, r));
+  }
+  if (!R.open || R.pos != pos) {
+    run_close<RING>(R, ring, a);
+    run_open<RING>(R, pos);
+  }
+  // lanes per round: the ring holds at most RING-16 unflushed bytes
+  const u32 nl = min(64u, (RING - 16) / I.maxlen);
+  const u64 rend = r + nhere;
+  for (u64 rr = r; rr < rend; rr += nl) {
+    const bool act = lane < nl && rr + lane < rend;
+    const u64 rk = rr + lane;
+    u32 len = 0;
+    Emit e;
+    if (I.cls & A5X_WF_RADIX) {
+      const u32 idx = (u32)(rk + 1);
+      if (act) {
+        int l = (int)I.L + 1;
+        u32 n = idx;
+        for (u32 i = 0; i < I.nslots; i++) {
+          const Slot& sl = S.slots[i];
+          const u32 q = fastdiv(n, sl.magic, sl.shift);
+          const u32 d = n - q * sl.R;
+          n = q;
+          if (d) l += (int)T.ch[sl.choice_base + d].len - (int)sl.klen;
+        }
+        len = (u32)l;
+      }
+      const u32 incl = wave_incl_scan_u32(len);
+      const u32 tot = __shfl((int)incl, 63);
+      const u64 off = R.pos + incl - len - R.base;
+      if (act) {
+        e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
+        u32 prev = 0, n = idx;
+        for (u32 i = 0; i < I.nslots; i++) {
+          const Slot& sl = S.slots[i];
+          const u32 q = fastdiv(n, sl.magic, sl.shift);
+          const u32 d = n - q * sl.R;
+          n = q;
+          if (sl.pos > prev) em_bytes<RING>(e, ring, S.wbuf, prev, sl.pos - prev);
+          em_choice<RING>(e, ring, T, sl.choice_base + d);
+          prev = sl.pos + sl.klen;
+        }
+        if (I.L > prev) em_bytes<RING>(e, ring, S.wbuf, prev, I.L - prev);
+        em_put<RING>(e, ring, '\n', 1);
+        em_finish<RING>(e, ring);
+      }
+      R.pos += tot;
+    } else {
+      if (act) len = dp_walk<false, RING>(S, T, I, rk, e, ring);
+      const u32 incl = wave_incl_scan_u32(len);
+      const u32 tot = __shfl((int)incl, 63);
+      const u64 off = R.pos + incl - len - R.base;
+      if (act) {
+        e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
+        dp_walk<true, RING>(S, T, I, rk, e, ring);
+        em_finish<RING>(e, ring);
+      }
+      R.pos += tot;
+    }
+    WAVE_SYNC();
+    const u64 full = R.pos & ~15ull;
+    if (full > R.flushed) run_flush<RING>(R, ring, a, full, R.pos);
+  }
+  WAVE_SYNC();
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// k_expand_fast: windows of consecutive FAST words (radix, <= 64 B, fanout <= 3).
+// Lane j holds word (w+j)'s offsets; the window's bytes are staged in LDS with
+// dword loads; lanes (one per word) cut each word into slots and precombine, per
+// (slot, digit), the literal run before the slot with the chosen value into one
+// <= 4-byte piece.  Rounds of 64 consecutive candidates then span word
+// boundaries: pass 1 = one division + one LDS read per slot (2-bit digits kept
+// packed), wave scan of lengths, pass 2 = one piece read + one emit per slot.
+// Non-FAST words are holes, written by k_expand_slow / k_expand_b.
+// ---------------------------------------------------------------------------
+#define FW_WB 512   // window word-byte budget
+#define FW_WS 64    // window radix-slot budget
+#define FW_WP 96    // window piece budget
+#define FW_WW 32    // window word budget
+#define FW_RING 4096
+
+struct FSlot {        // 16 B, one per radix slot
+  u32 magic;
+  uint8_t shift, R, ps, pad0;  // ps: piece index (within the word) the digit selects
+  u32 plen4;          // length of piece ps for digit d in byte d
+  u32 pad1;
+};
+struct FPiece {       // 8 B: <= 4 bytes of output for one digit value
+  u32 b4;
+  u32 len;
+};
+struct FWord {        // 32 B
+  uint16_t sbase, ns, pbase, np;
+  u32 lconst;         // bytes of the digit-independent pieces (literals, tail, '\n')
+  u32 pad;
+  u64 c0;             // first global candidate index of the word
+  u64 pad2;
+};
+struct FWin {
+  u32 bytes32[(FW_WB + 32) / 4];
+  FSlot slots[FW_WS];
+  FPiece pieces[FW_WP * 4];
+  FWord words[FW_WW];
+};
+
+// Branch-free emit of a <= 4-byte piece: OR the (growing) low dword every time --
+// OR is idempotent -- and advance when it is complete.
+__device__ __forceinline__ void put4(Emit& e, u32* ring, u32 b4, u32 len) {
+  e.acc |= (u64)b4 << (8u * e.n);
+  e.n += len;
+  atomicOr(&ring[e.dw & (FW_RING / 4 - 1)], (u32)e.acc);
+  const bool adv = e.n >= 4;
+  e.dw += adv ? 1u : 0u;
+  e.acc = adv ? (e.acc >> 32) : e.acc;
+  e.n -= adv ? 4u : 0u;
+}
+
+// window setup helper: write literal bytes [off, off+m) as 4-byte literal pieces
+__device__ __forceinline__ u32 add_lit_pieces(FWin& F, const uint8_t* wbytes, u32 pi, u32 off, u32 m, u32 tailnl) {
+  // tailnl: append '\n' after the run (word tail)
+  const u32 total = m + tailnl;
+  for (u32 k = 0; k < total; k += 4) {
+    const u32 n = min(4u, total - k);
+    u32 v = 0;
+    if (k < m) v = keep_bytes(lds_ld4(wbytes, off + k), min(n, m - k));
+    if (tailnl && k + n == total) v |= 10u << (8 * (n - 1));
+    FPiece P;
+    P.b4 = v; P.len = n;
+    if (pi < FW_WP) F.pieces[pi * 4] = P;
+    pi++;
+  }
+  return pi;
+}
+
+__device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
   const u64 g0 = max(a.cand_begin, chunk * a.CH);
   const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
   if (g0 >= g1) return;
   u64 w = a.chunk_w0[chunk];
-  // the chunk map gives the word holding chunk*CH; advance to the one holding g0
-  while (a.cand_off[w + 1] <= g0) w++;
+  if (w >= a.nw) { guard_trip(a, 2, chunk, w, g0, a.nw); return; }
+  while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
+  if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
+  u64 g = g0;
+  Run R;
+  R.open = false;
+  const uint8_t* wbytes = (const uint8_t*)F.bytes32;
+  while (g < g1) {
+    if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
+    // ---- window metadata: lane j <-> word w + j ----
+    const u64 wl = w + lane;
+    const bool inb = lane < FW_WW && wl < a.nw;
+    const u64 c0 = inb ? a.cand_off[wl] : ~0ull;
+    const u64 c1 = inb ? a.cand_off[wl + 1] : ~0ull;
+    const u64 ws = inb ? a.woff[wl] : 0;
+    const u64 we = inb ? a.woff[wl + 1] : 0;
+    const u32 fl = inb ? a.flags[wl] : 0u;
+    const bool fast = inb && (fl & A5X_WF_FAST) && c0 < g1;
+    const u32 L = fast ? (u32)(we - ws) : 0u;
+    const u32 ns = fast ? (fl >> 16) & 255u : 0u;
+    const u32 np = fast ? (fl >> 24) & 63u : 0u;
+    const u32 incL = wave_incl_scan_u32(L);
+    const u32 incS = wave_incl_scan_u32(ns);
+    const u32 incP = wave_incl_scan_u32(np);
+    const bool ok = fast && incL + 3 <= FW_WB && incS <= FW_WS && incP <= FW_WP;
+    const u64 badm = __ballot(!ok);
+    const u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
+    if (k == 0) {
+      // word w is a hole here (slow / BIG) or empty
+      const u64 w0c1 = uniform64(c1);
+      if (w0c1 > g) {
+        run_close<FW_RING>(R, ring, a);
+        g = min(w0c1, g1);
+      }
+      w++;
+      continue;
+    }
+    // ---- window bytes -> LDS (aligned dwords) ----
+    const u64 A0 = uniform64(ws) & ~3ull;
+    const u64 Aend = uniform64(shfl_u64(we, (int)k - 1));
+    if (Aend < A0 || Aend - A0 > FW_WB || w + k > a.nw) {
+      guard_trip(a, 5, chunk, w, k, Aend - A0);
+      break;
+    }
+    const u32 ndw = (u32)((Aend - A0 + 3) / 4);
+    const u32* src = (const u32*)(a.words + A0);
+    for (u32 i = lane; i < ndw + 2; i += 64) F.bytes32[i] = i < ndw ? src[i] : 0u;
+    WAVE_SYNC();
+    // ---- slots + pieces, lane per word (words without candidates have none) ----
+    u32 maxl = 0;
+    if (lane < k && ns) {
+      const u32 off = (u32)(ws - A0);
+      const u32 pbase = incP - np;
+      u32 si = incS - ns, pi = pbase, prev = 0, mlen = 0, lconst = 0;
+      for (u32 p = 0; p < L; p++) {
+        const u32 b = wbytes[off + p];
+        const u32 ks = T.bucket[b], ke = T.bucket[b + 1];
+        for (u32 kk = ks; kk < ke; kk++) {
+          const A5xKey key = T.keys[kk];
+          if (p + key.klen > L) continue;
+          bool m = true;
+          const A5xChoice ck = T.ch[key.choice_base];
+          for (u32 i = 1; i < key.klen && m; i++) {
+            const u32 kb = i < 4 ? ((ck.first4 >> (8 * i)) & 255u) : T.blob[ck.blob_off + i];
+            m = wbytes[off + p + i] == kb;
+          }
+          if (!m) continue;
+          const u32 run = p - prev;
+          u32 lit = 0, lit4 = 0;
+          if (run + key.maxclen <= 4) {
+            lit = run;
+            lit4 = run ? keep_bytes(lds_ld4(wbytes, off + prev), run) : 0u;
+          } else {
+            const u32 pi0 = pi;
+            pi = add_lit_pieces(F, wbytes, pi, off + prev, run, 0);
+            lconst += run;
+            (void)pi0;
+          }
+          u32 plen4 = 0, pm = 0;
+          for (u32 d = 0; d <= key.nvals; d++) {
+            const A5xChoice c = T.ch[key.choice_base + d];
+            FPiece P;
+            P.len = lit + c.len;
+            P.b4 = lit4 | (lit < 4 ? (c.first4 << (8 * lit)) : 0u);
+            if (pi < FW_WP) F.pieces[pi * 4 + d] = P;
+            plen4 |= P.len << (8 * d);
+            pm = max(pm, P.len);
+          }
+          if (si < FW_WS) {
+            FSlot sl;
+            sl.magic = key.magic; sl.shift = (uint8_t)key.shift; sl.R = (uint8_t)(key.nvals + 1u);
+            sl.ps = (uint8_t)(pi - pbase); sl.pad0 = 0; sl.plen4 = plen4; sl.pad1 = 0;
+            F.slots[si] = sl;
+          }
+          si++;
+          pi++;
+          mlen += pm;
+          prev = p + key.klen;
+          p += key.klen - 1;
+          break;  // radix words: exactly one match here and none inside it
+        }
+      }
+      pi = add_lit_pieces(F, wbytes, pi, off + prev, L - prev, 1);
+      lconst += L - prev + 1;
+      FWord fw;
+      fw.sbase = (uint16_t)(incS - ns); fw.ns = (uint16_t)ns;
+      fw.pbase = (uint16_t)pbase; fw.np = (uint16_t)np;
+      fw.lconst = lconst; fw.pad = 0; fw.pad2 = 0;
+      fw.c0 = c0;
+      F.words[lane] = fw;
+      if (si != incS || pi != incP) atomicOr(a.err, A5X_DERR_STATE);
+      maxl = mlen + lconst;
+    }
+    const u32 winmax = wave_max_u32(maxl);
+    WAVE_SYNC();
+    // ---- run position of g ----
+    const u64 r0 = g - uniform64(c0);
+    u64 pos = uniform64(a.byte_off[w]) - a.out_base;
+    if (r0) {
+      // closed-form prefix bytes of candidates [0, r0) of word w (lanes over its slots)
+      const FWord f0 = F.words[0];
+      const u64 Y = r0 + 1;
+      u64 Rl = 1;
+      FSlot sl;
+      if (lane < f0.ns) { sl = F.slots[f0.sbase + lane]; Rl = sl.R; }
+      u64 inc = Rl;  // inclusive prefix product of R over slots
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const u64 y = shfl_up_u64(inc, d);
+        if ((int)lane >= d) inc *= y;
+      }
+      i64 part = 0, base0 = 0;
+      if (lane < f0.ns) {
+        const u64 Q = inc / Rl, full = Y / inc, rem = Y % inc;
+        const int l0 = (int)(sl.plen4 & 255u);
+        base0 = l0;
+        for (u32 v = 1; v < sl.R; v++) {
+          const u64 lo = (u64)v * Q;
+          const u64 cnt = full * Q + (rem > lo ? min(Q, rem - lo) : 0);
+          part += ((i64)((sl.plen4 >> (8 * v)) & 255u) - l0) * (i64)cnt;
+        }
+      }
+      // every candidate = lconst + digit-0 piece lengths + deltas
+      const i64 lbase = wave_sum_i64(base0) + f0.lconst;
+      pos += (u64)((i64)r0 * lbase + wave_sum_i64(part));
+    }
+    if (!R.open || R.pos != pos) {
+      run_close<FW_RING>(R, ring, a);
+      run_open<FW_RING>(R, pos);
+    }
+    // ---- rounds ----
+    const u64 gend = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
+    const u32 nl = uniform(min(64u, (FW_RING - 16) / max(winmax, 1u)));
+    const u32 c1rel = (lane < k) ? (u32)(c1 - g) : 0xffffffffu;  // chunk-relative ends
+    for (u64 rr = g; rr < gend; rr += nl) {
+      const u32 grel = (u32)(rr - g) + lane;
+      const bool act = lane < nl && rr + lane < gend;
+      // word of the candidate: first j < k with c1rel_j > grel
+      u32 lo = 0, hi = k - 1;
+#pragma unroll
+      for (int it = 0; it < 5; it++) {
+        const u32 mid = (lo + hi) >> 1;
+        const u32 v = (u32)__shfl((int)c1rel, (int)mid);
+        if (lo < hi) { if (v <= grel) lo = mid + 1; else hi = mid; }
+      }
+      const FWord fw = F.words[lo];
+      u32 len = 0;
+      u64 dig = 0;
+      if (act) {
+        u32 n = (u32)(rr + lane - fw.c0 + 1);
+        len = fw.lconst;
+        for (u32 i = 0; i < fw.ns; i++) {
+          const FSlot sl = F.slots[fw.sbase + i];
+          const u32 q = fastdiv(n, sl.magic, sl.shift);
+          const u32 d = n - q * sl.R;
+          n = q;
+          dig |= (u64)d << (2 * sl.ps);
+          len += (sl.plen4 >> (8 * d)) & 255u;
+        }
+      }
+      const u32 incl = wave_incl_scan_u32(len);
+      const u32 tot = uniform((u32)__shfl((int)incl, 63));
+      if (act) {
+        const u64 off = R.pos + incl - len - R.base;
+        Emit e;
+        e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
+        const FPiece* pp = F.pieces + fw.pbase * 4;
+        for (u32 i = 0; i < fw.np; i++) {
+          const u32 d = (u32)(dig >> (2 * i)) & 3u;
+          const FPiece P = pp[i * 4 + d];
+          put4(e, ring, P.b4, P.len);
+        }
+        if (e.n) atomicOr(&ring[e.dw & (FW_RING / 4 - 1)], (u32)e.acc);
+      }
+      R.pos += tot;
+      WAVE_SYNC();
+      const u64 full = R.pos & ~15ull;
+      if (full > R.flushed) run_flush<FW_RING>(R, ring, a, full, R.pos);
+    }
+    g = gend;
+    w += k;
+    WAVE_SYNC();
+  }
+  run_close<FW_RING>(R, ring, a);
+}
+
+__device__ __forceinline__ u32 lds_per_wave_fast() { return (FW_RING + (u32)sizeof(FWin) + 15u) & ~15u; }
+
+__global__ void __launch_bounds__(256) k_expand_fast(ExpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  load_table(smem, a.table, a.table_bytes);
+  const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
+  const u32 tb = (a.table_bytes + 15u) & ~15u;
+  uint8_t* mine = smem + tb + wv * lds_per_wave_fast();
+  u32* ring = (u32*)mine;
+  FWin& F = *(FWin*)(mine + FW_RING);
+  for (u32 i = lane_id(); i < FW_RING / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
+  if (chunk * a.CH >= a.cand_end) return;
+  expand_chunk_fast(F, ring, T, a, chunk);
+}
+
+// k_expand_slow: non-FAST, non-BIG words (overlapping keys, capped windows,
+// fanout > 3, ...) one word at a time through wave_setup; everything else is a hole.
+template <int LMAX, int MLMAX, int DPENT, u32 RING>
+__device__ void expand_chunk_kind(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab& T, const ExpArgs& a,
+                                  u64 chunk, bool bigpass) {
+  const u64 g0 = max(a.cand_begin, chunk * a.CH);
+  const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
+  if (g0 >= g1) return;
+  u64 w = a.chunk_w0[chunk];
+  if (w >= a.nw) { guard_trip(a, 2, chunk, w, g0, a.nw); return; }
+  while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
+  if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
   u64 r = g0 - a.cand_off[w];
   u64 g = g0;
   Run R;
   R.open = false;
   while (g < g1) {
+    if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
     const u64 cnt = a.cand_off[w + 1] - a.cand_off[w];
     if (cnt == 0) { w++; continue; }
     const u64 nhere = min(cnt - r, g1 - g);
     const u32 fl = a.flags[w];
-    const bool mine = PASSB ? (fl & A5X_WF_BIG) != 0 : (fl & A5X_WF_BIG) == 0;
+    const bool mine = bigpass ? (fl & A5X_WF_BIG) != 0 : !(fl & (A5X_WF_BIG | A5X_WF_FAST));
     if (!mine) {
-      run_close<RING>(R, ring, a.out);
-      g += nhere; w++; r = 0;
-      continue;
-    }
-    WordInfo I = wave_setup<LMAX, MLMAX, DPENT>(S, T, a.words, a.woff, w, a.mn, a.mx);
-    if (!I.fits || I.count != cnt || I.maxlen > RING - 16) {
-      if (lane == 0) atomicOr(a.err, A5X_DERR_STATE);
-      run_close<RING>(R, ring, a.out);
-      return;
-    }
-    u64 pos = a.byte_off[w] - a.out_base;
-    if (r) {
-      if (I.cls & A5X_WF_RADIX) pos += radix_prefix_bytes(S, T, I, r);
-      else pos += uniform64(dp_prefix_bytes(S, T, I, r));
-    }
-    if (!R.open || R.pos != pos) {
-      run_close<RING>(R, ring, a.out);
-      run_open<RING>(R, pos);
-    }
-    // lanes per round: the ring holds at most RING-16 unflushed bytes
-    const u32 nl = min(64u, (RING - 16) / I.maxlen);
-    const u64 rend = r + nhere;
-    for (u64 rr = r; rr < rend; rr += nl) {
-      const bool act = lane < nl && rr + lane < rend;
-      const u64 rk = rr + lane;
-      u32 len = 0;
-      Emit e;
-      if (I.cls & A5X_WF_RADIX) {
-        const u32 idx = (u32)(rk + 1);
-        if (act) {
-          if (I.cls & A5X_WF_BIN) {
-            if (I.udelta != INT32_MIN) {
-              len = I.L + 1 + (u32)((int)__popc(idx) * I.udelta);
-            } else {
-              int l = (int)I.L + 1;
-              for (u32 i = 0; i < I.nslots; i++) l += ((idx >> i) & 1u) ? S.slots[i].delta1 : 0;
-              len = (u32)l;
-            }
-          } else {
-            int l = (int)I.L + 1;
-            u32 n = idx;
-            for (u32 i = 0; i < I.nslots; i++) {
-              const Slot& sl = S.slots[i];
-              const u32 q = fastdiv(n, sl.magic, sl.shift);
-              const u32 d = n - q * sl.R;
-              n = q;
-              if (d) l += (int)T.ch[sl.choice_base + d].len - (int)sl.klen;
-            }
-            len = (u32)l;
-          }
-        }
-        const u32 incl = wave_incl_scan_u32(len);
-        const u32 tot = __shfl((int)incl, 63);
-        const u64 off = R.pos + incl - len - R.base;
-        if (act) {
-          e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
-          u32 prev = 0, n = idx;
-          for (u32 i = 0; i < I.nslots; i++) {
-            const Slot& sl = S.slots[i];
-            u32 d;
-            if (I.cls & A5X_WF_BIN) d = (idx >> i) & 1u;
-            else { const u32 q = fastdiv(n, sl.magic, sl.shift); d = n - q * sl.R; n = q; }
-            if (sl.pos > prev) em_bytes<RING>(e, ring, S.wbuf, prev, sl.pos - prev);
-            em_choice<RING>(e, ring, T, sl.choice_base + d);
-            prev = sl.pos + sl.klen;
-          }
-          if (I.L > prev) em_bytes<RING>(e, ring, S.wbuf, prev, I.L - prev);
-          em_put<RING>(e, ring, '\n', 1);
-          em_finish<RING>(e, ring);
-        }
-        R.pos += tot;
-      } else {
-        if (act) len = dp_walk<false, RING>(S, T, I, rk, e, ring);
-        const u32 incl = wave_incl_scan_u32(len);
-        const u32 tot = __shfl((int)incl, 63);
-        const u64 off = R.pos + incl - len - R.base;
-        if (act) {
-          e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
-          dp_walk<true, RING>(S, T, I, rk, e, ring);
-          em_finish<RING>(e, ring);
-        }
-        R.pos += tot;
-      }
-      WAVE_SYNC();
-      const u64 full = R.pos & ~15ull;
-      if (full > R.flushed) run_flush<RING>(R, ring, a.out, full, R.pos);
+      run_close<RING>(R, ring, a);
+    } else if (!expand_word<LMAX, MLMAX, DPENT, RING>(S, ring, T, a, R, w, r, nhere, cnt)) {
+      break;
     }
     g += nhere; w++; r = 0;
-    WAVE_SYNC();
   }
-  run_close<RING>(R, ring, a.out);
+  run_close<RING>(R, ring, a);
 }
 
-template <int LMAX, int MLMAX, int DPENT, u32 RING, bool PASSB>
-__device__ void expand_body(const ExpArgs& a) {
+__device__ __forceinline__ u32 lds_per_wave_slow() { return (A5X_RING_A + (u32)sizeof(LdsA) + 15u) & ~15u; }
+
+__global__ void __launch_bounds__(256) k_expand_slow(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   load_table(smem, a.table, a.table_bytes);
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   const u32 tb = (a.table_bytes + 15u) & ~15u;
-  const u32 per = (u32)((sizeof(WaveLds<LMAX, MLMAX, DPENT>) + RING + 15u) & ~15u);
-  uint8_t* mine = smem + tb + wv * per;
+  uint8_t* mine = smem + tb + wv * lds_per_wave_slow();
   u32* ring = (u32*)mine;
-  WaveLds<LMAX, MLMAX, DPENT>& S = *(WaveLds<LMAX, MLMAX, DPENT>*)(mine + RING);
-  for (u32 i = lane_id(); i < RING / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+  LdsA& S = *(LdsA*)(mine + A5X_RING_A);
+  for (u32 i = lane_id(); i < A5X_RING_A / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   const Tab T = tab_view(smem);
-  const u64 c0 = a.cand_begin / a.CH;
-  const u64 chunk = c0 + (u64)blockIdx.x * nwv + wv;
+  const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
   if (chunk * a.CH >= a.cand_end) return;
-  if (PASSB && !a.chunk_big[chunk]) return;
-  expand_chunk<LMAX, MLMAX, DPENT, RING, PASSB>(S, ring, T, a, chunk);
+  if (!(a.chunk_kind[chunk] & 1u)) return;
+  expand_chunk_kind<A5X_LMAX_A, A5X_MLMAX_A, A5X_DPENT_A, A5X_RING_A>(S, ring, T, a, chunk, false);
 }
 
-__global__ void __launch_bounds__(256) k_expand_a(ExpArgs a) {
-  expand_body<A5X_LMAX_A, A5X_MLMAX_A, A5X_DPENT_A, A5X_RING_A, false>(a);
-}
 __global__ void __launch_bounds__(64) k_expand_b(ExpArgs a) {
-  expand_body<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B, A5X_RING_B, true>(a);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  load_table(smem, a.table, a.table_bytes);
+  const u32 tb = (a.table_bytes + 15u) & ~15u;
+  u32* ring = (u32*)(smem + tb);
+  LdsB& S = *(LdsB*)(smem + tb + A5X_RING_B);
+  for (u32 i = lane_id(); i < A5X_RING_B / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  const u64 chunk = a.cand_begin / a.CH + blockIdx.x;
+  if (chunk * a.CH >= a.cand_end) return;
+  if (!(a.chunk_kind[chunk] & 2u)) return;
+  expand_chunk_kind<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B, A5X_RING_B>(S, ring, T, a, chunk, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -1052,7 +1396,7 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   KsArgs a;
   a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
   a.mn = L.mn; a.mx = L.mx; a.count = L.count; a.bytes = L.bytes; a.flags = L.flags;
-  a.defer_list = L.defer_list; a.defer_n = L.defer_n; a.nbig = L.nbig; a.err = L.err;
+  a.defer_list = L.defer_list; a.defer_n = L.defer_n; a.nbig = L.nbig; a.nslow = L.nslow; a.err = L.err;
   hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, 256, 65536)), dim3(256), L.table_bytes, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1091,10 +1435,10 @@ hipError_t a5x_launch_scan(const u64* ca, const u64* cb, u64 n, u64* outa, u64* 
   return hipGetLastError();
 }
 
-hipError_t a5x_launch_plan(const u64* cand_off, const u32* flags, u64 nw, u64 CH, u32* chunk_w0, u32* chunk_big,
+hipError_t a5x_launch_plan(const u64* cand_off, const u32* flags, u64 nw, u64 CH, u32* chunk_w0, u32* chunk_kind,
                            hipStream_t st) {
   hipLaunchKernelGGL(k_plan, dim3(blocks_for(nw, 256, 65536)), dim3(256), 0, st, cand_off, flags, nw, CH, chunk_w0,
-                     chunk_big);
+                     chunk_kind);
   return hipGetLastError();
 }
 
@@ -1102,29 +1446,32 @@ static ExpArgs exp_args(const A5xExpLaunch& L) {
   ExpArgs a;
   a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
   a.cand_off = L.cand_off; a.byte_off = L.byte_off; a.flags = L.flags; a.chunk_w0 = L.chunk_w0;
-  a.chunk_big = L.chunk_big; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.out = L.out;
-  a.out_base = L.out_base; a.mn = L.mn; a.mx = L.mx; a.err = L.err;
+  a.chunk_kind = L.chunk_kind; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.out = L.out;
+  a.out_base = L.out_base; a.out_cap = L.out_cap; a.mn = L.mn; a.mx = L.mx; a.err = L.err; a.dbg = L.dbg;
   return a;
 }
 
-size_t a5x_expand_lds(u32 table_bytes, int passb, u32 waves) {
+size_t a5x_expand_lds(u32 table_bytes, int kind, u32 waves) {
   const size_t tb = (table_bytes + 15u) & ~15u;
-  if (passb) return tb + ((sizeof(LdsB) + A5X_RING_B + 15u) & ~(size_t)15u);
-  return tb + waves * ((sizeof(LdsA) + A5X_RING_A + 15u) & ~(size_t)15u);
+  if (kind == 2) return tb + ((A5X_RING_B + sizeof(LdsB) + 15u) & ~(size_t)15u);
+  if (kind == 1) return tb + waves * ((A5X_RING_A + sizeof(LdsA) + 15u) & ~(size_t)15u);
+  return tb + waves * ((FW_RING + sizeof(FWin) + 15u) & ~(size_t)15u);
 }
 
-hipError_t a5x_launch_expand(const A5xExpLaunch& L, int passb, hipStream_t st) {
+// kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b
+hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   ExpArgs a = exp_args(L);
   const u64 c0 = L.cand_begin / L.CH, c1 = (L.cand_end + L.CH - 1) / L.CH;
   const u64 nchunks = c1 - c0;
   if (nchunks == 0) return hipSuccess;
-  if (!passb) {
-    const u32 waves = L.waves_per_block;
-    const u64 nb = (nchunks + waves - 1) / waves;
-    hipLaunchKernelGGL(k_expand_a, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);
-  } else {
-    hipLaunchKernelGGL(k_expand_b, dim3((u32)nchunks), dim3(64), a5x_expand_lds(L.table_bytes, 1, 1), st, a);
-  }
+  const u32 waves = L.waves_per_block;
+  const u64 nb = (nchunks + waves - 1) / waves;
+  if (kind == 0)
+    hipLaunchKernelGGL(k_expand_fast, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);
+  else if (kind == 1)
+    hipLaunchKernelGGL(k_expand_slow, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 1, waves), st, a);
+  else
+    hipLaunchKernelGGL(k_expand_b, dim3((u32)nchunks), dim3(64), a5x_expand_lds(L.table_bytes, 2, 1), st, a);
   return hipGetLastError();
 }
 
@@ -1147,5 +1494,7 @@ hipError_t a5x_set_kernel_attrs() {
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_locate, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_expand_a, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  e = hipFuncSetAttribute((const void*)k_expand_slow, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_expand_fast, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }

@@ -17,6 +17,7 @@ struct A5xKsLaunch {
   uint32_t* defer_list;
   uint32_t* defer_n;
   uint32_t* nbig;
+  uint32_t* nslow;
   uint32_t* err;
   uint32_t defer_blocks;
 };
@@ -31,13 +32,15 @@ struct A5xExpLaunch {
   const uint64_t* byte_off;
   const uint32_t* flags;
   const uint32_t* chunk_w0;
-  const uint32_t* chunk_big;
+  const uint32_t* chunk_kind;
   uint64_t cand_begin, cand_end;
   uint64_t CH;
   uint8_t* out;
   uint64_t out_base;
+  uint64_t out_cap;
   int mn, mx;
   uint32_t* err;
+  uint64_t* dbg;
   uint32_t waves_per_block;
 };
 
@@ -48,9 +51,10 @@ uint64_t a5x_scan_tmp_elems(uint64_t n);
 hipError_t a5x_launch_scan(const uint64_t* ca, const uint64_t* cb, uint64_t n, uint64_t* outa, uint64_t* outb,
                            uint64_t* tmp, uint32_t* err, hipStream_t st);
 hipError_t a5x_launch_plan(const uint64_t* cand_off, const uint32_t* flags, uint64_t nw, uint64_t CH,
-                           uint32_t* chunk_w0, uint32_t* chunk_big, hipStream_t st);
-size_t a5x_expand_lds(uint32_t table_bytes, int passb, uint32_t waves);
-hipError_t a5x_launch_expand(const A5xExpLaunch& L, int passb, hipStream_t st);
+                           uint32_t* chunk_w0, uint32_t* chunk_kind, hipStream_t st);
+size_t a5x_expand_lds(uint32_t table_bytes, int kind, uint32_t waves);
+// kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b (pass B)
+hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st);
 hipError_t a5x_launch_locate(const A5xExpLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out_bytes,
                              hipStream_t st);
 hipError_t a5x_launch_digest(const uint8_t* out, const uint64_t* byte_off, uint64_t out_base, uint64_t nw,

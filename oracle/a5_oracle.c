@@ -642,25 +642,28 @@ A5O_EXPORT int64_t a5o_expand_batch(const a5o_table *t, const uint8_t *words, co
 /* writer goroutine with a 4 KiB bufio.Writer doing WriteString(s + "\n").   */
 /* ------------------------------------------------------------------------ */
 #define CHAN_CAP 1000
+/* A buffered Go channel: one lock, a ring of CHAN_CAP, parked senders/receiver
+ * are woken only when someone actually waits (Go's runtime hands off the same
+ * way instead of signalling on every operation). */
 typedef struct {
     pthread_mutex_t mu; pthread_cond_t not_full, not_empty;
-    bstr q[CHAN_CAP]; size_t head, len; int closed;
+    bstr q[CHAN_CAP]; size_t head, len; int closed; int wait_send, wait_recv;
 } chan_t;
 
 static void chan_send(chan_t *c, bstr s) {
     pthread_mutex_lock(&c->mu);
-    while (c->len == CHAN_CAP) pthread_cond_wait(&c->not_full, &c->mu);
+    while (c->len == CHAN_CAP) { c->wait_send++; pthread_cond_wait(&c->not_full, &c->mu); c->wait_send--; }
     c->q[(c->head + c->len) % CHAN_CAP] = s; c->len++;
-    pthread_cond_signal(&c->not_empty);
+    if (c->wait_recv) pthread_cond_signal(&c->not_empty);
     pthread_mutex_unlock(&c->mu);
 }
 
 static int chan_recv(chan_t *c, bstr *s) {
     pthread_mutex_lock(&c->mu);
-    while (c->len == 0 && !c->closed) pthread_cond_wait(&c->not_empty, &c->mu);
+    while (c->len == 0 && !c->closed) { c->wait_recv++; pthread_cond_wait(&c->not_empty, &c->mu); c->wait_recv--; }
     if (c->len == 0) { pthread_mutex_unlock(&c->mu); return 0; }
     *s = c->q[c->head]; c->head = (c->head + 1) % CHAN_CAP; c->len--;
-    pthread_cond_signal(&c->not_full);
+    if (c->wait_send) pthread_cond_signal(&c->not_full);
     pthread_mutex_unlock(&c->mu);
     return 1;
 }
@@ -713,7 +716,11 @@ A5O_EXPORT int a5o_run_pipeline(const a5o_table *t, const uint8_t *words, const 
                                 uint64_t *out_cands, uint64_t *out_bytes) {
     pipe_job *j = (pipe_job *)calloc(1, sizeof(pipe_job));
     j->t = t; j->words = words; j->off = off; j->nw = nw; j->mode = mode; j->mn = mn; j->mx = mx; j->fd = fd;
-    pthread_mutex_init(&j->ch.mu, NULL); pthread_cond_init(&j->ch.not_full, NULL); pthread_cond_init(&j->ch.not_empty, NULL);
+    pthread_mutexattr_t ma;
+    pthread_mutexattr_init(&ma);
+    pthread_mutexattr_settype(&ma, PTHREAD_MUTEX_ADAPTIVE_NP);  /* spin, then park (like Go's runtime lock) */
+    pthread_mutex_init(&j->ch.mu, &ma);
+    pthread_mutexattr_destroy(&ma); pthread_cond_init(&j->ch.not_full, NULL); pthread_cond_init(&j->ch.not_empty, NULL);
     atomic_init(&j->next, 0); atomic_init(&j->err, 0);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;

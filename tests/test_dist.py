@@ -1,0 +1,82 @@
+"""Multi-rank path on CPU (gloo, world_size 2): balanced shards + counter all-reduce.
+
+Per rank, the oracle (C restatement) digests its shard; the all-reduced totals must
+equal the single-process totals -- the same reduction bench.py and the product use
+over RCCL on GPUs (no data-path collective: words are independent, main.go:77)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+
+from conftest import ROOT
+
+WORKER = r"""
+import os, sys, json
+sys.path.insert(0, {root!r})
+import numpy as np
+from hashcat_a5_table_generator_amd import dist as D, synth
+from oracle import c_oracle as co
+dist, rank, world, _ = D.init_from_env("gloo")
+tables, (data, offs) = synth.config_words("c3", 3000, seed=11)
+t = co.CTable([os.path.join({root!r}, "tests", "golden", "tables", x + ".table") for x in tables])
+dig = t.digest_batch(data, offs, 0, 0, 15, nthreads=1)
+prefix = np.zeros(len(offs), dtype=np.uint64); prefix[1:] = np.cumsum(dig[:, 1])
+w0, w1 = D.shard_bounds(prefix, world, rank)
+sd, so = D.shard_words(data, offs, w0, w1)
+mine = t.digest_batch(sd, so, 0, 0, 15, nthreads=1)
+tot = D.allreduce_u64(dist, [mine[:, 0].sum(), mine[:, 1].sum(), mine[:, 2].sum(dtype=np.uint64), w1 - w0], "gloo")
+ref = [dig[:, 0].sum(), dig[:, 1].sum(), dig[:, 2].sum(dtype=np.uint64), len(offs) - 1]
+out = dict(rank=rank, shard=[w0, w1], bytes=int(mine[:, 1].sum()), ok=[int(a) == int(b) for a, b in zip(tot, ref)])
+print(json.dumps(out), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_gloo_two_ranks_shard_and_reduce(tmp_path):
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=ROOT))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), A5X_DIST_BACKEND="gloo")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e[-2000:]
+        outs.append(o.strip().splitlines()[-1])
+    import json
+    res = sorted((json.loads(x) for x in outs), key=lambda d: d["rank"])
+    assert all(all(r["ok"]) for r in res), res
+    # contiguous, covering shards, balanced by output bytes
+    assert res[0]["shard"][0] == 0 and res[0]["shard"][1] == res[1]["shard"][0] and res[1]["shard"][1] == 3000
+    b0, b1 = res[0]["bytes"], res[1]["bytes"]
+    assert abs(b0 - b1) / (b0 + b1) < 0.05
+
+
+def test_partition_properties():
+    from hashcat_a5_table_generator_amd import partition
+    rng = np.random.default_rng(0)
+    w = rng.integers(0, 1000, size=1000).astype(np.uint64)
+    prefix = np.zeros(1001, dtype=np.uint64)
+    prefix[1:] = np.cumsum(w)
+    for parts in (1, 2, 3, 8, 64):
+        s = partition(prefix, parts)
+        assert s[0] == 0 and s[-1] == 1000 and np.all(np.diff(s.astype(np.int64)) >= 0)
+        total = int(prefix[-1])
+        for r in range(1, parts):
+            # split r starts at the first word whose start offset reaches r/parts of the total
+            assert int(prefix[s[r]]) >= total * r // parts
+            assert s[r] == 0 or int(prefix[s[r] - 1]) < -(-total * r // parts)
