@@ -37,6 +37,20 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def build_diag(verbose: bool = False) -> str:
+    """Diagnostic variant with per-phase s_memtime stamps (-DA5X_STAMPS) in _build_diag/."""
+    out = os.path.join(PKG, "_build_diag")
+    os.makedirs(out, exist_ok=True)
+    lib = os.path.join(out, "liba5x.so")
+    srcs = [os.path.join(CSRC, s) for s in LIB_SRCS]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+           "-DA5X_STAMPS", "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", lib]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return lib
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OUT, exist_ok=True)
     hipcc = _hipcc()

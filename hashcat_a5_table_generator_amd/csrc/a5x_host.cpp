@@ -92,7 +92,7 @@ struct a5x_ctx {
   size_t h_out_cap = 0;
 
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint64_t chunk = 1024;      // candidates per expand wave
+  uint64_t chunk = 4096;      // candidates per expand wave
   uint32_t waves_per_block = 4;
 };
 
@@ -753,6 +753,12 @@ int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t 
   }
   if (stats) *stats = total;
   return A5X_OK;
+}
+
+// diagnostic builds only (-DA5X_STAMPS); A5X_E_UNSUPPORTED otherwise
+int a5x_debug_stamps(unsigned long long* out16, int reset) {
+  const int rc = a5x_read_stamps(out16, reset);
+  return rc == 0 ? A5X_OK : (rc == -9 ? A5X_E_UNSUPPORTED : A5X_E_HIP);
 }
 
 int a5x_partition(const uint64_t* prefix, uint64_t n, uint32_t parts, uint64_t* split) {

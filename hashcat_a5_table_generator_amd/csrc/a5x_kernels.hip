@@ -38,6 +38,19 @@ typedef int64_t i64;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
   } while (0)
 
+// Diagnostic build only (-DA5X_STAMPS): per-phase s_memtime cycle sums of the
+// fast kernel, read back with a5x_debug_stamps().  Never in the shipped build.
+#ifdef A5X_STAMPS
+__device__ unsigned long long g_a5x_stamps[16];
+#define STAMP_DECL unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_acc[10] = {0,0,0,0,0,0,0,0,0,0};
+#define STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_t; st_t = t_; } while (0)
+#define STAMP_FLUSH() do { if (lane_id() == 0) for (int i_ = 0; i_ < 10; i_++) atomicAdd(&g_a5x_stamps[i_], st_acc[i_]); } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH() do {} while (0)
+#endif
+
 enum : u32 {
   A5X_DERR_TABLE = 1u << 0,   // table blob does not fit LDS / bad magic
   A5X_DERR_OVF = 1u << 1,     // u64 overflow in a keyspace
@@ -64,14 +77,20 @@ __device__ __forceinline__ u64 shfl_xor_u64(u64 v, int m) {
   u32 lo = __shfl_xor((int)(u32)v, m), hi = __shfl_xor((int)(u32)(v >> 32), m);
   return ((u64)hi << 32) | lo;
 }
+// Wave64 inclusive prefix sum on DPP (VALU only, no LDS): row_shr 1/2/4/8 inside
+// each 16-lane row, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3).
+// The sequence LLVM's AMDGPU atomic optimizer uses on gfx9.
 __device__ __forceinline__ u32 wave_incl_scan_u32(u32 x) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    u32 y = __shfl_up((int)x, d);
-    if ((int)lane_id() >= d) x += y;
-  }
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
   return x;
 }
+__device__ __forceinline__ u32 lane63(u32 x) { return (u32)__builtin_amdgcn_readlane((int)x, 63); }
+__device__ __forceinline__ u32 readlane_u32(u32 x, u32 l) { return (u32)__builtin_amdgcn_readlane((int)x, (int)l); }
 __device__ __forceinline__ u64 wave_sum_u64(u64 x) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) x += shfl_xor_u64(x, m);
@@ -914,7 +933,7 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
         len = (u32)l;
       }
       const u32 incl = wave_incl_scan_u32(len);
-      const u32 tot = __shfl((int)incl, 63);
+      const u32 tot = lane63(incl);
       const u64 off = R.pos + incl - len - R.base;
       if (act) {
         e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
@@ -936,7 +955,7 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
     } else {
       if (act) len = dp_walk<false, RING>(S, T, I, rk, e, ring);
       const u32 incl = wave_incl_scan_u32(len);
-      const u32 tot = __shfl((int)incl, 63);
+      const u32 tot = lane63(incl);
       const u64 off = R.pos + incl - len - R.base;
       if (act) {
         e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
@@ -1022,64 +1041,99 @@ __device__ __forceinline__ u32 add_lit_pieces(FWin& F, const uint8_t* wbytes, u3
   return pi;
 }
 
+// Offsets of word wl (lane-parallel window metadata, one round trip).
+struct WMeta {
+  u64 c0, c1, ws, we, bo;
+  u32 fl;
+};
+__device__ __forceinline__ WMeta load_meta(const ExpArgs& a, u64 wl, bool inb) {
+  WMeta m;
+  m.c0 = inb ? a.cand_off[wl] : ~0ull;
+  m.c1 = inb ? a.cand_off[wl + 1] : ~0ull;
+  m.ws = inb ? a.woff[wl] : 0;
+  m.we = inb ? a.woff[wl + 1] : 0;
+  m.bo = inb ? a.byte_off[wl] : 0;
+  m.fl = inb ? a.flags[wl] : 0u;
+  return m;
+}
+
+#define FW_PF 3  // prefetched window-byte dwords per lane (>= (FW_WB + 8) / 4 / 64)
+
 __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
   const u64 g0 = max(a.cand_begin, chunk * a.CH);
   const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
   if (g0 >= g1) return;
   u64 w = a.chunk_w0[chunk];
+  const u64 wtotal = a.woff[a.nw];  // bytes of the word buffer (prefetch bound)
   if (w >= a.nw) { guard_trip(a, 2, chunk, w, g0, a.nw); return; }
   while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
   if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
   u64 g = g0;
   Run R;
   R.open = false;
+  u64 pend = 0;  // complete blocks [R.flushed, pend) awaiting the deferred flush
   const uint8_t* wbytes = (const uint8_t*)F.bytes32;
+  WMeta M = load_meta(a, w + lane, lane < FW_WW && w + lane < a.nw);
+  u64 pfbase = ~0ull;  // dword-aligned byte address of the prefetched window bytes
+  u32 pf[FW_PF];
+  STAMP_DECL
   while (g < g1) {
     if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
-    // ---- window metadata: lane j <-> word w + j ----
-    const u64 wl = w + lane;
-    const bool inb = lane < FW_WW && wl < a.nw;
-    const u64 c0 = inb ? a.cand_off[wl] : ~0ull;
-    const u64 c1 = inb ? a.cand_off[wl + 1] : ~0ull;
-    const u64 ws = inb ? a.woff[wl] : 0;
-    const u64 we = inb ? a.woff[wl + 1] : 0;
-    const u32 fl = inb ? a.flags[wl] : 0u;
-    const bool fast = inb && (fl & A5X_WF_FAST) && c0 < g1;
-    const u32 L = fast ? (u32)(we - ws) : 0u;
-    const u32 ns = fast ? (fl >> 16) & 255u : 0u;
-    const u32 np = fast ? (fl >> 24) & 63u : 0u;
+    // ---- window extent: lane j <-> word w + j ----
+    const bool inb = lane < FW_WW && w + lane < a.nw;
+    const bool fast = inb && (M.fl & A5X_WF_FAST) && M.c0 < g1;
+    const u32 L = fast ? (u32)(M.we - M.ws) : 0u;
+    const u32 ns = fast ? (M.fl >> 16) & 255u : 0u;
+    const u32 np = fast ? (M.fl >> 24) & 63u : 0u;
     const u32 incL = wave_incl_scan_u32(L);
     const u32 incS = wave_incl_scan_u32(ns);
     const u32 incP = wave_incl_scan_u32(np);
     const bool ok = fast && incL + 3 <= FW_WB && incS <= FW_WS && incP <= FW_WP;
     const u64 badm = __ballot(!ok);
     const u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
+    STAMP(0);
     if (k == 0) {
       // word w is a hole here (slow / BIG) or empty
-      const u64 w0c1 = uniform64(c1);
+      const u64 w0c1 = uniform64(M.c1);
       if (w0c1 > g) {
+        if (R.open && pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
         run_close<FW_RING>(R, ring, a);
         g = min(w0c1, g1);
       }
       w++;
+      M = load_meta(a, w + lane, lane < FW_WW && w + lane < a.nw);
       continue;
     }
-    // ---- window bytes -> LDS (aligned dwords) ----
-    const u64 A0 = uniform64(ws) & ~3ull;
-    const u64 Aend = uniform64(shfl_u64(we, (int)k - 1));
+    // ---- window bytes -> LDS (aligned dwords; prefetched when contiguous) ----
+    const u64 A0 = uniform64(M.ws) & ~3ull;
+    const u64 Aend = uniform64(shfl_u64(M.we, (int)k - 1));
     if (Aend < A0 || Aend - A0 > FW_WB || w + k > a.nw) {
       guard_trip(a, 5, chunk, w, k, Aend - A0);
       break;
     }
     const u32 ndw = (u32)((Aend - A0 + 3) / 4);
-    const u32* src = (const u32*)(a.words + A0);
-    for (u32 i = lane; i < ndw + 2; i += 64) F.bytes32[i] = i < ndw ? src[i] : 0u;
+    if (A0 == pfbase) {
+#pragma unroll
+      for (u32 t = 0; t < FW_PF; t++) F.bytes32[lane + 64 * t] = (lane + 64 * t < ndw) ? pf[t] : 0u;
+    } else {
+      const u32* src = (const u32*)(a.words + A0);
+      for (u32 i = lane; i < ndw + 2; i += 64) F.bytes32[i] = i < ndw ? src[i] : 0u;
+    }
     WAVE_SYNC();
+    // ---- prefetch the next window (metadata + bytes from this window's end) ----
+    const WMeta Mn = load_meta(a, w + k + lane, lane < FW_WW && w + k + lane < a.nw);
+    pfbase = Aend & ~3ull;
+#pragma unroll
+    for (u32 t = 0; t < FW_PF; t++) {
+      const u64 addr = pfbase + 4ull * (lane + 64 * t);
+      pf[t] = addr + 4 <= wtotal + 16 ? *(const u32*)(a.words + addr) : 0u;
+    }
+    STAMP(1);
     // ---- slots + pieces, lane per word (words without candidates have none) ----
     u32 maxl = 0;
     if (lane < k && ns) {
-      const u32 off = (u32)(ws - A0);
+      const u32 off = (u32)(M.ws - A0);
       const u32 pbase = incP - np;
       u32 si = incS - ns, pi = pbase, prev = 0, mlen = 0, lconst = 0;
       for (u32 p = 0; p < L; p++) {
@@ -1101,10 +1155,8 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
             lit = run;
             lit4 = run ? keep_bytes(lds_ld4(wbytes, off + prev), run) : 0u;
           } else {
-            const u32 pi0 = pi;
             pi = add_lit_pieces(F, wbytes, pi, off + prev, run, 0);
             lconst += run;
-            (void)pi0;
           }
           u32 plen4 = 0, pm = 0;
           for (u32 d = 0; d <= key.nvals; d++) {
@@ -1136,16 +1188,17 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
       fw.sbase = (uint16_t)(incS - ns); fw.ns = (uint16_t)ns;
       fw.pbase = (uint16_t)pbase; fw.np = (uint16_t)np;
       fw.lconst = lconst; fw.pad = 0; fw.pad2 = 0;
-      fw.c0 = c0;
+      fw.c0 = M.c0;
       F.words[lane] = fw;
       if (si != incS || pi != incP) atomicOr(a.err, A5X_DERR_STATE);
       maxl = mlen + lconst;
     }
     const u32 winmax = wave_max_u32(maxl);
     WAVE_SYNC();
+    STAMP(2);
     // ---- run position of g ----
-    const u64 r0 = g - uniform64(c0);
-    u64 pos = uniform64(a.byte_off[w]) - a.out_base;
+    const u64 r0 = g - uniform64(M.c0);
+    u64 pos = uniform64(M.bo) - a.out_base;
     if (r0) {
       // closed-form prefix bytes of candidates [0, r0) of word w (lanes over its slots)
       const FWord f0 = F.words[0];
@@ -1175,23 +1228,27 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
       pos += (u64)((i64)r0 * lbase + wave_sum_i64(part));
     }
     if (!R.open || R.pos != pos) {
+      if (R.open && pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
       run_close<FW_RING>(R, ring, a);
       run_open<FW_RING>(R, pos);
+      pend = R.flushed;
     }
-    // ---- rounds ----
-    const u64 gend = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
-    const u32 nl = uniform(min(64u, (FW_RING - 16) / max(winmax, 1u)));
-    const u32 c1rel = (lane < k) ? (u32)(c1 - g) : 0xffffffffu;  // chunk-relative ends
+    STAMP(3);
+    // ---- rounds: two rounds of bytes live in the ring (deferred flush) ----
+    const u64 gend = min(g1, uniform64(shfl_u64(M.c1, (int)k - 1)));
+    const u32 nl = uniform(min(64u, (FW_RING / 2 - 16) / max(winmax, 1u)));
+    const u32 c0rel = (lane < k) ? (u32)(M.c0 > g ? M.c0 - g : 0) : 0xffffffffu;
+    u32 jcur = 0;  // word holding the round's first candidate (uniform)
     for (u64 rr = g; rr < gend; rr += nl) {
-      const u32 grel = (u32)(rr - g) + lane;
+      const u32 rrel = (u32)(rr - g);
       const bool act = lane < nl && rr + lane < gend;
-      // word of the candidate: first j < k with c1rel_j > grel
-      u32 lo = 0, hi = k - 1;
-#pragma unroll
-      for (int it = 0; it < 5; it++) {
-        const u32 mid = (lo + hi) >> 1;
-        const u32 v = (u32)__shfl((int)c1rel, (int)mid);
-        if (lo < hi) { if (v <= grel) lo = mid + 1; else hi = mid; }
+      // word of each lane's candidate: walk the (uniform) words starting in this round
+      u32 lo = jcur;
+      for (u32 j = jcur + 1; j < k; j++) {
+        const u32 sj = readlane_u32(c0rel, j);
+        if (sj >= rrel + nl) break;
+        if (rrel + lane >= sj) lo = j;
+        jcur = j;
       }
       const FWord fw = F.words[lo];
       u32 len = 0;
@@ -1199,39 +1256,62 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
       if (act) {
         u32 n = (u32)(rr + lane - fw.c0 + 1);
         len = fw.lconst;
-        for (u32 i = 0; i < fw.ns; i++) {
-          const FSlot sl = F.slots[fw.sbase + i];
-          const u32 q = fastdiv(n, sl.magic, sl.shift);
-          const u32 d = n - q * sl.R;
-          n = q;
-          dig |= (u64)d << (2 * sl.ps);
-          len += (sl.plen4 >> (8 * d)) & 255u;
+        const FSlot* sp = F.slots + fw.sbase;
+        for (u32 i = 0; i < fw.ns; i += 2) {
+          const FSlot s0 = sp[i];
+          const FSlot s1 = sp[i + 1];  // may read past the word: unused then
+          {
+            const u32 q = fastdiv(n, s0.magic, s0.shift);
+            const u32 d = n - q * s0.R;
+            n = q;
+            dig |= (u64)d << (2 * s0.ps);
+            len += (s0.plen4 >> (8 * d)) & 255u;
+          }
+          if (i + 1 < fw.ns) {
+            const u32 q = fastdiv(n, s1.magic, s1.shift);
+            const u32 d = n - q * s1.R;
+            n = q;
+            dig |= (u64)d << (2 * s1.ps);
+            len += (s1.plen4 >> (8 * d)) & 255u;
+          }
         }
       }
+      STAMP(4);
       const u32 incl = wave_incl_scan_u32(len);
-      const u32 tot = uniform((u32)__shfl((int)incl, 63));
+      const u32 tot = lane63(incl);
+      STAMP(5);
+      // deferred flush of the previous round's complete blocks (their ORs are long done)
+      if (pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
+      STAMP(7);
       if (act) {
         const u64 off = R.pos + incl - len - R.base;
         Emit e;
         e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
         const FPiece* pp = F.pieces + fw.pbase * 4;
-        for (u32 i = 0; i < fw.np; i++) {
-          const u32 d = (u32)(dig >> (2 * i)) & 3u;
-          const FPiece P = pp[i * 4 + d];
-          put4(e, ring, P.b4, P.len);
+        for (u32 i = 0; i < fw.np; i += 4) {
+          // four piece loads in flight before their ORs
+          FPiece P[4];
+#pragma unroll
+          for (u32 t = 0; t < 4; t++) P[t] = pp[(i + t) * 4 + (i + t < 32 ? ((u32)(dig >> (2 * (i + t))) & 3u) : 0u)];
+#pragma unroll
+          for (u32 t = 0; t < 4; t++) put4(e, ring, P[t].b4, i + t < fw.np ? P[t].len : 0u);
         }
         if (e.n) atomicOr(&ring[e.dw & (FW_RING / 4 - 1)], (u32)e.acc);
       }
       R.pos += tot;
+      pend = R.pos & ~15ull;
       WAVE_SYNC();
-      const u64 full = R.pos & ~15ull;
-      if (full > R.flushed) run_flush<FW_RING>(R, ring, a, full, R.pos);
+      STAMP(6);
     }
     g = gend;
     w += k;
+    M = Mn;
     WAVE_SYNC();
   }
+  if (R.open && pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
   run_close<FW_RING>(R, ring, a);
+  STAMP(8);
+  STAMP_FLUSH();
 }
 
 __device__ __forceinline__ u32 lds_per_wave_fast() { return (FW_RING + (u32)sizeof(FWin) + 15u) & ~15u; }
@@ -1485,6 +1565,20 @@ hipError_t a5x_launch_digest(const uint8_t* out, const u64* byte_off, u64 out_ba
                              hipStream_t st) {
   hipLaunchKernelGGL(k_digest, dim3(blocks_for(nw, 256, 65536)), dim3(256), 0, st, out, byte_off, out_base, nw, dig);
   return hipGetLastError();
+}
+
+int a5x_read_stamps(unsigned long long* out16, int reset) {
+#ifdef A5X_STAMPS
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_a5x_stamps), 16 * 8) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_a5x_stamps), z, sizeof z) != hipSuccess) return -2;
+  }
+  return 0;
+#else
+  (void)out16; (void)reset;
+  return -9;
+#endif
 }
 
 hipError_t a5x_set_kernel_attrs() {

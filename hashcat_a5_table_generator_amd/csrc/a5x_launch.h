@@ -45,6 +45,7 @@ struct A5xExpLaunch {
 };
 
 hipError_t a5x_set_kernel_attrs();
+int a5x_read_stamps(unsigned long long* out16, int reset);
 hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st);
 size_t a5x_keyspace_wave_lds(uint32_t table_bytes);
 uint64_t a5x_scan_tmp_elems(uint64_t n);

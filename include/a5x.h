@@ -148,6 +148,10 @@ A5X_API int a5x_digest_device(a5x_ctx* ctx, const uint8_t* d_out, const uint64_t
  * rank r, split[parts] = n.  Pure host function. */
 A5X_API int a5x_partition(const uint64_t* prefix, uint64_t n, uint32_t parts, uint64_t* split);
 
+/* Diagnostic builds only (compiled with -DA5X_STAMPS): per-phase cycle sums of
+ * the fast expansion kernel.  A5X_E_UNSUPPORTED in shipped builds. */
+A5X_API int a5x_debug_stamps(unsigned long long* out16, int reset);
+
 /* ---- device memory helpers (so hosts without torch can drive the API) ---------- */
 A5X_API int a5x_dev_alloc(a5x_ctx* ctx, void** p, size_t bytes);
 A5X_API int a5x_dev_free(a5x_ctx* ctx, void* p);
