@@ -5,7 +5,7 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 One "step" = one full pass of the hot path over one batch already resident in HBM:
-keyspace (k_keyspace_*) -> prefix scans -> chunk plan -> expansion (k_expand_a[/b])
+keyspace (k_keyspace_*) -> prefix scans -> chunk plan -> expansion (k_expand_fast [+ k_expand_slow, k_expand_b])
 into an HBM output buffer, i.e. a5x_expand_device() of include/a5x.h.  The default
 workload is BASELINE.json configs[2]: czech.table + german.table over a synthetic
 10M-word [a-z] list (len U[6,12]) per GPU.  Multi-GPU = weak scaling: every rank
@@ -209,7 +209,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_expand_a" + ("+k_expand_b" if launches > 1 else ""),
+                "kernel": "k_expand_fast+k_expand_slow+k_expand_b (launched when present)",
                 "ms_per_launch": ms_exp,
                 "ms_per_launch_max_rank": ms_exp_max,
                 "ms_keyspace_scan_plan": ms_ks,

@@ -1294,7 +1294,10 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
 #pragma unroll
           for (u32 t = 0; t < 4; t++) P[t] = pp[(i + t) * 4 + (i + t < 32 ? ((u32)(dig >> (2 * (i + t))) & 3u) : 0u)];
 #pragma unroll
-          for (u32 t = 0; t < 4; t++) put4(e, ring, P[t].b4, i + t < fw.np ? P[t].len : 0u);
+          for (u32 t = 0; t < 4; t++) {
+            const bool live = i + t < fw.np;  // pieces past np belong to the next word
+            put4(e, ring, live ? P[t].b4 : 0u, live ? P[t].len : 0u);
+          }
         }
         if (e.n) atomicOr(&ring[e.dw & (FW_RING / 4 - 1)], (u32)e.acc);
       }
