@@ -27,7 +27,7 @@ EXPORTS = (
     "a5x_load_table_file", "a5x_parse_table", "a5x_set_table", "a5x_clear_table", "a5x_table_export",
     "a5x_split_words", "a5x_keyspace", "a5x_expand", "a5x_expand_device", "a5x_keyspace_device",
     "a5x_digest_device", "a5x_partition", "a5x_dev_alloc", "a5x_dev_free", "a5x_memcpy_h2d",
-    "a5x_memcpy_d2h", "a5x_synchronize", "a5x_debug_stamps",
+    "a5x_memcpy_d2h", "a5x_synchronize", "a5x_debug_stamps", "a5x_debug_plan_word",
 )
 
 
@@ -95,6 +95,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     L.a5x_memcpy_d2h.argtypes = [vp, vp, vp, sz]
     L.a5x_synchronize.argtypes = [vp]
     L.a5x_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i]
+    L.a5x_debug_plan_word.argtypes = [vp, vp, sz, i, i, vp, sz, vp]
     _lib = L
     return L
 

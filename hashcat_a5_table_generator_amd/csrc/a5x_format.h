@@ -64,13 +64,13 @@ enum : uint32_t {
   A5X_WF_GENERAL = 1u << 2, // overlapping / multi matches or capped: DP walk
   A5X_WF_BIG = 1u << 3,     // does not fit the pass-A wave budget: pass B
   A5X_WF_DEFER = 1u << 4,   // keyspace needs the wave-level DP kernel
-  A5X_WF_FAST = 1u << 5,    // radix, <= 64 B, fanout <= 3, choices <= 4 B, <= 32 pieces: k_expand_fast
+  A5X_WF_FAST = 1u << 5,    // radix, <= 64 B, piece plan fits (plan_word): k_expand_fast
   A5X_WF_ERR_OVF = 1u << 8, // count/bytes overflow u64
   A5X_WF_ERR_BIG = 1u << 9, // exceeds pass-B limits
 };
 
-// bits 16..23 of a RADIX word's flags: its slot count (<= 64); bits 24..29 of a
-// FAST word: its piece count (<= 32), see fast_piece_count() in a5x_kernels.hip
+// FAST words: bits 10..14 = group pieces, 16..23 = piece entries, 24..28 = pieces
+// (plan_word in a5x_kernels.hip).
 
 // Limits of the expansion passes (documented in DESIGN.md).
 #define A5X_WAVE 64

@@ -19,10 +19,12 @@
 #include <algorithm>
 #include <string>
 #include <unordered_map>
+#include <memory>
 #include <vector>
 
 #include "a5x.h"
 #include "a5x_format.h"
+#include "a5x_plan.h"
 #include "a5x_gosem.h"
 #include "a5x_launch.h"
 
@@ -759,6 +761,56 @@ int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t 
 int a5x_debug_stamps(unsigned long long* out16, int reset) {
   const int rc = a5x_read_stamps(out16, reset);
   return rc == 0 ? A5X_OK : (rc == -9 ? A5X_E_UNSUPPORTED : A5X_E_HIP);
+}
+
+int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int mx, uint8_t* out, size_t cap,
+                        uint64_t* info) {
+  if (!c || !info || (!word && len) || (!out && cap)) return A5X_E_ARG;
+  if (c->table.keys.empty()) return fail(c, A5X_E_NOTABLE, "no substitution table loaded");
+  if (c->table_dirty || c->blob.empty()) {
+    int rc = compile_table(c);
+    if (rc) return rc;
+  }
+  info[0] = info[1] = info[2] = info[3] = 0;
+  if (len > A5X_LMAX_A && mx >= 1) {
+    info[2] = A5X_WF_DEFER;
+    return A5X_OK;
+  }
+  std::vector<uint8_t> wb(word, word + len);
+  wb.resize(len + 16, 0);
+  GWord gw;
+  gw.p = wb.data();
+  const Tab T = tab_view(c->blob.data());
+  const WordClass C = classify_word(gw, (u32)len, T, mn, mx, A5X_RING_A - 16);
+  info[0] = C.count; info[1] = C.bytes; info[2] = C.flags;
+  if (!(C.flags & A5X_WF_FAST) || C.count == 0) return A5X_OK;
+  std::unique_ptr<FWin> F(new FWin());
+  memset(F.get(), 0, sizeof(FWin));
+  const Plan P = plan_word<true>(gw, (u32)len, T, F.get(), 0, 0);
+  if (!P.ok || P.ng != ff_ng(C.flags) || P.ne != ff_ne(C.flags) || P.np != ff_np(C.flags))
+    return fail(c, A5X_E_BOUNDS, "piece plan disagrees with the keyspace fields");
+  // replay k_expand_fast passes 1-2 for candidates 0..count-1 (index n = r + 1)
+  uint64_t w = 0;
+  for (uint64_t r = 0; r < C.count; r++) {
+    u64 dlo, dhi;
+    const u32 clen = fw_pass1(F->groups, P.ng, P.lconst, (u32)(r + 1), dlo, dhi);
+    if (w + clen > cap) return fail(c, A5X_E_CAPACITY, "output buffer too small");
+    u32 row = 0, got = 0;
+    u64 cur = dlo;
+    for (u32 i = 0; i < P.np; i++) {
+      const u64 e = F->ent[row + ((u32)cur & 7u)];
+      row += (((u32)cur >> 3) & 7u) + 1u;
+      cur = (i == 9) ? dhi : (cur >> 6);
+      const u32 pl = fw_len(e);
+      for (u32 b = 0; b < pl; b++) out[w + got + b] = (uint8_t)(e >> (8 * b));
+      got += pl;
+    }
+    if (got != clen) return fail(c, A5X_E_BOUNDS, "candidate %llu: pass-1 length %u != pieces %u",
+                                 (unsigned long long)r, clen, got);
+    w += got;
+  }
+  info[3] = w;
+  return A5X_OK;
 }
 
 int a5x_partition(const uint64_t* prefix, uint64_t n, uint32_t parts, uint64_t* split) {

@@ -26,10 +26,7 @@
 #include <stdint.h>
 
 #include "a5x_format.h"
-
-typedef uint64_t u64;
-typedef uint32_t u32;
-typedef int64_t i64;
+#include "a5x_plan.h"
 
 #define WAVE_SYNC()                                          \
   do {                                                       \
@@ -113,18 +110,6 @@ __device__ __forceinline__ u64 uniform64(u64 x) {
   return ((u64)uniform((u32)(x >> 32)) << 32) | (u64)uniform((u32)x);
 }
 
-// a*b with overflow flag
-__device__ __forceinline__ u64 mul_ovf(u64 a, u64 b, bool& ovf) {
-  u64 r;
-  ovf |= __builtin_mul_overflow(a, b, &r);
-  return r;
-}
-__device__ __forceinline__ u64 add_ovf(u64 a, u64 b, bool& ovf) {
-  u64 r = a + b;
-  ovf |= r < a;
-  return r;
-}
-
 __device__ __forceinline__ u32 keep_bytes(u32 v, u32 n) { return n >= 4 ? v : (v & ((1u << (8 * n)) - 1u)); }
 
 // unaligned 4-byte read from LDS (base must have 8 readable bytes past off)
@@ -132,27 +117,6 @@ __device__ __forceinline__ u32 lds_ld4(const uint8_t* base, u32 off) {
   const u32* p = (const u32*)(base + (off & ~3u));
   u32 lo = p[0], hi = p[1];
   return __builtin_amdgcn_alignbyte(hi, lo, off & 3u);
-}
-
-// ---------------------------------------------------------------------------
-// the device table (see a5x_format.h), viewed in LDS
-// ---------------------------------------------------------------------------
-struct Tab {
-  const A5xTableHdr* hdr;
-  const uint16_t* bucket;
-  const A5xKey* keys;
-  const A5xChoice* ch;
-  const uint8_t* blob;
-};
-
-__device__ __forceinline__ Tab tab_view(const uint8_t* base) {
-  Tab t;
-  t.hdr = (const A5xTableHdr*)base;
-  t.bucket = (const uint16_t*)(base + t.hdr->off_bucket);
-  t.keys = (const A5xKey*)(base + t.hdr->off_keys);
-  t.ch = (const A5xChoice*)(base + t.hdr->off_choices);
-  t.blob = base + t.hdr->off_blob;
-  return t;
 }
 
 // whole workgroup copies the table blob (multiple of 16 B) into LDS
@@ -173,12 +137,17 @@ __device__ __forceinline__ bool key_match_global(const uint8_t* wp, u32 p, const
   return true;
 }
 
-// Pieces of a FAST word (k_expand_fast emits one <= 4-byte piece per step): the
-// literal run before a slot merges with the slot's choice when run + longest
-// choice <= 4, else it is cut into 4-byte literal pieces; the tail + '\n' is cut
-// the same way.  Both the keyspace pass and the window setup use this rule.
-__device__ __forceinline__ u32 lit_pieces(u32 m) { return (m + 3) / 4; }
-__device__ __forceinline__ u32 slot_pieces(u32 run, u32 maxclen) { return run + maxclen <= 4 ? 1u : lit_pieces(run) + 1u; }
+
+// The window bytes of a word in LDS, for plan_word (a5x_plan.h).
+struct LWord {
+  const uint8_t* base;  // window bytes (>= 8 readable bytes past any word)
+  u32 off;
+  __device__ __forceinline__ u32 at(u32 i) const { return base[off + i]; }
+  __device__ __forceinline__ u64 ld(u32 i, u32 n) const {
+    const u64 v = (u64)lds_ld4(base, off + i) | ((u64)lds_ld4(base, off + i + 4) << 32);
+    return keep_bytes64(v, n);
+  }
+};
 
 // ---------------------------------------------------------------------------
 // Keyspace, one lane per word (radix fast path; SURVEY 8(a) closed form)
@@ -209,67 +178,24 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < a.nw; w += stride) {
     const u64 s = a.woff[w], e = a.woff[w + 1];
     const u64 L64 = e - s;
-    if (a.mx < 1 || L64 == 0) {  // processWord emits nothing
-      a.count[w] = 0; a.bytes[w] = 0; a.flags[w] = A5X_WF_RADIX | A5X_WF_FAST;
-      continue;
-    }
-    if (L64 > A5X_LMAX_A) {  // long words: the wave kernel (loops over positions)
+    if (L64 > A5X_LMAX_A && a.mx >= 1) {  // long words: the wave kernel (loops over positions)
       a.flags[w] = A5X_WF_DEFER;
       a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
       continue;
     }
-    const u32 L = (u32)L64;
-    const uint8_t* wp = a.words + s;
-    u32 nmatch = 0, last_end = 0, maxl = L + 1, maxnv = 0, maxcl = 0, npiece = 0, pend = 0;
-    bool conflict = false, bin = true, ovf = false;
-    u64 P = 1, Dp = 0, Dn = 0;
-    for (u32 p = 0; p < L; p++) {
-      const u32 b = wp[p];
-      const u32 ks = T.bucket[b], ke = T.bucket[b + 1];
-      for (u32 k = ks; k < ke; k++) {
-        const A5xKey key = T.keys[k];
-        if (p + key.klen > L || !key_match_global(wp, p, key, T)) continue;
-        nmatch++;
-        if (p < last_end) conflict = true;  // overlaps a previous match or 2nd match at p
-        last_end = max(last_end, p + (u32)key.klen);
-        const u64 R = (u64)key.nvals + 1;
-        // sum over this slot's values of (|v| - klen), split by sign
-        const u64 spos = key.sum_dpos, sneg = key.sum_dneg;
-        Dp = add_ovf(mul_ovf(Dp, R, ovf), mul_ovf(P, spos, ovf), ovf);
-        Dn = add_ovf(mul_ovf(Dn, R, ovf), mul_ovf(P, sneg, ovf), ovf);
-        P = mul_ovf(P, R, ovf);
-        if (key.nvals != 1) bin = false;
-        if (key.maxdelta > 0) maxl += (u32)key.maxdelta;
-        maxnv = max(maxnv, (u32)key.nvals);
-        maxcl = max(maxcl, (u32)key.maxclen);
-        npiece += slot_pieces(p - pend, key.maxclen);  // meaningful only without conflicts
-        pend = p + key.klen;
-      }
-    }
-    const bool freew = (a.mn <= 1) && ((i64)nmatch <= (i64)a.mx);
-    if (nmatch == 0) {
-      a.count[w] = 0; a.bytes[w] = 0; a.flags[w] = A5X_WF_RADIX | A5X_WF_FAST;
-    } else if (!conflict && freew && !ovf && P <= (1ull << 32) && maxl <= A5X_RING_A - 16) {
-      bool o2 = false;
-      const u64 cnt = P - 1;
-      u64 byt = add_ovf(mul_ovf(cnt, (u64)L + 1, o2), Dp, o2);
-      if (byt < Dn) o2 = true;
-      byt -= Dn;
-      if (o2) {
-        a.flags[w] = A5X_WF_ERR_OVF; a.count[w] = 0; a.bytes[w] = 0;
-        atomicOr(a.err, A5X_DERR_OVF);
-      } else {
-        a.count[w] = cnt; a.bytes[w] = byt;
-        npiece += lit_pieces(L - pend + 1);  // tail + '\n'
-        const bool fast = maxnv <= 3 && maxcl <= 4 && npiece <= 32;
-        if (!fast) atomicAdd(a.nslow, 1u);
-        a.flags[w] = A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u) | (fast ? A5X_WF_FAST : 0u) | (nmatch << 16) |
-                     (fast ? npiece << 24 : 0u);
-      }
-    } else {
-      a.flags[w] = A5X_WF_DEFER;
+    GWord gw;
+    gw.p = a.words + s;
+    const WordClass C = classify_word(gw, (u32)L64, T, a.mn, a.mx, A5X_RING_A - 16);
+    u32 f = C.flags;
+    if (C.ovf) atomicOr(a.err, A5X_DERR_OVF);
+    if ((f & A5X_WF_DEFER) || (!(f & (A5X_WF_FAST | A5X_WF_RADIX | A5X_WF_ERR_OVF)))) {
+      // capped windows, unit limits, or a cluster word that is not FAST: the DP kernel
+      f = A5X_WF_DEFER;
       a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
+    } else if (!(f & (A5X_WF_FAST | A5X_WF_ERR_OVF))) {
+      atomicAdd(a.nslow, 1u);
     }
+    a.count[w] = C.count; a.bytes[w] = C.bytes; a.flags[w] = f;
   }
 }
 
@@ -316,13 +242,6 @@ struct WordInfo {
   u32 why;         // diagnostics when !fits: 1 long, 2 matches, 3 columns, 4 DP size
 };
 
-__device__ __forceinline__ void divmagic(u32 d, u32& magic, u32& shift) {
-  // libdivide u32 branchfree: l = ceil(log2 d), M = floor(2^32 (2^l - d) / d) + 1
-  u32 l = 32 - __clz(d - 1);
-  u64 m = (((u64)1 << 32) * (((u64)1 << l) - d)) / d + 1;
-  magic = (u32)m;
-  shift = l - 1;
-}
 __device__ __forceinline__ u32 fastdiv(u32 n, u32 magic, u32 shift) {
   u32 q = __umulhi(n, magic);
   return (q + ((n - q) >> 1)) >> shift;
@@ -517,6 +436,7 @@ __device__ WordInfo wave_setup(WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, con
 // Keyspace for deferred words: one wave per word (pass-B budget)
 // ---------------------------------------------------------------------------
 typedef WaveLds<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B> LdsB;
+static_assert(sizeof(FWin) <= sizeof(WaveLds<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>), "k_locate aliases an FWin onto LdsB");
 typedef WaveLds<A5X_LMAX_A, A5X_MLMAX_A, A5X_DPENT_A> LdsA;
 
 __global__ void __launch_bounds__(64) k_keyspace_wave(KsArgs a) {
@@ -973,74 +893,30 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 }
 
 // ---------------------------------------------------------------------------
-// k_expand_fast: windows of consecutive FAST words (radix, <= 64 B, fanout <= 3).
-// Lane j holds word (w+j)'s offsets; the window's bytes are staged in LDS with
-// dword loads; lanes (one per word) cut each word into slots and precombine, per
-// (slot, digit), the literal run before the slot with the chosen value into one
-// <= 4-byte piece.  Rounds of 64 consecutive candidates then span word
-// boundaries: pass 1 = one division + one LDS read per slot (2-bit digits kept
-// packed), wave scan of lengths, pass 2 = one piece read + one emit per slot.
+// k_expand_fast: windows of consecutive FAST words (radix, <= 64 B; every
+// substitution unit has <= 8 choices of <= 7 bytes).
+//
+// Piece plan (plan_word, shared by k_keyspace_thread and the window setup):
+// a word is cut left to right into pieces of <= 7 bytes.  A *group* piece holds
+// one or more consecutive substitution units (a key match with its R = 1 + nvals
+// choices) together with the literal bytes between/before/after them, with all
+// R_1 x R_2 x ... <= 8 combinations precombined; a *literal* piece holds <= 7
+// plain bytes.  Combination index a_1 + R_1 (a_2 + R_2 (...)) of a group is
+// exactly the mixed-radix digit order of the units (left unit least significant),
+// so candidate numbering is the same as the per-unit radix order used by
+// k_locate and the other expansion kernels.
+//
+// Device format per window (LDS): entries u64 = 7 content bytes + meta byte
+// (len | (R-1) << 3), the R entries of a piece consecutive; FGroup per group
+// piece (libdivide magic for R, digit shift 3 * piece index, 4-bit lengths of
+// its R entries).  Rounds of <= 64 consecutive candidates span word boundaries:
+// pass 1 = one division + one LDS read per group (3-bit digits packed per piece),
+// wave scan of lengths; pass 2 = one entry read + one or two ds_or_b64 per piece
+// at the candidate's byte offset in a zeroed per-wave ring (OR is exact: every
+// output byte is written by exactly one piece; zeros elsewhere).  Complete 16-B
+// ring blocks are streamed out with 16-B stores one round later.
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
-#define FW_WB 512   // window word-byte budget
-#define FW_WS 64    // window radix-slot budget
-#define FW_WP 96    // window piece budget
-#define FW_WW 32    // window word budget
-#define FW_RING 4096
-
-struct FSlot {        // 16 B, one per radix slot
-  u32 magic;
-  uint8_t shift, R, ps, pad0;  // ps: piece index (within the word) the digit selects
-  u32 plen4;          // length of piece ps for digit d in byte d
-  u32 pad1;
-};
-struct FPiece {       // 8 B: <= 4 bytes of output for one digit value
-  u32 b4;
-  u32 len;
-};
-struct FWord {        // 32 B
-  uint16_t sbase, ns, pbase, np;
-  u32 lconst;         // bytes of the digit-independent pieces (literals, tail, '\n')
-  u32 pad;
-  u64 c0;             // first global candidate index of the word
-  u64 pad2;
-};
-struct FWin {
-  u32 bytes32[(FW_WB + 32) / 4];
-  FSlot slots[FW_WS];
-  FPiece pieces[FW_WP * 4];
-  FWord words[FW_WW];
-};
-
-// Branch-free emit of a <= 4-byte piece: OR the (growing) low dword every time --
-// OR is idempotent -- and advance when it is complete.
-__device__ __forceinline__ void put4(Emit& e, u32* ring, u32 b4, u32 len) {
-  e.acc |= (u64)b4 << (8u * e.n);
-  e.n += len;
-  atomicOr(&ring[e.dw & (FW_RING / 4 - 1)], (u32)e.acc);
-  const bool adv = e.n >= 4;
-  e.dw += adv ? 1u : 0u;
-  e.acc = adv ? (e.acc >> 32) : e.acc;
-  e.n -= adv ? 4u : 0u;
-}
-
-// window setup helper: write literal bytes [off, off+m) as 4-byte literal pieces
-__device__ __forceinline__ u32 add_lit_pieces(FWin& F, const uint8_t* wbytes, u32 pi, u32 off, u32 m, u32 tailnl) {
-  // tailnl: append '\n' after the run (word tail)
-  const u32 total = m + tailnl;
-  for (u32 k = 0; k < total; k += 4) {
-    const u32 n = min(4u, total - k);
-    u32 v = 0;
-    if (k < m) v = keep_bytes(lds_ld4(wbytes, off + k), min(n, m - k));
-    if (tailnl && k + n == total) v |= 10u << (8 * (n - 1));
-    FPiece P;
-    P.b4 = v; P.len = n;
-    if (pi < FW_WP) F.pieces[pi * 4] = P;
-    pi++;
-  }
-  return pi;
-}
-
 // Offsets of word wl (lane-parallel window metadata, one round trip).
 struct WMeta {
   u64 c0, c1, ws, we, bo;
@@ -1057,10 +933,43 @@ __device__ __forceinline__ WMeta load_meta(const ExpArgs& a, u64 wl, bool inb) {
   return m;
 }
 
+
 #define FW_PF 3  // prefetched window-byte dwords per lane (>= (FW_WB + 8) / 4 / 64)
+
+// Closed-form bytes of candidates [0, r) of a FAST word (candidate r <-> index r + 1
+// in the group mixed radix, group 0 least significant).  Wave-collective: lanes over
+// the word's groups (ng <= 64).
+__device__ u64 fast_prefix_bytes(const FGroup* gp, u32 ng, u32 lconst, u64 r) {
+  const u32 lane = lane_id();
+  const u64 Y = r + 1;
+  u64 Rl = 1;
+  FGroup G;
+  if (lane < ng) { G = gp[lane]; Rl = G.R; }
+  u64 inc = Rl;  // inclusive prefix product of R over groups
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u64 y = shfl_up_u64(inc, d);
+    if ((int)lane >= d) inc *= y;
+  }
+  i64 part = 0, base0 = 0;
+  if (lane < ng) {
+    const u64 Q = inc / Rl, full = Y / inc, rem = Y % inc;
+    const int l0 = (int)(G.plen & 15u);
+    base0 = l0;
+    for (u32 v = 1; v < G.R; v++) {
+      const u64 lo = (u64)v * Q;
+      const u64 cnt = full * Q + (rem > lo ? min(Q, rem - lo) : 0);
+      part += ((i64)((G.plen >> (4 * v)) & 15u) - l0) * (i64)cnt;
+    }
+  }
+  // every candidate = lconst + digit-0 group lengths + deltas
+  const i64 lbase = wave_sum_i64(base0) + lconst;
+  return (u64)((i64)r * lbase + wave_sum_i64(part));
+}
 
 __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
+  unsigned long long* ring64 = (unsigned long long*)ring;
   const u64 g0 = max(a.cand_begin, chunk * a.CH);
   const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
   if (g0 >= g1) return;
@@ -1084,12 +993,12 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
     const bool inb = lane < FW_WW && w + lane < a.nw;
     const bool fast = inb && (M.fl & A5X_WF_FAST) && M.c0 < g1;
     const u32 L = fast ? (u32)(M.we - M.ws) : 0u;
-    const u32 ns = fast ? (M.fl >> 16) & 255u : 0u;
-    const u32 np = fast ? (M.fl >> 24) & 63u : 0u;
+    const u32 ng = fast ? ff_ng(M.fl) : 0u;
+    const u32 ne = fast ? ff_ne(M.fl) : 0u;
     const u32 incL = wave_incl_scan_u32(L);
-    const u32 incS = wave_incl_scan_u32(ns);
-    const u32 incP = wave_incl_scan_u32(np);
-    const bool ok = fast && incL + 3 <= FW_WB && incS <= FW_WS && incP <= FW_WP;
+    const u32 incG = wave_incl_scan_u32(ng);
+    const u32 incE = wave_incl_scan_u32(ne);
+    const bool ok = fast && incL + 3 <= FW_WB && incG <= FW_WG && incE <= FW_WE;
     const u64 badm = __ballot(!ok);
     const u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
     STAMP(0);
@@ -1130,68 +1039,20 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
       pf[t] = addr + 4 <= wtotal + 16 ? *(const u32*)(a.words + addr) : 0u;
     }
     STAMP(1);
-    // ---- slots + pieces, lane per word (words without candidates have none) ----
+    // ---- piece plan, lane per word (words without candidates have none) ----
     u32 maxl = 0;
-    if (lane < k && ns) {
-      const u32 off = (u32)(M.ws - A0);
-      const u32 pbase = incP - np;
-      u32 si = incS - ns, pi = pbase, prev = 0, mlen = 0, lconst = 0;
-      for (u32 p = 0; p < L; p++) {
-        const u32 b = wbytes[off + p];
-        const u32 ks = T.bucket[b], ke = T.bucket[b + 1];
-        for (u32 kk = ks; kk < ke; kk++) {
-          const A5xKey key = T.keys[kk];
-          if (p + key.klen > L) continue;
-          bool m = true;
-          const A5xChoice ck = T.ch[key.choice_base];
-          for (u32 i = 1; i < key.klen && m; i++) {
-            const u32 kb = i < 4 ? ((ck.first4 >> (8 * i)) & 255u) : T.blob[ck.blob_off + i];
-            m = wbytes[off + p + i] == kb;
-          }
-          if (!m) continue;
-          const u32 run = p - prev;
-          u32 lit = 0, lit4 = 0;
-          if (run + key.maxclen <= 4) {
-            lit = run;
-            lit4 = run ? keep_bytes(lds_ld4(wbytes, off + prev), run) : 0u;
-          } else {
-            pi = add_lit_pieces(F, wbytes, pi, off + prev, run, 0);
-            lconst += run;
-          }
-          u32 plen4 = 0, pm = 0;
-          for (u32 d = 0; d <= key.nvals; d++) {
-            const A5xChoice c = T.ch[key.choice_base + d];
-            FPiece P;
-            P.len = lit + c.len;
-            P.b4 = lit4 | (lit < 4 ? (c.first4 << (8 * lit)) : 0u);
-            if (pi < FW_WP) F.pieces[pi * 4 + d] = P;
-            plen4 |= P.len << (8 * d);
-            pm = max(pm, P.len);
-          }
-          if (si < FW_WS) {
-            FSlot sl;
-            sl.magic = key.magic; sl.shift = (uint8_t)key.shift; sl.R = (uint8_t)(key.nvals + 1u);
-            sl.ps = (uint8_t)(pi - pbase); sl.pad0 = 0; sl.plen4 = plen4; sl.pad1 = 0;
-            F.slots[si] = sl;
-          }
-          si++;
-          pi++;
-          mlen += pm;
-          prev = p + key.klen;
-          p += key.klen - 1;
-          break;  // radix words: exactly one match here and none inside it
-        }
-      }
-      pi = add_lit_pieces(F, wbytes, pi, off + prev, L - prev, 1);
-      lconst += L - prev + 1;
+    if (lane < k && ng) {
+      LWord wd;
+      wd.base = wbytes;
+      wd.off = (u32)(M.ws - A0);
+      const u32 gb = incG - ng, eb = incE - ne;
+      const Plan P = plan_word<true>(wd, L, T, &F, gb, eb);
       FWord fw;
-      fw.sbase = (uint16_t)(incS - ns); fw.ns = (uint16_t)ns;
-      fw.pbase = (uint16_t)pbase; fw.np = (uint16_t)np;
-      fw.lconst = lconst; fw.pad = 0; fw.pad2 = 0;
-      fw.c0 = M.c0;
+      fw.gbase = (uint16_t)gb; fw.ng = (uint16_t)P.ng; fw.ebase = (uint16_t)eb; fw.np = (uint16_t)P.np;
+      fw.lconst = P.lconst; fw.maxl = P.maxl; fw.c0 = M.c0; fw.pad = 0;
       F.words[lane] = fw;
-      if (si != incS || pi != incP) atomicOr(a.err, A5X_DERR_STATE);
-      maxl = mlen + lconst;
+      if (!P.ok || P.ng != ng || P.ne != ne || P.np != ff_np(M.fl)) atomicOr(a.err, A5X_DERR_STATE);
+      maxl = P.maxl;
     }
     const u32 winmax = wave_max_u32(maxl);
     WAVE_SYNC();
@@ -1200,32 +1061,8 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
     const u64 r0 = g - uniform64(M.c0);
     u64 pos = uniform64(M.bo) - a.out_base;
     if (r0) {
-      // closed-form prefix bytes of candidates [0, r0) of word w (lanes over its slots)
       const FWord f0 = F.words[0];
-      const u64 Y = r0 + 1;
-      u64 Rl = 1;
-      FSlot sl;
-      if (lane < f0.ns) { sl = F.slots[f0.sbase + lane]; Rl = sl.R; }
-      u64 inc = Rl;  // inclusive prefix product of R over slots
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const u64 y = shfl_up_u64(inc, d);
-        if ((int)lane >= d) inc *= y;
-      }
-      i64 part = 0, base0 = 0;
-      if (lane < f0.ns) {
-        const u64 Q = inc / Rl, full = Y / inc, rem = Y % inc;
-        const int l0 = (int)(sl.plen4 & 255u);
-        base0 = l0;
-        for (u32 v = 1; v < sl.R; v++) {
-          const u64 lo = (u64)v * Q;
-          const u64 cnt = full * Q + (rem > lo ? min(Q, rem - lo) : 0);
-          part += ((i64)((sl.plen4 >> (8 * v)) & 255u) - l0) * (i64)cnt;
-        }
-      }
-      // every candidate = lconst + digit-0 piece lengths + deltas
-      const i64 lbase = wave_sum_i64(base0) + f0.lconst;
-      pos += (u64)((i64)r0 * lbase + wave_sum_i64(part));
+      pos += fast_prefix_bytes(F.groups + f0.gbase, f0.ng, f0.lconst, r0);
     }
     if (!R.open || R.pos != pos) {
       if (R.open && pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
@@ -1251,31 +1088,11 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
         jcur = j;
       }
       const FWord fw = F.words[lo];
+      // pass 1: group digits -> per-piece fields (digit | (R-1) << 3) << 6 (i mod 10);
+      // literal pieces keep field 0 (R = 1, entry 0)
       u32 len = 0;
-      u64 dig = 0;
-      if (act) {
-        u32 n = (u32)(rr + lane - fw.c0 + 1);
-        len = fw.lconst;
-        const FSlot* sp = F.slots + fw.sbase;
-        for (u32 i = 0; i < fw.ns; i += 2) {
-          const FSlot s0 = sp[i];
-          const FSlot s1 = sp[i + 1];  // may read past the word: unused then
-          {
-            const u32 q = fastdiv(n, s0.magic, s0.shift);
-            const u32 d = n - q * s0.R;
-            n = q;
-            dig |= (u64)d << (2 * s0.ps);
-            len += (s0.plen4 >> (8 * d)) & 255u;
-          }
-          if (i + 1 < fw.ns) {
-            const u32 q = fastdiv(n, s1.magic, s1.shift);
-            const u32 d = n - q * s1.R;
-            n = q;
-            dig |= (u64)d << (2 * s1.ps);
-            len += (s1.plen4 >> (8 * d)) & 255u;
-          }
-        }
-      }
+      u64 dlo = 0, dhi = 0;
+      if (act) len = fw_pass1(F.groups + fw.gbase, fw.ng, fw.lconst, (u32)(rr + lane - fw.c0 + 1), dlo, dhi);
       STAMP(4);
       const u32 incl = wave_incl_scan_u32(len);
       const u32 tot = lane63(incl);
@@ -1283,23 +1100,25 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
       // deferred flush of the previous round's complete blocks (their ORs are long done)
       if (pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
       STAMP(7);
-      if (act) {
-        const u64 off = R.pos + incl - len - R.base;
-        Emit e;
-        e.acc = 0; e.n = (u32)off & 3u; e.dw = (u32)(off >> 2);
-        const FPiece* pp = F.pieces + fw.pbase * 4;
-        for (u32 i = 0; i < fw.np; i += 4) {
-          // four piece loads in flight before their ORs
-          FPiece P[4];
-#pragma unroll
-          for (u32 t = 0; t < 4; t++) P[t] = pp[(i + t) * 4 + (i + t < 32 ? ((u32)(dig >> (2 * (i + t))) & 3u) : 0u)];
-#pragma unroll
-          for (u32 t = 0; t < 4; t++) {
-            const bool live = i + t < fw.np;  // pieces past np belong to the next word
-            put4(e, ring, live ? P[t].b4 : 0u, live ? P[t].len : 0u);
-          }
+      // pass 2: entry of piece i = row_i + digit_i, row_{i+1} = row_i + R_i (from the
+      // fields, so entry reads do not wait on each other); OR each piece at its offset
+      if (act && fw.np) {
+        u32 o = (u32)(R.pos + incl - len - R.base);  // ring-relative byte offset
+        u32 row = fw.ebase;
+        u64 cur = dlo;
+        u64 e = F.ent[row + ((u32)cur & 7u)];
+        for (u32 i = 0; i < fw.np; i++) {
+          row += (((u32)cur >> 3) & 7u) + 1u;
+          cur = (i == 9) ? dhi : (cur >> 6);
+          const u64 en = F.ent[min(row + ((u32)cur & 7u), (u32)FW_WE - 1u)];  // next piece, in flight
+          const u32 plen = (u32)(e >> 56) & 7u;
+          const u64 c = e & FW_M56;
+          const u32 sh = (o & 7u) * 8u;
+          atomicOr(ring64 + ((o >> 3) & (FW_RING / 8 - 1)), (unsigned long long)(c << sh));
+          if ((o & 7u) + plen > 8u) atomicOr(ring64 + (((o >> 3) + 1u) & (FW_RING / 8 - 1)), (unsigned long long)(c >> (64u - sh)));
+          o += plen;
+          e = en;
         }
-        if (e.n) atomicOr(&ring[e.dw & (FW_RING / 4 - 1)], (u32)e.acc);
       }
       R.pos += tot;
       pend = R.pos & ~15ull;
@@ -1319,7 +1138,7 @@ __device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArg
 
 __device__ __forceinline__ u32 lds_per_wave_fast() { return (FW_RING + (u32)sizeof(FWin) + 15u) & ~15u; }
 
-__global__ void __launch_bounds__(256) k_expand_fast(ExpArgs a) {
+__global__ void __launch_bounds__(256, 3) k_expand_fast(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   load_table(smem, a.table, a.table_bytes);
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
@@ -1422,7 +1241,20 @@ __global__ void __launch_bounds__(64) k_locate(ExpArgs a, const u64* cands, u32 
     }
     const u64 w = lo, r = g - a.cand_off[w];
     u64 pos = a.byte_off[w];
-    if (r) {
+    if (r && (a.flags[w] & A5X_WF_FAST)) {
+      // FAST words: the unit-radix order of k_expand_fast (cluster units included)
+      FWin& F = *(FWin*)&S;
+      if (lane_id() == 0) {
+        GWord gw;
+        gw.p = a.words + a.woff[w];
+        const Plan P = plan_word<true>(gw, (u32)(a.woff[w + 1] - a.woff[w]), T, &F, 0, 0);
+        F.words[0].ng = (uint16_t)P.ng;
+        F.words[0].lconst = P.lconst;
+        if (!P.ok) atomicOr(a.err, A5X_DERR_STATE);
+      }
+      WAVE_SYNC();
+      pos += fast_prefix_bytes(F.groups, F.words[0].ng, F.words[0].lconst, r);
+    } else if (r) {
       WordInfo I = wave_setup<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>(S, T, a.words, a.woff, w, a.mn, a.mx);
       if (!I.fits) { if (lane_id() == 0) atomicOr(a.err, A5X_DERR_STATE); return; }
       if (I.cls & A5X_WF_RADIX) pos += radix_prefix_bytes(S, T, I, r);
