@@ -41,8 +41,9 @@ struct A5xKey {
   uint32_t sumlen;        // sum of value lengths (byte DP)
   int16_t maxdelta;       // max(|v|) - klen
   uint16_t maxclen;       // max(klen, max |v|): longest choice
-  uint32_t magic;         // branch-free u32 division by R = nvals + 1 (libdivide form)
-  uint32_t shift;
+  uint16_t minclen;       // min(klen, min |v|): shortest choice
+  uint16_t pad0;
+  uint32_t pad1;
   uint32_t sum_dpos;      // sum over values of max(|v| - klen, 0)
   uint32_t sum_dneg;      // sum over values of max(klen - |v|, 0)
 };

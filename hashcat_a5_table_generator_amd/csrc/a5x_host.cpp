@@ -82,7 +82,8 @@ struct a5x_ctx {
   uint32_t table_bytes = 0;
 
   DevBuf<uint64_t> count, bytes, cand_off, byte_off, scan_tmp, locate;
-  DevBuf<uint32_t> flags, defer, chunk_w0, chunk_kind;
+  DevBuf<uint32_t> flags, defer, chunk_w0, chunk_kind, roff;
+  DevBuf<uint64_t> rec;  // FAST plan records (keyspace tiles of FW_TILE_REC u64)
   uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] nslow, [16..31] guard record
   uint32_t* h_scalars = nullptr;  // pinned
   uint64_t* h_totals = nullptr;   // pinned [0] cands [1] bytes [2..3] locate
@@ -235,10 +236,10 @@ int compile_table(a5x_ctx* c) {
       const long d = (long)v.size() - (long)k.size();
       if (d > 0) key.sum_dpos += (uint32_t)d; else key.sum_dneg += (uint32_t)(-d);
     }
-    {  // libdivide u32 branch-free magic for R = nvals + 1 (>= 2)
-      const uint32_t R = (uint32_t)vs.size() + 1, l = 32 - __builtin_clz(R - 1);
-      key.magic = (uint32_t)(((((uint64_t)1) << 32) * ((((uint64_t)1) << l) - R)) / R + 1);
-      key.shift = l - 1;
+    {
+      size_t mn = k.size();
+      for (auto& v : vs) mn = std::min(mn, v.size());
+      key.minclen = (uint16_t)std::min<size_t>(mn, 65535);
     }
     max_klen = std::max(max_klen, (uint32_t)k.size());
     keys.push_back(key);
@@ -332,7 +333,9 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   if ((rc = upload_table(c))) return rc;
   if (nw > 0xffffffffull) return fail(c, A5X_E_ARG, "batch of %llu words (max 2^32-1)", (unsigned long long)nw);
   if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
-      (rc = grow(c, c->defer, nw + 1)) || (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)))
+      (rc = grow(c, c->defer, nw + 1)) || (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)) ||
+      (rc = grow(c, c->roff, nw + 1)) ||
+      (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC + 2)))
     return rc;
   if (!d_cand_off) {
     if ((rc = grow(c, c->cand_off, nw + 1))) return rc;
@@ -350,6 +353,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
     K.mn = mn; K.mx = mx; K.count = c->count.p; K.bytes = c->bytes.p; K.flags = c->flags.p;
     K.defer_list = c->defer.p; K.defer_n = c->d_scalars; K.nbig = c->d_scalars + 1; K.err = c->d_scalars + 2;
     K.nslow = c->d_scalars + 3;
+    K.rec = c->rec.p; K.roff = c->roff.p;
     K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nw, (uint64_t)c->cus * 4));
     HIPCHK(c, a5x_launch_keyspace(K, st));
     HIPCHK(c, a5x_launch_scan(c->count.p, c->bytes.p, nw, d_cand_off, d_byte_off, c->scan_tmp.p,
@@ -400,6 +404,7 @@ A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   E.chunk_kind = c->chunk_kind.p; E.CH = c->chunk; E.mn = mn; E.mx = mx; E.err = c->d_scalars + 2;
   E.dbg = (uint64_t*)(c->d_scalars + 16);
   E.waves_per_block = c->waves_per_block;
+  E.rec = c->rec.p; E.roff = c->roff.p;
   return E;
 }
 
@@ -784,32 +789,51 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   const WordClass C = classify_word(gw, (u32)len, T, mn, mx, A5X_RING_A - 16);
   info[0] = C.count; info[1] = C.bytes; info[2] = C.flags;
   if (!(C.flags & A5X_WF_FAST) || C.count == 0) return A5X_OK;
-  std::unique_ptr<FWin> F(new FWin());
-  memset(F.get(), 0, sizeof(FWin));
-  const Plan P = plan_word<true>(gw, (u32)len, T, F.get(), 0, 0);
+  // the record exactly as k_keyspace_thread builds it
+  std::vector<u64> rec(FW_RMAX + 16, 0);
+  ArraySink sk;
+  sk.rec = rec.data(); sk.ng = ff_ng(C.flags);
+  const Plan P = plan_word<true>(gw, (u32)len, T, sk);
+  rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl);
   if (!P.ok || P.ng != ff_ng(C.flags) || P.ne != ff_ne(C.flags) || P.np != ff_np(C.flags))
     return fail(c, A5X_E_BOUNDS, "piece plan disagrees with the keyspace fields");
-  // replay k_expand_fast passes 1-2 for candidates 0..count-1 (index n = r + 1)
-  uint64_t w = 0;
-  for (uint64_t r = 0; r < C.count; r++) {
-    u64 dlo, dhi;
-    const u32 clen = fw_pass1(F->groups, P.ng, P.lconst, (u32)(r + 1), dlo, dhi);
-    if (w + clen > cap) return fail(c, A5X_E_CAPACITY, "output buffer too small");
-    u32 row = 0, got = 0;
-    u64 cur = dlo;
-    for (u32 i = 0; i < P.np; i++) {
-      const u64 e = F->ent[row + ((u32)cur & 7u)];
-      row += (((u32)cur >> 3) & 7u) + 1u;
-      cur = (i == 9) ? dhi : (cur >> 6);
-      const u32 pl = fw_len(e);
-      for (u32 b = 0; b < pl; b++) out[w + got + b] = (uint8_t)(e >> (8 * b));
-      got += pl;
+  // replay k_expand_fast: rounds of 64 lanes, passes 1-2 into a ring, head/carry
+  // hand-over exactly as the kernel does it (lanes run one after the other here)
+  if (C.bytes > cap) return fail(c, A5X_E_CAPACITY, "output buffer too small");
+  const u32 RING = 2048, mask = RING / 4 - 1;
+  std::vector<u32> ring(RING / 4, 0xA5A5A5A5u);
+  uint64_t pos = 0, flushed = 0;  // bytes written to out / complete in the ring
+  u32 carry = 0;
+  const u32 nl = std::min<u32>(64, (RING - 32) / std::max<u32>(P.maxl, 1));
+  for (uint64_t rr = 0; rr < C.count; rr += nl) {
+    const u32 nact = (u32)std::min<uint64_t>(nl, C.count - rr);
+    u32 len[64], o[64], acc[64], nn[64], head[64], dend[64];
+    u64 f[64];
+    u32 run = (u32)pos;
+    for (u32 l = 0; l < nact; l++) {
+      len[l] = fw_pass1(rec.data() + 1, P.ng, P.lconst, (u32)(rr + l + 1), f[l]);
+      o[l] = run;
+      run += len[l];
     }
-    if (got != clen) return fail(c, A5X_E_BOUNDS, "candidate %llu: pass-1 length %u != pieces %u",
-                                 (unsigned long long)r, clen, got);
-    w += got;
+    for (u32 l = 0; l < nact; l++) {
+      acc[l] = l == 0 ? carry : 0u;
+      dend[l] = fw_pass2(rec.data() + 1 + P.ng, P.np, f[l], o[l], ring.data(), mask, l != 0, &acc[l], &nn[l],
+                         &head[l]);
+    }
+    for (u32 l = 0; l + 1 < nact; l++)
+      if (nn[l]) ring[dend[l] & mask] = acc[l] | head[l + 1];
+    carry = acc[nact - 1];
+    pos = run;
+    // flush complete 16-B blocks
+    const uint64_t full = pos & ~15ull;
+    for (uint64_t X = flushed; X < full; X++) out[X] = (uint8_t)(ring[(X >> 2) & mask] >> (8 * (X & 3)));
+    flushed = std::max(flushed, full);
   }
-  info[3] = w;
+  if (pos & 3) ring[(pos >> 2) & mask] = carry;
+  for (uint64_t X = flushed; X < pos; X++) out[X] = (uint8_t)(ring[(X >> 2) & mask] >> (8 * (X & 3)));
+  if (pos != C.bytes) return fail(c, A5X_E_BOUNDS, "replayed %llu bytes, keyspace says %llu",
+                                  (unsigned long long)pos, (unsigned long long)C.bytes);
+  info[3] = pos;
   return A5X_OK;
 }
 

@@ -138,17 +138,6 @@ __device__ __forceinline__ bool key_match_global(const uint8_t* wp, u32 p, const
 }
 
 
-// The window bytes of a word in LDS, for plan_word (a5x_plan.h).
-struct LWord {
-  const uint8_t* base;  // window bytes (>= 8 readable bytes past any word)
-  u32 off;
-  __device__ __forceinline__ u32 at(u32 i) const { return base[off + i]; }
-  __device__ __forceinline__ u64 ld(u32 i, u32 n) const {
-    const u64 v = (u64)lds_ld4(base, off + i) | ((u64)lds_ld4(base, off + i + 4) << 32);
-    return keep_bytes64(v, n);
-  }
-};
-
 // ---------------------------------------------------------------------------
 // Keyspace, one lane per word (radix fast path; SURVEY 8(a) closed form)
 // ---------------------------------------------------------------------------
@@ -167,35 +156,93 @@ struct KsArgs {
   u32* nbig;
   u32* nslow;
   u32* err;
+  u64* rec;     // FAST plan records: tile t owns rec[t * FW_TILE_REC, (t + 1) * FW_TILE_REC)
+  u32* roff;    // per word: record offset (u64 units) into rec
 };
 
+// The open group of plan_word lives in LDS (FW_UMAXR u64 per lane, lane-strided);
+// entries and group descriptors go straight to the word's record in HBM.
+struct DevRecSink {
+  u64* g;       // LDS: g[a * 256]
+  u64* rec;     // global record base
+  u32 ng;
+  __device__ u64 gld(u32 a) const { return g[a * 256u]; }
+  __device__ void gst(u32 a, u64 v) { g[a * 256u] = v; }
+  __device__ void ent(u32 i, u64 v) { rec[1 + ng + i] = v; }
+  __device__ void grp(u32 i, u64 v) { rec[1 + i] = v; }
+};
+
+// One lane per word, one 256-word tile per workgroup iteration: classification,
+// closed-form (count, bytes), and for FAST words the plan record, packed densely
+// in word order inside the tile's record region (workgroup scan of the sizes).
 __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const u32 tb = (a.table_bytes + 15u) & ~15u;
+  u64* gbuf = (u64*)(smem + tb);                      // 256 x FW_UMAXR open-group entries
+  u32* wsum = (u32*)(smem + tb + 256 * FW_UMAXR * 8);  // per-wave sums of the scan
   load_table(smem, a.table, a.table_bytes);
   __syncthreads();
   const Tab T = tab_view(smem);
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < a.nw; w += stride) {
-    const u64 s = a.woff[w], e = a.woff[w + 1];
-    const u64 L64 = e - s;
-    if (L64 > A5X_LMAX_A && a.mx >= 1) {  // long words: the wave kernel (loops over positions)
-      a.flags[w] = A5X_WF_DEFER;
-      a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
-      continue;
-    }
+  const u32 tid = threadIdx.x, lane = lane_id(), wv = tid / 64;
+  const u64 ntiles = (a.nw + FW_TILE - 1) / FW_TILE;
+  for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const u64 w = tile * FW_TILE + tid;
+    const bool valid = w < a.nw;
+    WordClass C;
+    C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
+    u32 f = 0;
     GWord gw;
-    gw.p = a.words + s;
-    const WordClass C = classify_word(gw, (u32)L64, T, a.mn, a.mx, A5X_RING_A - 16);
-    u32 f = C.flags;
-    if (C.ovf) atomicOr(a.err, A5X_DERR_OVF);
-    if ((f & A5X_WF_DEFER) || (!(f & (A5X_WF_FAST | A5X_WF_RADIX | A5X_WF_ERR_OVF)))) {
-      // capped windows, unit limits, or a cluster word that is not FAST: the DP kernel
-      f = A5X_WF_DEFER;
-      a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
-    } else if (!(f & (A5X_WF_FAST | A5X_WF_ERR_OVF))) {
-      atomicAdd(a.nslow, 1u);
+    u32 L = 0;
+    if (valid) {
+      const u64 s = a.woff[w], e = a.woff[w + 1];
+      const u64 L64 = e - s;
+      gw.p = a.words + s;
+      L = (u32)min(L64, (u64)0xffffffffu);
+      if (L64 > A5X_LMAX_A && a.mx >= 1) {  // long words: the wave kernel (loops over positions)
+        f = A5X_WF_DEFER;
+      } else {
+        C = classify_word(gw, L, T, a.mn, a.mx, A5X_RING_A - 16);
+        f = C.flags;
+        if (C.ovf) atomicOr(a.err, A5X_DERR_OVF);
+        if ((f & A5X_WF_DEFER) || !(f & (A5X_WF_FAST | A5X_WF_RADIX | A5X_WF_ERR_OVF)))
+          f = A5X_WF_DEFER;  // capped windows, unit limits, non-FAST clusters: the DP kernel
+      }
     }
-    a.count[w] = C.count; a.bytes[w] = C.bytes; a.flags[w] = f;
+    // record sizes -> exclusive workgroup scan
+    const bool fast = valid && (f & A5X_WF_FAST) && C.count > 0;
+    const u32 rs = fast ? ff_rsize(f) : 0u;
+    const u32 inc = wave_incl_scan_u32(rs);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    u32 base = 0;
+    for (u32 k = 0; k < wv; k++) base += wsum[k];
+    __syncthreads();
+    const u32 ro = base + inc - rs;
+    bool built = false;
+    if (fast && ro + rs <= FW_TILE_REC) {
+      u64* rec = a.rec + tile * FW_TILE_REC + ro;
+      DevRecSink sk;
+      sk.g = gbuf + tid; sk.rec = rec; sk.ng = ff_ng(f);
+      const Plan P = plan_word<true>(gw, L, T, sk);
+      rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl);
+      if (!P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
+      a.roff[w] = (u32)(tile * FW_TILE_REC + ro);
+      built = true;
+    }
+    if (valid) {
+      if ((f & A5X_WF_FAST) && C.count > 0 && !built) {
+        // the tile's record budget is spent: the slow path takes the word
+        f = C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
+      }
+      if (f & A5X_WF_DEFER) {
+        a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
+      } else if (!(f & (A5X_WF_FAST | A5X_WF_ERR_OVF))) {
+        atomicAdd(a.nslow, 1u);
+      }
+      a.count[w] = (f & A5X_WF_DEFER) ? 0 : C.count;
+      a.bytes[w] = (f & A5X_WF_DEFER) ? 0 : C.bytes;
+      a.flags[w] = f;
+    }
   }
 }
 
@@ -436,7 +483,7 @@ __device__ WordInfo wave_setup(WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, con
 // Keyspace for deferred words: one wave per word (pass-B budget)
 // ---------------------------------------------------------------------------
 typedef WaveLds<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B> LdsB;
-static_assert(sizeof(FWin) <= sizeof(WaveLds<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>), "k_locate aliases an FWin onto LdsB");
+static_assert(FW_RMAX * 8 <= sizeof(WaveLds<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>), "k_locate stages a record in LdsB");
 typedef WaveLds<A5X_LMAX_A, A5X_MLMAX_A, A5X_DPENT_A> LdsA;
 
 __global__ void __launch_bounds__(64) k_keyspace_wave(KsArgs a) {
@@ -593,6 +640,8 @@ struct ExpArgs {
   int mn, mx;
   u32* err;
   u64* dbg;              // 8-word debug record of the first tripped guard
+  const u64* rec;        // FAST plan records (k_keyspace_thread)
+  const u32* roff;       // per word: record offset into rec
 };
 
 // Record the first tripped guard (code + context) and flag the call as failed.
@@ -893,265 +942,239 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 }
 
 // ---------------------------------------------------------------------------
-// k_expand_fast: windows of consecutive FAST words (radix, <= 64 B; every
-// substitution unit has <= 8 choices of <= 7 bytes).
+// k_expand_fast: one wave per CH-candidate chunk; windows of consecutive FAST
+// words of one keyspace tile.
 //
-// Piece plan (plan_word, shared by k_keyspace_thread and the window setup):
-// a word is cut left to right into pieces of <= 7 bytes.  A *group* piece holds
-// one or more consecutive substitution units (a key match with its R = 1 + nvals
-// choices) together with the literal bytes between/before/after them, with all
-// R_1 x R_2 x ... <= 8 combinations precombined; a *literal* piece holds <= 7
-// plain bytes.  Combination index a_1 + R_1 (a_2 + R_2 (...)) of a group is
-// exactly the mixed-radix digit order of the units (left unit least significant),
-// so candidate numbering is the same as the per-unit radix order used by
-// k_locate and the other expansion kernels.
-//
-// Device format per window (LDS): entries u64 = 7 content bytes + meta byte
-// (len | (R-1) << 3), the R entries of a piece consecutive; FGroup per group
-// piece (libdivide magic for R, digit shift 3 * piece index, 4-bit lengths of
-// its R entries).  Rounds of <= 64 consecutive candidates span word boundaries:
-// pass 1 = one division + one LDS read per group (3-bit digits packed per piece),
-// wave scan of lengths; pass 2 = one entry read + one or two ds_or_b64 per piece
-// at the candidate's byte offset in a zeroed per-wave ring (OR is exact: every
-// output byte is written by exactly one piece; zeros elsewhere).  Complete 16-B
-// ring blocks are streamed out with 16-B stores one round later.
+// The plan records (a5x_plan.h) were built by k_keyspace_thread, packed in word
+// order per tile, so a window's records are ONE contiguous HBM range: the window
+// setup is a 16-B-per-lane copy into LDS plus one metadata load per word.
+// Rounds of <= 64 consecutive candidates span word boundaries (lane = candidate):
+//   pass 1  one u64 LDS read + one umulhi per group -> length + per-piece digits;
+//   scan    DPP wave prefix sum of the lengths -> byte offsets;
+//   pass 2  one entry read per piece, bytes appended to whole aligned dwords of a
+//           per-wave LDS ring (fw_pass2: plain ds_write_b32, no atomics, no
+//           zeroing; a dword shared by two candidates is completed by the earlier
+//           lane with the later lane's head bytes, the round's last partial dword
+//           is carried into the next round in a register);
+//   flush   complete 16-B ring blocks -> global_store_dwordx4 (1 KiB per wave
+//           instruction, consecutive lanes consecutive addresses).
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
-// Offsets of word wl (lane-parallel window metadata, one round trip).
-struct WMeta {
-  u64 c0, c1, ws, we, bo;
-  u32 fl;
+#define FX_RING 2048  // per-wave output ring (bytes)
+#define FX_WREC 256   // window record budget (u64)
+#define FX_WW 32      // window words
+
+struct FXWin {
+  u64 rec[FX_WREC];   // the window's records
+  u64 wc0[FX_WW];     // first global candidate of word j
+  u32 winfo[FX_WW];   // record base (u64 index) | ng << 9 | np << 13 | lconst << 17
 };
-__device__ __forceinline__ WMeta load_meta(const ExpArgs& a, u64 wl, bool inb) {
-  WMeta m;
-  m.c0 = inb ? a.cand_off[wl] : ~0ull;
-  m.c1 = inb ? a.cand_off[wl + 1] : ~0ull;
-  m.ws = inb ? a.woff[wl] : 0;
-  m.we = inb ? a.woff[wl + 1] : 0;
-  m.bo = inb ? a.byte_off[wl] : 0;
-  m.fl = inb ? a.flags[wl] : 0u;
-  return m;
-}
-
-
-#define FW_PF 3  // prefetched window-byte dwords per lane (>= (FW_WB + 8) / 4 / 64)
+static_assert(FW_RMAX <= FX_WREC, "a FAST record must fit a window");
 
 // Closed-form bytes of candidates [0, r) of a FAST word (candidate r <-> index r + 1
-// in the group mixed radix, group 0 least significant).  Wave-collective: lanes over
-// the word's groups (ng <= 64).
-__device__ u64 fast_prefix_bytes(const FGroup* gp, u32 ng, u32 lconst, u64 r) {
+// in the group mixed radix, group 0 least significant).  rec = the word's record
+// (LDS).  Wave-collective: lanes over the word's groups (ng <= FW_PMAX).
+__device__ u64 fast_prefix_bytes(const u64* rec, u64 r) {
   const u32 lane = lane_id();
+  const u64 hdr = rec[0];
+  const u32 ng = frh_ng(hdr);
   const u64 Y = r + 1;
-  u64 Rl = 1;
-  FGroup G;
-  if (lane < ng) { G = gp[lane]; Rl = G.R; }
+  u64 Rl = 1, G = 0;
+  if (lane < ng) { G = rec[1 + lane]; Rl = frg_R(G); }
   u64 inc = Rl;  // inclusive prefix product of R over groups
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
+  for (int d = 1; d < 16; d <<= 1) {
     const u64 y = shfl_up_u64(inc, d);
     if ((int)lane >= d) inc *= y;
   }
   i64 part = 0, base0 = 0;
   if (lane < ng) {
     const u64 Q = inc / Rl, full = Y / inc, rem = Y % inc;
-    const int l0 = (int)(G.plen & 15u);
+    const int l0 = (int)frg_len(G, 0);
     base0 = l0;
-    for (u32 v = 1; v < G.R; v++) {
+    for (u32 v = 1; v < (u32)Rl; v++) {
       const u64 lo = (u64)v * Q;
       const u64 cnt = full * Q + (rem > lo ? min(Q, rem - lo) : 0);
-      part += ((i64)((G.plen >> (4 * v)) & 15u) - l0) * (i64)cnt;
+      part += ((i64)frg_len(G, v) - l0) * (i64)cnt;
     }
   }
   // every candidate = lconst + digit-0 group lengths + deltas
-  const i64 lbase = wave_sum_i64(base0) + lconst;
+  const i64 lbase = wave_sum_i64(base0) + frh_lconst(hdr);
   return (u64)((i64)r * lbase + wave_sum_i64(part));
 }
 
-__device__ void expand_chunk_fast(FWin& F, u32* ring, const Tab& T, const ExpArgs& a, u64 chunk) {
+// stream complete blocks [R.flushed, upto) (upto 16-aligned) of the ring
+__device__ __forceinline__ void fx_flush(Run& R, const u32* ring, const ExpArgs& a, u64 upto, u64 hi) {
   const u32 lane = lane_id();
-  unsigned long long* ring64 = (unsigned long long*)ring;
+  const u32 nb = (u32)((upto - R.flushed) / 16);
+  for (u32 b = lane; b < nb; b += 64) {
+    const u64 X = R.flushed + (u64)b * 16;
+    const uint4 v = ((const uint4*)ring)[((u32)(X - R.base) / 16u) & (FX_RING / 16 - 1)];
+    store_block(a, X, v, R.lo, hi);
+  }
+  R.flushed = upto;
+}
+
+// write the carried partial dword, flush everything up to R.pos (tail block byte-exact)
+__device__ __forceinline__ void fx_close(Run& R, u32* ring, const ExpArgs& a, u32 carry) {
+  if (!R.open) return;
+  if (R.pos & 3u) {
+    if (lane_id() == 0) ring[((u32)(R.pos - R.base) >> 2) & (FX_RING / 4 - 1)] = carry;
+    WAVE_SYNC();
+  }
+  const u64 full = R.pos & ~15ull;
+  if (full > R.flushed) fx_flush(R, ring, a, full, R.pos);
+  if (R.pos > R.flushed) fx_flush(R, ring, a, R.flushed + 16, R.pos);
+  WAVE_SYNC();
+  R.open = false;
+}
+
+__device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
+  const u32 lane = lane_id();
   const u64 g0 = max(a.cand_begin, chunk * a.CH);
   const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
   if (g0 >= g1) return;
   u64 w = a.chunk_w0[chunk];
-  const u64 wtotal = a.woff[a.nw];  // bytes of the word buffer (prefetch bound)
   if (w >= a.nw) { guard_trip(a, 2, chunk, w, g0, a.nw); return; }
   while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
   if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
   u64 g = g0;
   Run R;
   R.open = false;
-  u64 pend = 0;  // complete blocks [R.flushed, pend) awaiting the deferred flush
-  const uint8_t* wbytes = (const uint8_t*)F.bytes32;
-  WMeta M = load_meta(a, w + lane, lane < FW_WW && w + lane < a.nw);
-  u64 pfbase = ~0ull;  // dword-aligned byte address of the prefetched window bytes
-  u32 pf[FW_PF];
+  u32 carry = 0;
   STAMP_DECL
   while (g < g1) {
     if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
-    // ---- window extent: lane j <-> word w + j ----
-    const bool inb = lane < FW_WW && w + lane < a.nw;
-    const bool fast = inb && (M.fl & A5X_WF_FAST) && M.c0 < g1;
-    const u32 L = fast ? (u32)(M.we - M.ws) : 0u;
-    const u32 ng = fast ? ff_ng(M.fl) : 0u;
-    const u32 ne = fast ? ff_ne(M.fl) : 0u;
-    const u32 incL = wave_incl_scan_u32(L);
-    const u32 incG = wave_incl_scan_u32(ng);
-    const u32 incE = wave_incl_scan_u32(ne);
-    const bool ok = fast && incL + 3 <= FW_WB && incG <= FW_WG && incE <= FW_WE;
+    // ---- window: lane j <-> word w + j (same keyspace tile) ----
+    const u64 wl = w + lane;
+    const bool inb = lane < FX_WW && wl < a.nw && wl / FW_TILE == w / FW_TILE;
+    const u64 c0 = inb ? a.cand_off[wl] : ~0ull;
+    const u64 c1 = inb ? a.cand_off[wl + 1] : ~0ull;
+    const u32 fl = inb ? a.flags[wl] : 0u;
+    const bool hasc = inb && c1 > c0;
+    const bool fast = inb && (fl & A5X_WF_FAST) && c0 < g1;
+    const u32 rs = (fast && hasc) ? ff_rsize(fl) : 0u;
+    const u32 incR = wave_incl_scan_u32(rs);
+    const bool ok = fast && incR <= FX_WREC;
     const u64 badm = __ballot(!ok);
     const u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
     STAMP(0);
     if (k == 0) {
       // word w is a hole here (slow / BIG) or empty
-      const u64 w0c1 = uniform64(M.c1);
+      const u64 w0c1 = uniform64(c1);
       if (w0c1 > g) {
-        if (R.open && pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
-        run_close<FW_RING>(R, ring, a);
+        fx_close(R, ring, a, carry);
         g = min(w0c1, g1);
       }
       w++;
-      M = load_meta(a, w + lane, lane < FW_WW && w + lane < a.nw);
       continue;
     }
-    // ---- window bytes -> LDS (aligned dwords; prefetched when contiguous) ----
-    const u64 A0 = uniform64(M.ws) & ~3ull;
-    const u64 Aend = uniform64(shfl_u64(M.we, (int)k - 1));
-    if (Aend < A0 || Aend - A0 > FW_WB || w + k > a.nw) {
-      guard_trip(a, 5, chunk, w, k, Aend - A0);
-      break;
+    // ---- records -> LDS (one contiguous range), word info ----
+    const u64 fm = __ballot(lane < k && rs > 0);
+    if (fm == 0) {  // only words without candidates: skip them
+      w += k;
+      continue;
     }
-    const u32 ndw = (u32)((Aend - A0 + 3) / 4);
-    if (A0 == pfbase) {
-#pragma unroll
-      for (u32 t = 0; t < FW_PF; t++) F.bytes32[lane + 64 * t] = (lane + 64 * t < ndw) ? pf[t] : 0u;
-    } else {
-      const u32* src = (const u32*)(a.words + A0);
-      for (u32 i = lane; i < ndw + 2; i += 64) F.bytes32[i] = i < ndw ? src[i] : 0u;
+    const u32 jf = (u32)__builtin_ctzll(fm);
+    const u32 roff = (lane < k && rs > 0) ? a.roff[wl] : 0u;
+    const u64 src0 = (u64)readlane_u32(roff, jf);
+    const u32 ntot = readlane_u32(incR, k - 1);
+    {
+      const uint4* src = (const uint4*)(a.rec + src0);  // records are 8-B aligned: copy u64 pairs
+      const u64* s64 = a.rec + src0;
+      if ((src0 & 1) == 0) {
+        for (u32 i = lane; i < (ntot + 1) / 2; i += 64) ((uint4*)F.rec)[i] = src[i];
+      } else {
+        for (u32 i = lane; i < ntot; i += 64) F.rec[i] = s64[i];
+      }
     }
+    const u32 rb = incR - rs;
+    const u64 bo = (lane == 0) ? a.byte_off[w] : 0;
     WAVE_SYNC();
-    // ---- prefetch the next window (metadata + bytes from this window's end) ----
-    const WMeta Mn = load_meta(a, w + k + lane, lane < FW_WW && w + k + lane < a.nw);
-    pfbase = Aend & ~3ull;
-#pragma unroll
-    for (u32 t = 0; t < FW_PF; t++) {
-      const u64 addr = pfbase + 4ull * (lane + 64 * t);
-      pf[t] = addr + 4 <= wtotal + 16 ? *(const u32*)(a.words + addr) : 0u;
-    }
-    STAMP(1);
-    // ---- piece plan, lane per word (words without candidates have none) ----
     u32 maxl = 0;
-    if (lane < k && ng) {
-      LWord wd;
-      wd.base = wbytes;
-      wd.off = (u32)(M.ws - A0);
-      const u32 gb = incG - ng, eb = incE - ne;
-      const Plan P = plan_word<true>(wd, L, T, &F, gb, eb);
-      FWord fw;
-      fw.gbase = (uint16_t)gb; fw.ng = (uint16_t)P.ng; fw.ebase = (uint16_t)eb; fw.np = (uint16_t)P.np;
-      fw.lconst = P.lconst; fw.maxl = P.maxl; fw.c0 = M.c0; fw.pad = 0;
-      F.words[lane] = fw;
-      if (!P.ok || P.ng != ng || P.ne != ne || P.np != ff_np(M.fl)) atomicOr(a.err, A5X_DERR_STATE);
-      maxl = P.maxl;
+    if (lane < k) {
+      F.wc0[lane] = c0;
+      u32 info = 0;
+      if (rs) {
+        const u64 hdr = F.rec[rb];
+        maxl = frh_maxl(hdr);
+        info = rb | (frh_ng(hdr) << 9) | (frh_np(hdr) << 13) | (frh_lconst(hdr) << 17);
+      }
+      F.winfo[lane] = info;
     }
     const u32 winmax = wave_max_u32(maxl);
     WAVE_SYNC();
-    STAMP(2);
+    STAMP(1);
     // ---- run position of g ----
-    const u64 r0 = g - uniform64(M.c0);
-    u64 pos = uniform64(M.bo) - a.out_base;
-    if (r0) {
-      const FWord f0 = F.words[0];
-      pos += fast_prefix_bytes(F.groups + f0.gbase, f0.ng, f0.lconst, r0);
-    }
+    const u64 wc0 = uniform64(c0);
+    const u64 r0 = g - wc0;
+    u64 pos = uniform64(bo) - a.out_base;
+    if (r0) pos += fast_prefix_bytes(F.rec + (F.winfo[0] & 511u), r0);
     if (!R.open || R.pos != pos) {
-      if (R.open && pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
-      run_close<FW_RING>(R, ring, a);
-      run_open<FW_RING>(R, pos);
-      pend = R.flushed;
+      fx_close(R, ring, a, carry);
+      run_open<FX_RING>(R, pos);
+      carry = 0;
     }
-    STAMP(3);
-    // ---- rounds: two rounds of bytes live in the ring (deferred flush) ----
-    const u64 gend = min(g1, uniform64(shfl_u64(M.c1, (int)k - 1)));
-    const u32 nl = uniform(min(64u, (FW_RING / 2 - 16) / max(winmax, 1u)));
-    const u32 c0rel = (lane < k) ? (u32)(M.c0 > g ? M.c0 - g : 0) : 0xffffffffu;
+    STAMP(2);
+    // ---- rounds ----
+    const u64 gend = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
+    const u32 nl = uniform(min(64u, (FX_RING - 32) / max(winmax, 1u)));
+    const u32 c0rel = (lane < k) ? (u32)(c0 > g ? c0 - g : 0) : 0xffffffffu;
     u32 jcur = 0;  // word holding the round's first candidate (uniform)
     for (u64 rr = g; rr < gend; rr += nl) {
       const u32 rrel = (u32)(rr - g);
-      const bool act = lane < nl && rr + lane < gend;
+      const u32 nact = (u32)min((u64)nl, gend - rr);
+      const bool act = lane < nact;
       // word of each lane's candidate: walk the (uniform) words starting in this round
       u32 lo = jcur;
       for (u32 j = jcur + 1; j < k; j++) {
         const u32 sj = readlane_u32(c0rel, j);
-        if (sj >= rrel + nl) break;
+        if (sj >= rrel + nact) break;
         if (rrel + lane >= sj) lo = j;
         jcur = j;
       }
-      const FWord fw = F.words[lo];
-      // pass 1: group digits -> per-piece fields (digit | (R-1) << 3) << 6 (i mod 10);
-      // literal pieces keep field 0 (R = 1, entry 0)
+      const u32 info = F.winfo[lo];
+      const u64 wc = F.wc0[lo];
+      const u32 wrb = info & 511u, ng = (info >> 9) & 15u, np = (info >> 13) & 15u, lconst = info >> 17;
+      u64 f = 0;
       u32 len = 0;
-      u64 dlo = 0, dhi = 0;
-      if (act) len = fw_pass1(F.groups + fw.gbase, fw.ng, fw.lconst, (u32)(rr + lane - fw.c0 + 1), dlo, dhi);
-      STAMP(4);
+      if (act) len = fw_pass1(F.rec + wrb + 1, ng, lconst, (u32)(rr + lane - wc + 1), f);
+      STAMP(3);
       const u32 incl = wave_incl_scan_u32(len);
       const u32 tot = lane63(incl);
-      STAMP(5);
-      // deferred flush of the previous round's complete blocks (their ORs are long done)
-      if (pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
-      STAMP(7);
-      // pass 2: entry of piece i = row_i + digit_i, row_{i+1} = row_i + R_i (from the
-      // fields, so entry reads do not wait on each other); OR each piece at its offset
-      if (act && fw.np) {
-        u32 o = (u32)(R.pos + incl - len - R.base);  // ring-relative byte offset
-        u32 row = fw.ebase;
-        u64 cur = dlo;
-        u64 e = F.ent[row + ((u32)cur & 7u)];
-        for (u32 i = 0; i < fw.np; i++) {
-          row += (((u32)cur >> 3) & 7u) + 1u;
-          cur = (i == 9) ? dhi : (cur >> 6);
-          const u64 en = F.ent[min(row + ((u32)cur & 7u), (u32)FW_WE - 1u)];  // next piece, in flight
-          const u32 plen = (u32)(e >> 56) & 7u;
-          const u64 c = e & FW_M56;
-          const u32 sh = (o & 7u) * 8u;
-          atomicOr(ring64 + ((o >> 3) & (FW_RING / 8 - 1)), (unsigned long long)(c << sh));
-          if ((o & 7u) + plen > 8u) atomicOr(ring64 + (((o >> 3) + 1u) & (FW_RING / 8 - 1)), (unsigned long long)(c >> (64u - sh)));
-          o += plen;
-          e = en;
-        }
-      }
+      const u32 o = (u32)(R.pos - R.base) + incl - len;
+      u32 acc = (lane == 0) ? carry : 0u, n = 0, head = 0, Dend = 0;
+      if (act) Dend = fw_pass2(F.rec + wrb + 1 + ng, np, f, o, ring, FX_RING / 4 - 1, lane != 0, &acc, &n, &head);
+      const u32 hnext = (u32)__shfl_down((int)head, 1);
+      if (act && lane + 1 < nact && n) ring[Dend & (FX_RING / 4 - 1)] = acc | hnext;
+      carry = readlane_u32(acc, nact - 1);
       R.pos += tot;
-      pend = R.pos & ~15ull;
+      STAMP(4);
       WAVE_SYNC();
-      STAMP(6);
+      const u64 full = R.pos & ~15ull;
+      if (full > R.flushed) fx_flush(R, ring, a, full, R.pos);
+      STAMP(5);
     }
     g = gend;
     w += k;
-    M = Mn;
     WAVE_SYNC();
   }
-  if (R.open && pend > R.flushed) run_flush<FW_RING>(R, ring, a, pend, R.pos);
-  run_close<FW_RING>(R, ring, a);
-  STAMP(8);
+  fx_close(R, ring, a, carry);
+  STAMP(6);
   STAMP_FLUSH();
 }
 
-__device__ __forceinline__ u32 lds_per_wave_fast() { return (FW_RING + (u32)sizeof(FWin) + 15u) & ~15u; }
+__device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + (u32)sizeof(FXWin) + 15u) & ~15u; }
 
-__global__ void __launch_bounds__(256, 3) k_expand_fast(ExpArgs a) {
+__global__ void __launch_bounds__(256) k_expand_fast(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  load_table(smem, a.table, a.table_bytes);
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
-  const u32 tb = (a.table_bytes + 15u) & ~15u;
-  uint8_t* mine = smem + tb + wv * lds_per_wave_fast();
+  uint8_t* mine = smem + wv * lds_per_wave_fast();
   u32* ring = (u32*)mine;
-  FWin& F = *(FWin*)(mine + FW_RING);
-  for (u32 i = lane_id(); i < FW_RING / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  const Tab T = tab_view(smem);
+  FXWin& F = *(FXWin*)(mine + FX_RING);
   const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
   if (chunk * a.CH >= a.cand_end) return;
-  expand_chunk_fast(F, ring, T, a, chunk);
+  expand_chunk_fast(F, ring, a, chunk);
 }
 
 // k_expand_slow: non-FAST, non-BIG words (overlapping keys, capped windows,
@@ -1242,18 +1265,12 @@ __global__ void __launch_bounds__(64) k_locate(ExpArgs a, const u64* cands, u32 
     const u64 w = lo, r = g - a.cand_off[w];
     u64 pos = a.byte_off[w];
     if (r && (a.flags[w] & A5X_WF_FAST)) {
-      // FAST words: the unit-radix order of k_expand_fast (cluster units included)
-      FWin& F = *(FWin*)&S;
-      if (lane_id() == 0) {
-        GWord gw;
-        gw.p = a.words + a.woff[w];
-        const Plan P = plan_word<true>(gw, (u32)(a.woff[w + 1] - a.woff[w]), T, &F, 0, 0);
-        F.words[0].ng = (uint16_t)P.ng;
-        F.words[0].lconst = P.lconst;
-        if (!P.ok) atomicOr(a.err, A5X_DERR_STATE);
-      }
+      // FAST words: the group radix order of k_expand_fast (record from HBM)
+      u64* rec = (u64*)&S;
+      const u32 rs = ff_rsize(a.flags[w]);
+      for (u32 i2 = lane_id(); i2 < rs; i2 += 64) rec[i2] = a.rec[a.roff[w] + i2];
       WAVE_SYNC();
-      pos += fast_prefix_bytes(F.groups, F.words[0].ng, F.words[0].lconst, r);
+      pos += fast_prefix_bytes(rec, r);
     } else if (r) {
       WordInfo I = wave_setup<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>(S, T, a.words, a.woff, w, a.mn, a.mx);
       if (!I.fits) { if (lane_id() == 0) atomicOr(a.err, A5X_DERR_STATE); return; }
@@ -1312,12 +1329,17 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
   a.mn = L.mn; a.mx = L.mx; a.count = L.count; a.bytes = L.bytes; a.flags = L.flags;
   a.defer_list = L.defer_list; a.defer_n = L.defer_n; a.nbig = L.nbig; a.nslow = L.nslow; a.err = L.err;
-  hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, 256, 65536)), dim3(256), L.table_bytes, st, a);
+  a.rec = L.rec; a.roff = L.roff;
+  hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t lds = ((L.table_bytes + 15u) & ~15u) + sizeof(LdsB);
   hipLaunchKernelGGL(k_keyspace_wave, dim3(L.defer_blocks), dim3(64), lds, st, a);
   return hipGetLastError();
+}
+
+size_t a5x_keyspace_thread_lds(u32 table_bytes) {
+  return ((table_bytes + 15u) & ~15u) + FW_TILE * FW_UMAXR * 8 + 64;
 }
 
 size_t a5x_keyspace_wave_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + sizeof(LdsB); }
@@ -1363,6 +1385,7 @@ static ExpArgs exp_args(const A5xExpLaunch& L) {
   a.cand_off = L.cand_off; a.byte_off = L.byte_off; a.flags = L.flags; a.chunk_w0 = L.chunk_w0;
   a.chunk_kind = L.chunk_kind; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.out = L.out;
   a.out_base = L.out_base; a.out_cap = L.out_cap; a.mn = L.mn; a.mx = L.mx; a.err = L.err; a.dbg = L.dbg;
+  a.rec = L.rec; a.roff = L.roff;
   return a;
 }
 
@@ -1370,7 +1393,7 @@ size_t a5x_expand_lds(u32 table_bytes, int kind, u32 waves) {
   const size_t tb = (table_bytes + 15u) & ~15u;
   if (kind == 2) return tb + ((A5X_RING_B + sizeof(LdsB) + 15u) & ~(size_t)15u);
   if (kind == 1) return tb + waves * ((A5X_RING_A + sizeof(LdsA) + 15u) & ~(size_t)15u);
-  return tb + waves * ((FW_RING + sizeof(FWin) + 15u) & ~(size_t)15u);
+  return waves * ((FX_RING + sizeof(FXWin) + 15u) & ~(size_t)15u);
 }
 
 // kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b
@@ -1420,6 +1443,8 @@ hipError_t a5x_set_kernel_attrs() {
   hipError_t e = hipFuncSetAttribute((const void*)k_expand_b, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_keyspace_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_keyspace_thread, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_locate, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;

@@ -20,6 +20,8 @@ struct A5xKsLaunch {
   uint32_t* nslow;
   uint32_t* err;
   uint32_t defer_blocks;
+  uint64_t* rec;   // FAST plan records (tile regions of FW_TILE_REC u64)
+  uint32_t* roff;  // per-word record offsets
 };
 
 struct A5xExpLaunch {
@@ -42,12 +44,15 @@ struct A5xExpLaunch {
   uint32_t* err;
   uint64_t* dbg;
   uint32_t waves_per_block;
+  const uint64_t* rec;
+  const uint32_t* roff;
 };
 
 hipError_t a5x_set_kernel_attrs();
 int a5x_read_stamps(unsigned long long* out16, int reset);
 hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st);
 size_t a5x_keyspace_wave_lds(uint32_t table_bytes);
+size_t a5x_keyspace_thread_lds(uint32_t table_bytes);
 uint64_t a5x_scan_tmp_elems(uint64_t n);
 hipError_t a5x_launch_scan(const uint64_t* ca, const uint64_t* cb, uint64_t n, uint64_t* outa, uint64_t* outb,
                            uint64_t* tmp, uint32_t* err, hipStream_t st);

@@ -70,49 +70,63 @@ A5X_HD u32 fastdiv_hd(u32 n, u32 magic, u32 shift) {
 }
 
 // ---------------------------------------------------------------------------
-// FAST window format (see k_expand_fast)
+// FAST plan records (built once per word by k_keyspace_thread, streamed by
+// k_expand_fast).  A record is a run of u64 in HBM:
+//   [0]               header  (fr_hdr)
+//   [1, 1+ng)         group descriptors, one per group piece (fr_group)
+//   [1+ng, 1+ng+ne)   piece entries: the R entries of a piece consecutive, pieces
+//                     in order; entry = 7 content bytes + meta byte (len | (R-1) << 3)
+// A word is cut left to right into pieces of <= FW_PLEN bytes: a *group* piece
+// holds one or more consecutive substitution units (a key match with its R =
+// 1 + nvals choices, or a cluster of overlapping matches) with the literal bytes
+// around them, all R_1 x R_2 x ... <= FW_UMAXR combinations precombined; a
+// *literal* piece holds plain bytes.  Combination a_1 + R_1 (a_2 + R_2 (...)) of a
+// group is the mixed-radix digit order of its units (left unit least significant),
+// and groups are digits of the word's candidate index n = rank + 1 in the same
+// order, so candidate numbering equals the per-unit radix order of the other
+// expansion kernels.
 // ---------------------------------------------------------------------------
-#define FW_WB 512   // window word-byte budget
-#define FW_WG 64    // window group-piece budget
-#define FW_WE 512   // window entry budget (u64 each)
-#define FW_WW 32    // window word budget
-#define FW_PMAX 20  // pieces per word (6-bit digit|R-1 fields, 10 per u64, two u64)
-#define FW_PLEN 7   // bytes per piece
-#define FW_RING 4096
-#define FW_UMAXM 8  // matches per cluster unit
-#define FW_UMAXR 8  // choices per unit / group
-
-static_assert(FW_WE <= 65535 && FW_WG <= 255, "window budgets");
-
-struct FGroup {   // 16 B, one per group piece
-  u32 magic;
-  uint8_t shift, R, dsh, dhi;   // digit field of piece i: dsh = 6 (i mod 10), dhi = i >= 10
-  u32 plen;                     // 4-bit length of entry a at bits 4a
-  u32 pad1;
-};
-struct FWord {    // 32 B
-  uint16_t gbase, ng, ebase, np;
-  u32 lconst;     // bytes of the literal pieces (digit-independent)
-  u32 maxl;       // longest candidate + '\n'
-  u64 c0;         // first global candidate index of the word
-  u64 pad;
-};
-struct FWin {
-  u32 bytes32[(FW_WB + 32) / 4];
-  FGroup groups[FW_WG];
-  u64 ent[FW_WE];
-  FWord words[FW_WW];
-};
+#define FW_PLEN 7    // bytes per piece
+#define FW_UMAXM 8   // matches per cluster unit
+#define FW_UMAXR 8   // choices per unit / group
+#define FW_PMAX 10   // pieces per word (6-bit digit|R-1 fields in one u64)
+#define FW_RMAX 256  // record u64 per word (window budget)
+#define FW_TILE 256  // words per keyspace tile (one workgroup)
+#define FW_TILE_REC (FW_TILE * 40)  // record u64 budget per tile (avg 320 B / word)
+#define FW_MAXL 1000 // longest candidate (+ newline) of a FAST word
+#define FW_PMAX_CNT (1u << 29)  // keyspace bound of the magic division (n * (R-1) < 2^32)
 
 #define FW_M56 0x00FFFFFFFFFFFFFFull
 A5X_HD u64 fw_meta(u32 len, u32 R) { return (u64)(len | ((R - 1u) << 3)) << 56; }
 A5X_HD u32 fw_len(u64 e) { return (u32)(e >> 56) & 7u; }
 A5X_HD u64 keep_bytes64(u64 v, u32 n) { return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1ull)); }
 
-// FAST flag fields (written by the keyspace pass)
+// header: np | ng << 4 | ne << 8 | lconst << 16 | maxl << 24 | minl << 36
+A5X_HD u64 fr_hdr(u32 np, u32 ng, u32 ne, u32 lconst, u32 maxl, u32 minl) {
+  return (u64)np | ((u64)ng << 4) | ((u64)ne << 8) | ((u64)lconst << 16) | ((u64)maxl << 24) | ((u64)minl << 36);
+}
+A5X_HD u32 frh_np(u64 h) { return (u32)h & 15u; }
+A5X_HD u32 frh_ng(u64 h) { return (u32)(h >> 4) & 15u; }
+A5X_HD u32 frh_ne(u64 h) { return (u32)(h >> 8) & 255u; }
+A5X_HD u32 frh_lconst(u64 h) { return (u32)(h >> 16) & 255u; }
+A5X_HD u32 frh_maxl(u64 h) { return (u32)(h >> 24) & 4095u; }
+A5X_HD u32 frh_minl(u64 h) { return (u32)(h >> 36) & 4095u; }
+
+// group: magic = ceil(2^32 / R) | 3-bit entry lengths << 32 | (R-1) << 56 | piece << 59.
+// q = umulhi(n, magic) = n / R exactly for n (R - 1) < 2^32 (FW_PMAX_CNT bound).
+A5X_HD u32 fr_magic(u32 R) { return (u32)((((u64)1 << 32) + R - 1) / R); }
+A5X_HD u64 fr_group(u32 R, u32 lens, u32 piece) {
+  return (u64)fr_magic(R) | ((u64)lens << 32) | ((u64)(R - 1) << 56) | ((u64)piece << 59);
+}
+A5X_HD u32 frg_R(u64 G) { return ((u32)(G >> 56) & 7u) + 1u; }
+A5X_HD u32 frg_len(u64 G, u32 d) { return (u32)(G >> (32 + 3 * d)) & 7u; }
+A5X_HD u32 frg_piece(u64 G) { return (u32)(G >> 59) & 15u; }
+
+// FAST flag fields (written by the keyspace pass): record size = 1 + ng + ne
 A5X_HD u32 ff_ng(u32 f) { return (f >> 10) & 31u; }
 A5X_HD u32 ff_ne(u32 f) { return (f >> 16) & 255u; }
 A5X_HD u32 ff_np(u32 f) { return (f >> 24) & 31u; }
+A5X_HD u32 ff_rsize(u32 f) { return 1u + ff_ng(f) + ff_ne(f); }
 
 // A word's bytes in global memory (or host memory).
 struct GWord {
@@ -150,6 +164,7 @@ struct Unit {
   u32 s, e;        // byte span [s, e) of the original word
   u32 R;           // choices; choice 0 = the span unchanged
   u32 ml;          // longest choice (bytes)
+  u32 mnl;         // shortest choice (bytes)
   u32 spos, sneg;  // sums over choices of max(len - span, 0) and max(span - len, 0)
   int maxd;        // longest choice - span
   u32 nm;          // key matches in the unit (bounds the substitutions of a choice)
@@ -169,7 +184,7 @@ A5X_HD u32 unit_mpos(const Unit& U, u32 j) { return U.s + ((u32)((j < 4 ? U.m0 :
 template <class W>
 A5X_HD void cluster_choices(const W& wd, Unit& U, const Tab& T, int target, u64* content, u32* len) {
   const u32 span = U.e - U.s;
-  u32 R = 0, ml = 0, spos = 0, sneg = 0;
+  u32 R = 0, ml = 0, mnl = 0xffffffffu, spos = 0, sneg = 0;
   int maxd = -(int)span;
   bool ok = U.ok;
   for (u32 mask = 0; mask < (1u << U.k) && ok; mask++) {
@@ -211,6 +226,7 @@ A5X_HD void cluster_choices(const W& wd, Unit& U, const Tab& T, int target, u64*
       }
       R++;
       ml = umax32(ml, n);
+      mnl = umin32(mnl, n);
       if (n > span) spos += n - span; else sneg += span - n;
       maxd = (int)n - (int)span > maxd ? (int)n - (int)span : maxd;
       // next value combination
@@ -224,7 +240,7 @@ A5X_HD void cluster_choices(const W& wd, Unit& U, const Tab& T, int target, u64*
       if (j == U.k) break;
     }
   }
-  U.R = R; U.ml = ml; U.spos = spos; U.sneg = sneg; U.maxd = maxd; U.ok = ok;
+  U.R = R; U.ml = ml; U.mnl = mnl; U.spos = spos; U.sneg = sneg; U.maxd = maxd; U.ok = ok;
 }
 
 // Next unit at or after p (p advances past it).  Returns false at the end of the word.
@@ -257,7 +273,7 @@ A5X_HD bool next_unit(const W& wd, u32 L, u32& p, const Tab& T, Unit& U) {
     if (nmatch == 1) {
       const A5xKey key = T.keys[k0];
       U.key = k0; U.k = 0;
-      U.R = key.nvals + 1u; U.ml = key.maxclen;
+      U.R = key.nvals + 1u; U.ml = key.maxclen; U.mnl = key.minclen;
       U.spos = key.sum_dpos; U.sneg = key.sum_dneg; U.maxd = key.maxdelta;
       U.ok = true;
     } else {
@@ -286,26 +302,62 @@ A5X_HD u64 unit_choice(const W& wd, const Unit& U, const Tab& T, u32 a, u32& len
 }
 
 // ---------------------------------------------------------------------------
-// piece plan
+// piece plan -> record
 // ---------------------------------------------------------------------------
 struct Plan {
-  u32 np, ng, ne, lconst, maxl;
+  u32 np, ng, ne, lconst, maxl, minl;
   bool ok;
 };
 
-// Cut a unit-radix word into pieces (see k_expand_fast).  BUILD also writes the
-// window's entries (from entry index e0) and FGroups (from g0).
-template <bool BUILD, class W>
-A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, FWin* F, u32 g0, u32 e0) {
+// Record sinks.  gld/gst: the R <= FW_UMAXR entries of the open group (built in
+// place while units merge into it); ent(i, v): final entry i; grp(g, v): group g.
+struct NullSink {
+  A5X_HD u64 gld(u32) const { return 0; }
+  A5X_HD void gst(u32, u64) {}
+  A5X_HD void ent(u32, u64) {}
+  A5X_HD void grp(u32, u64) {}
+};
+struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
+  u64* rec;
+  u32 ng;
+  u64 g[FW_UMAXR];
+  A5X_HD u64 gld(u32 a) const { return g[a]; }
+  A5X_HD void gst(u32 a, u64 v) { g[a] = v; }
+  A5X_HD void ent(u32 i, u64 v) { rec[1 + ng + i] = v; }
+  A5X_HD void grp(u32 i, u64 v) { rec[1 + i] = v; }
+};
+
+// Cut a unit-radix word into pieces (see the record format above).  BUILD: also
+// write the entries and group descriptors through the sink (the header is the
+// caller's: fr_hdr of the returned Plan).
+template <bool BUILD, class W, class S>
+A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk) {
   Plan P;
-  P.np = 0; P.ng = 0; P.ne = 0; P.lconst = 0; P.maxl = 0; P.ok = true;
+  P.np = 0; P.ng = 0; P.ne = 0; P.lconst = 0; P.maxl = 0; P.minl = 0; P.ok = true;
   bool open = false;  // a group piece is being built
-  u32 cR = 1, cmax = 0, ceb = 0, cpi = 0, cplen = 0;
+  u32 cR = 1, cmax = 0, cmin = 0, cpi = 0, cplen = 0;
   u32 prev = 0, p = 0;
   Unit U;
+  auto close_group = [&]() {
+    if constexpr (BUILD) {
+      for (u32 a = 0; a < cR; a++) sk.ent(P.ne + a, sk.gld(a));
+      sk.grp(P.ng, fr_group(cR, cplen, cpi));
+    }
+    P.ne += cR; P.ng++; P.maxl += cmax; P.minl += cmin;
+    open = false;
+  };
+  auto literal = [&](u32 off, u32 n, bool nl_last) {  // one literal piece of n bytes
+    if constexpr (BUILD) {
+      const u32 nb = nl_last ? n - 1 : n;
+      u64 v = nb ? wd.ld(off, nb) : 0ull;
+      if (nl_last) v |= 10ull << (8 * nb);
+      sk.ent(P.ne, v | fw_meta(n, 1));
+    }
+    P.ne++; P.np++; P.lconst += n; P.maxl += n; P.minl += n;
+  };
   while (P.ok && next_unit(wd, L, p, T, U)) {
     const u32 Ru = U.R, ml = U.ml, run = U.s - prev;
-    if (!U.ok || ml > FW_PLEN || Ru > FW_UMAXR) { P.ok = false; break; }
+    if (!U.ok || ml > FW_PLEN || Ru > FW_UMAXR || Ru < 2) { P.ok = false; break; }
     if (open && cmax + run + ml <= FW_PLEN && cR * Ru <= FW_UMAXR) {
       // merge: entry a1 + cR * a2 = old[a1] ++ run ++ choice a2 (descending: in place)
       const u32 nR = cR * Ru;
@@ -316,55 +368,37 @@ A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, FWin* F, u32 g0, u32 e0)
           u32 cl = 0;
           const u64 cv = unit_choice(wd, U, T, (u32)a2, cl);
           for (int a1 = (int)cR - 1; a1 >= 0; a1--) {
-            const u32 ia = ceb + (u32)a1, ib = ceb + (u32)a1 + cR * (u32)a2;
-            const u64 old = (ia < FW_WE) ? F->ent[ia] : 0ull;
+            const u64 old = sk.gld((u32)a1);
             const u32 ol = fw_len(old);
             const u32 nl = ol + run + cl;
             const u64 v = (old & FW_M56) | (rb << (8 * ol)) | (cv << (8 * (ol + run)));
-            if (ib < FW_WE) F->ent[ib] = (v & FW_M56) | fw_meta(nl, nR);
-            nplen |= nl << (4 * ((u32)a1 + cR * (u32)a2));
+            sk.gst((u32)a1 + cR * (u32)a2, (v & FW_M56) | fw_meta(nl, nR));
+            nplen |= nl << (3 * ((u32)a1 + cR * (u32)a2));
           }
         }
         cplen = nplen;
       }
-      P.ne += nR - cR;
-      cR = nR; cmax += run + ml;
+      cR = nR; cmax += run + ml; cmin += run + U.mnl;
     } else {
-      if (open) {  // close the group piece
-        if constexpr (BUILD) {
-          if (g0 + P.ng < FW_WG) {
-            FGroup G;
-            u32 mg, sh;
-            divmagic(cR, mg, sh);
-            G.magic = mg; G.shift = (uint8_t)sh; G.R = (uint8_t)cR; G.dsh = (uint8_t)(6 * (cpi % 10));
-            G.dhi = (uint8_t)(cpi >= 10); G.plen = cplen; G.pad1 = 0;
-            F->groups[g0 + P.ng] = G;
-          }
-        }
-        P.ng++; P.maxl += cmax;
-        open = false;
-      }
+      if (open) close_group();
       u32 off = prev, rem = run;
       while (rem + ml > FW_PLEN) {  // literal run that does not fit with the unit
         const u32 n = umin32(FW_PLEN, rem);
-        if constexpr (BUILD) {
-          if (e0 + P.ne < FW_WE) F->ent[e0 + P.ne] = wd.ld(off, n) | fw_meta(n, 1);
-        }
-        P.ne++; P.np++; P.lconst += n; P.maxl += n;
+        literal(off, n, false);
         off += n; rem -= n;
       }
-      open = true; cR = Ru; cmax = rem + ml; ceb = e0 + P.ne; cpi = P.np; cplen = 0;
+      open = true; cR = Ru; cmax = rem + ml; cmin = rem + U.mnl; cpi = P.np; cplen = 0;
+      P.np++;
       if constexpr (BUILD) {
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
         for (u32 a = 0; a < Ru; a++) {
           u32 cl = 0;
           const u64 cv = unit_choice(wd, U, T, a, cl);
           const u64 v = rb | (cv << (8 * rem));
-          if (ceb + a < FW_WE) F->ent[ceb + a] = (v & FW_M56) | fw_meta(rem + cl, Ru);
-          cplen |= (rem + cl) << (4 * a);
+          sk.gst(a, (v & FW_M56) | fw_meta(rem + cl, Ru));
+          cplen |= (rem + cl) << (3 * a);
         }
       }
-      P.ne += Ru; P.np++;
     }
     prev = U.e;
   }
@@ -376,56 +410,23 @@ A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, FWin* F, u32 g0, u32 e0)
       const u64 tb = (run ? wd.ld(prev, run) : 0ull) | (10ull << (8 * run));
       u32 nplen = 0;
       for (u32 a = 0; a < cR; a++) {
-        const u32 ia = ceb + a;
-        const u64 old = (ia < FW_WE) ? F->ent[ia] : 0ull;
+        const u64 old = sk.gld(a);
         const u32 ol = fw_len(old);
-        if (ia < FW_WE) F->ent[ia] = ((old | (tb << (8 * ol))) & FW_M56) | fw_meta(ol + tl, cR);
-        nplen |= (ol + tl) << (4 * a);
+        sk.gst(a, ((old | (tb << (8 * ol))) & FW_M56) | fw_meta(ol + tl, cR));
+        nplen |= (ol + tl) << (3 * a);
       }
       cplen = nplen;
     }
-    cmax += tl;
+    cmax += tl; cmin += tl;
+    close_group();
   } else {
-    if (open) {
-      if constexpr (BUILD) {
-        if (g0 + P.ng < FW_WG) {
-          FGroup G;
-          u32 mg, sh;
-          divmagic(cR, mg, sh);
-          G.magic = mg; G.shift = (uint8_t)sh; G.R = (uint8_t)cR; G.dsh = (uint8_t)(6 * (cpi % 10));
-          G.dhi = (uint8_t)(cpi >= 10); G.plen = cplen; G.pad1 = 0;
-          F->groups[g0 + P.ng] = G;
-        }
-      }
-      P.ng++; P.maxl += cmax;
-      open = false;
-    }
+    if (open) close_group();
     u32 off = prev, rem = tl;
     while (rem) {
       const u32 n = umin32(FW_PLEN, rem);
-      if constexpr (BUILD) {
-        const bool last = n == rem;
-        const u32 nb = last ? n - 1 : n;
-        u64 v = nb ? wd.ld(off, nb) : 0ull;
-        if (last) v |= 10ull << (8 * nb);
-        if (e0 + P.ne < FW_WE) F->ent[e0 + P.ne] = v | fw_meta(n, 1);
-      }
-      P.ne++; P.np++; P.lconst += n; P.maxl += n;
+      literal(off, n, n == rem);
       off += n; rem -= n;
     }
-  }
-  if (open) {
-    if constexpr (BUILD) {
-      if (g0 + P.ng < FW_WG) {
-        FGroup G;
-        u32 mg, sh;
-        divmagic(cR, mg, sh);
-        G.magic = mg; G.shift = (uint8_t)sh; G.R = (uint8_t)cR; G.dsh = (uint8_t)(6 * (cpi % 10));
-        G.dhi = (uint8_t)(cpi >= 10); G.plen = cplen; G.pad1 = 0;
-        F->groups[g0 + P.ng] = G;
-      }
-    }
-    P.ng++; P.maxl += cmax;
   }
   return P;
 }
@@ -437,13 +438,14 @@ struct WordClass {
   u64 count, bytes;
   u32 flags;       // A5X_WF_* (+ FAST fields) or A5X_WF_DEFER
   bool ovf;        // count/bytes overflow u64
+  bool clusters;   // the word has overlapping-key units (the slow path needs the DP)
 };
 
 // ringmax: the slow kernel's per-wave ring (a radix word's longest candidate must fit)
 template <class W>
 A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx, u32 ringmax) {
   WordClass C;
-  C.count = 0; C.bytes = 0; C.flags = 0; C.ovf = false;
+  C.count = 0; C.bytes = 0; C.flags = 0; C.ovf = false; C.clusters = false;
   if (mx < 1 || L == 0) {  // processWord emits nothing
     C.flags = A5X_WF_RADIX | A5X_WF_FAST;
     return C;
@@ -467,6 +469,7 @@ A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx,
     if (U.k || U.R != 2) bin = false;
     if (U.maxd > 0) maxl += (u32)U.maxd;
   }
+  C.clusters = clusters;
   if (ok && nunits == 0) {
     C.flags = A5X_WF_RADIX | A5X_WF_FAST;
     return C;
@@ -487,8 +490,12 @@ A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx,
     return C;
   }
   C.count = cnt; C.bytes = byt;
-  const Plan PL = plan_word<false>(wd, L, T, (FWin*)nullptr, 0, 0);
-  const bool fast = PL.ok && PL.np <= FW_PMAX && PL.ne <= 255 && PL.ng <= FW_WG && PL.maxl <= FW_RING / 2 - 16;
+  NullSink ns;
+  const Plan PL = plan_word<false>(wd, L, T, ns);
+  // minl >= 3: a candidate completes the dword that holds its first byte (see
+  // fw_pass2); maxl bounds the per-round ring use
+  const bool fast = PL.ok && PL.np <= FW_PMAX && PL.ne <= 255 && 1 + PL.ng + PL.ne <= FW_RMAX &&
+                    PL.maxl <= FW_MAXL && PL.minl >= 3 && P <= FW_PMAX_CNT;
   if (fast) {
     C.flags = (clusters ? 0u : (A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u))) | A5X_WF_FAST | (PL.ng << 10) |
               (PL.ne << 16) | (PL.np << 24);
@@ -500,23 +507,61 @@ A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx,
 }
 
 // ---------------------------------------------------------------------------
-// pass 1 of k_expand_fast for one candidate: group digits -> per-piece fields
-// (digit | (R-1) << 3) << 6 (i mod 10) in dlo (pieces 0-9) / dhi (10-19); literal
-// pieces keep field 0 (R = 1, entry 0).  n = candidate index in the word + 1.
-// Returns the candidate's length including '\n'.
+// k_expand_fast, per candidate (host replay in a5x_debug_plan_word)
 // ---------------------------------------------------------------------------
-A5X_HD u32 fw_pass1(const FGroup* gp, u32 ng, u32 lconst, u32 n, u64& dlo, u64& dhi) {
+// pass 1: group digits of n (= rank in the word + 1) -> per-piece fields
+// (digit | (R-1) << 3) << 6 piece; literal pieces keep field 0 (R = 1, entry 0).
+// Returns the candidate's length including '\n'.
+A5X_HD u32 fw_pass1(const u64* grp, u32 ng, u32 lconst, u32 n, u64& f) {
   u32 len = lconst;
-  dlo = 0; dhi = 0;
+  f = 0;
   for (u32 i = 0; i < ng; i++) {
-    const FGroup G = gp[i];
-    const u32 q = fastdiv_hd(n, G.magic, G.shift);
-    const u32 d = n - q * G.R;
+    const u64 G = grp[i];
+    const u32 R = frg_R(G);
+    const u32 q = (u32)(((u64)n * (u32)G) >> 32);
+    const u32 d = n - q * R;
     n = q;
-    const u64 f = (u64)(d | ((u32)(G.R - 1) << 3)) << G.dsh;
-    dlo |= G.dhi ? 0ull : f;
-    dhi |= G.dhi ? f : 0ull;
-    len += (G.plen >> (4 * d)) & 15u;
+    f |= (u64)(d | ((R - 1u) << 3)) << (6 * frg_piece(G));
+    len += frg_len(G, d);
   }
   return len;
+}
+
+// pass 2: the candidate's pieces appended to the output as whole, aligned dwords
+// of a ring (u32 index & mask), no atomics.  The candidate starts at byte o (ring
+// relative); acc holds the n = o & 3 bytes before it: the previous candidate's
+// tail for a round's first lane (the carry), zeros otherwise.  Dword ownership:
+// the dword holding byte o belongs to the PREVIOUS candidate unless acc is the
+// carry (has_prev = false): it is returned in *head (zeros below o) for the
+// previous lane to merge into its last partial dword, which it writes.  Requires
+// the candidate to complete that dword (len >= 3, FAST minl).  Returns the ring
+// dword index of the unfinished last dword; *acc_io / *n_io = its bytes / count.
+A5X_HD u32 fw_pass2(const u64* ent, u32 np, u64 f, u32 o, u32* ring, u32 mask, bool has_prev, u32* acc_io,
+                    u32* n_io, u32* head) {
+  u32 acc = *acc_io, n = o & 3u, D = o >> 2;
+  bool hp = has_prev && n != 0;
+  u32 hd = 0, row = 0;
+  for (u32 i = 0; i < np; i++) {
+    const u64 e = ent[row + ((u32)f & 7u)];
+    row += (((u32)f >> 3) & 7u) + 1u;
+    f >>= 6;
+    const u32 t = n + fw_len(e);
+    const u64 c = e & FW_M56;
+    const u32 sh = 8u * n;
+    const u64 lo = (u64)acc | (c << sh);
+    const u32 hi = (u32)((c >> 1) >> (63u - sh));  // bytes 8, 9 (c >> (64 - sh); 0 for sh = 0)
+    if (t >= 4u) {
+      if (hp) hd = (u32)lo;
+      else ring[D & mask] = (u32)lo;
+      hp = false;
+    }
+    if (t >= 8u) ring[(D + 1u) & mask] = (u32)(lo >> 32);
+    acc = t >= 8u ? hi : (t >= 4u ? (u32)(lo >> 32) : (u32)lo);
+    D += t >> 2;
+    n = t & 3u;
+  }
+  *acc_io = acc;
+  *n_io = n;
+  *head = hd;
+  return D;
 }

@@ -52,6 +52,10 @@ __global__ void __launch_bounds__(256) k_rate(int iters, u32* sink) {
     if (KIND == 3) atomicOr((u32*)(my + (o & 8191u & ~3u)), (u32)v);    // aligned ds_or_b32
     if (KIND == 4) acc += *(const u32*)(my + ((o * 5) & 8191u));        // unaligned ds_read_b32
     if (KIND == 5) { const uint4 q = *(const uint4*)(my + ((o * 3) & 8191u & ~15u)); acc += q.x ^ q.w; }  // b128 aligned
+    if (KIND == 6) atomicOr((unsigned long long*)(my + (o & 8191u & ~7u)), (unsigned long long)v);  // ds_or_b64
+    if (KIND == 7) my[o & 8191u] = (uint8_t)v;                                                       // ds_write_b8
+    if (KIND == 8) *(uint16_t*)(my + (o & 8191u)) = (uint16_t)v;                                     // b16 unaligned
+    if (KIND == 9) *(uint4*)(my + (o & 8191u & ~15u)) = make_uint4((u32)v, (u32)(v >> 32), 1u, 2u);  // b128 aligned
     o += len * 8;  // lanes ~ stride 16 B apart, moving on
     v = v * 0x9E3779B97F4A7C15ull + 1;
   }
@@ -90,9 +94,10 @@ int main() {
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
   const char* names[] = {"ds_write_b64 unaligned", "ds_write_b32 unaligned", "ds_write_b64 aligned  ",
-                         "ds_or_b32 aligned     ", "ds_read_b32 unaligned ", "ds_read_b128 aligned  "};
+                         "ds_or_b32 aligned     ", "ds_read_b32 unaligned ", "ds_read_b128 aligned  ",
+                         "ds_or_b64 aligned     ", "ds_write_b8           ", "ds_write_b16 unaligned", "ds_write_b128 aligned "};
   const int iters = 8192;
-  for (int kind = 0; kind < 6; kind++) {
+  for (int kind = 0; kind < 10; kind++) {
     for (int bpc : {2, 4}) {
       const int blocks = cus * bpc;
       auto launch = [&]() {
@@ -103,6 +108,10 @@ int main() {
           case 3: hipLaunchKernelGGL(k_rate<3>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
           case 4: hipLaunchKernelGGL(k_rate<4>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
           case 5: hipLaunchKernelGGL(k_rate<5>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
+          case 6: hipLaunchKernelGGL(k_rate<6>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
+          case 7: hipLaunchKernelGGL(k_rate<7>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
+          case 8: hipLaunchKernelGGL(k_rate<8>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
+          case 9: hipLaunchKernelGGL(k_rate<9>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
         }
       };
       launch();
