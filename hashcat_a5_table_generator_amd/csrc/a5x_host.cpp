@@ -95,8 +95,9 @@ struct a5x_ctx {
   size_t h_out_cap = 0;
 
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint64_t chunk = 4096;      // candidates per expand wave
+  uint64_t chunk = 32768;     // candidates per expand wave
   uint32_t waves_per_block = 4;
+  uint32_t ablate = 0;        // A5X_ABLATE (timing experiments only)
 };
 
 namespace {
@@ -404,7 +405,8 @@ A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   E.chunk_kind = c->chunk_kind.p; E.CH = c->chunk; E.mn = mn; E.mx = mx; E.err = c->d_scalars + 2;
   E.dbg = (uint64_t*)(c->d_scalars + 16);
   E.waves_per_block = c->waves_per_block;
-  E.rec = c->rec.p; E.roff = c->roff.p;
+  E.rec = c->rec.p; E.roff = c->roff.p; E.rec_n = c->rec.cap;
+  E.ablate = c->ablate;
   return E;
 }
 
@@ -450,6 +452,7 @@ int a5x_create(int device, a5x_ctx** out) {
     return A5X_E_HIP;
   }
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
+  if (const char* e = getenv("A5X_ABLATE")) c->ablate = (uint32_t)atoi(e);
   if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   *out = c;
   return A5X_OK;
@@ -789,48 +792,74 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   const WordClass C = classify_word(gw, (u32)len, T, mn, mx, A5X_RING_A - 16);
   info[0] = C.count; info[1] = C.bytes; info[2] = C.flags;
   if (!(C.flags & A5X_WF_FAST) || C.count == 0) return A5X_OK;
-  // the record exactly as k_keyspace_thread builds it
-  std::vector<u64> rec(FW_RMAX + 16, 0);
+  // the record exactly as k_keyspace_thread builds it, placed as a one-word window
+  std::vector<u64> wrec(FX_WREC + FW_PMAX + 16, 0);
   ArraySink sk;
-  sk.rec = rec.data(); sk.ng = ff_ng(C.flags);
+  sk.rec = wrec.data(); sk.np = ff_np(C.flags);
   const Plan P = plan_word<true>(gw, (u32)len, T, sk);
-  rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl);
+  wrec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl, P.nbig, P.bstarts);
+  wrec[FX_ZSLOT] = 0;
   if (!P.ok || P.ng != ff_ng(C.flags) || P.ne != ff_ne(C.flags) || P.np != ff_np(C.flags))
     return fail(c, A5X_E_BOUNDS, "piece plan disagrees with the keyspace fields");
-  // replay k_expand_fast: rounds of 64 lanes, passes 1-2 into a ring, head/carry
-  // hand-over exactly as the kernel does it (lanes run one after the other here)
+  // big pieces and their entries as the k_expand_fast window setup builds them
+  u32 Rb[FB_NMAX], base[FB_NMAX], E = 0;
+  std::vector<u32> be(4 * 256, 0);
+  for (u32 b = 0; b < FB_NMAX; b++) {
+    Rb[b] = fb_R(wrec.data(), 0, wrec[0], b);
+    base[b] = E;
+    if (b < P.nbig) E += Rb[b];
+  }
+  if (E != P.bent) return fail(c, A5X_E_BOUNDS, "big entries %u != plan %u", E, P.bent);
+  for (u32 b = 0; b < P.nbig; b++)
+    for (u32 cc = 0; cc < Rb[b]; cc++) fb_entry(wrec.data(), 0, b, cc, &be[4 * (base[b] + cc)]);
+  // replay the rounds: lanes one after the other, passes 1-2 into a linear ring
+  // with the head/carry hand-over and block moves exactly as the kernel does them
   if (C.bytes > cap) return fail(c, A5X_E_CAPACITY, "output buffer too small");
-  const u32 RING = 2048, mask = RING / 4 - 1;
-  std::vector<u32> ring(RING / 4, 0xA5A5A5A5u);
-  uint64_t pos = 0, flushed = 0;  // bytes written to out / complete in the ring
+  const u32 RING = 2048;
+  std::vector<u32> ring(RING / 4 + 4 * 64, 0xA5A5A5A5u);
+  uint64_t pos = 0, B = 0;  // bytes produced / global byte of ring byte 0
   u32 carry = 0;
   const u32 nl = std::min<u32>(64, (RING - 32) / std::max<u32>(P.maxl, 1));
+  auto flush = [&]() {
+    const u32 nb = (u32)((pos - B) >> 4);
+    if (!nb) return;
+    for (uint64_t X = B; X < B + 16ull * nb; X++) out[X] = (uint8_t)(ring[(X - B) >> 2] >> (8 * ((X - B) & 3)));
+    for (u32 k = 0; k < 4; k++) ring[k] = ring[4 * nb + k];
+    B += 16ull * nb;
+  };
   for (uint64_t rr = 0; rr < C.count; rr += nl) {
     const u32 nact = (u32)std::min<uint64_t>(nl, C.count - rr);
-    u32 len[64], o[64], acc[64], nn[64], head[64], dend[64];
-    u64 f[64];
-    u32 run = (u32)pos;
+    u32 len[64], o[64], acc[64], pn[64], hd[64], D[64];
+    u32 ent[64][FB_NMAX][4];
+    u32 run = (u32)(pos - B);
     for (u32 l = 0; l < nact; l++) {
-      len[l] = fw_pass1(rec.data() + 1, P.ng, P.lconst, (u32)(rr + l + 1), f[l]);
+      u32 n = (u32)(rr + l + 1);
+      len[l] = 0;
+      for (u32 b = 0; b < FB_NMAX; b++) {
+        const u32 q = Rb[b] > 1 ? (u32)(((u64)n * fr_magic(Rb[b])) >> 32) : n;
+        const u32 d = n - q * Rb[b];
+        n = q;
+        for (u32 k = 0; k < 4; k++) ent[l][b][k] = b < P.nbig ? be[4 * (base[b] + d) + k] : 0u;
+        len[l] += ent[l][b][3] >> 24;
+      }
       o[l] = run;
       run += len[l];
     }
     for (u32 l = 0; l < nact; l++) {
-      acc[l] = l == 0 ? carry : 0u;
-      dend[l] = fw_pass2(rec.data() + 1 + P.ng, P.np, f[l], o[l], ring.data(), mask, l != 0, &acc[l], &nn[l],
-                         &head[l]);
+      pn[l] = o[l] & 3u; D[l] = o[l] >> 2; acc[l] = 0; hd[l] = 0;
+      u32 pv = l == 0 ? (carry << ((32u - 8u * pn[l]) & 31u)) : 0u;
+      bool hp = l != 0 && pn[l] != 0;
+      for (u32 b = 0; b < FB_NMAX; b++) fb_put(ent[l][b], pv, pn[l], D[l], hp, hd[l], acc[l], ring.data(), RING / 4 + 4 * l);
     }
-    for (u32 l = 0; l + 1 < nact; l++)
-      if (nn[l]) ring[dend[l] & mask] = acc[l] | head[l + 1];
+    for (u32 l = 0; l < nact; l++)
+      ring[(l + 1 < nact && pn[l]) ? D[l] : RING / 4 + 4 * l] = acc[l] | (l + 1 < nact ? hd[l + 1] : 0u);
     carry = acc[nact - 1];
-    pos = run;
-    // flush complete 16-B blocks
-    const uint64_t full = pos & ~15ull;
-    for (uint64_t X = flushed; X < full; X++) out[X] = (uint8_t)(ring[(X >> 2) & mask] >> (8 * (X & 3)));
-    flushed = std::max(flushed, full);
+    pos = B + run;
+    flush();
   }
-  if (pos & 3) ring[(pos >> 2) & mask] = carry;
-  for (uint64_t X = flushed; X < pos; X++) out[X] = (uint8_t)(ring[(X >> 2) & mask] >> (8 * (X & 3)));
+  if (pos & 3) ring[(u32)(pos - B) >> 2] = carry;
+  flush();
+  for (uint64_t X = B; X < pos; X++) out[X] = (uint8_t)(ring[(X - B) >> 2] >> (8 * ((X - B) & 3)));
   if (pos != C.bytes) return fail(c, A5X_E_BOUNDS, "replayed %llu bytes, keyspace says %llu",
                                   (unsigned long long)pos, (unsigned long long)C.bytes);
   info[3] = pos;

@@ -165,21 +165,56 @@ struct KsArgs {
 struct DevRecSink {
   u64* g;       // LDS: g[a * 256]
   u64* rec;     // global record base
-  u32 ng;
+  u32 np;
   __device__ u64 gld(u32 a) const { return g[a * 256u]; }
   __device__ void gst(u32 a, u64 v) { g[a * 256u] = v; }
-  __device__ void ent(u32 i, u64 v) { rec[1 + ng + i] = v; }
-  __device__ void grp(u32 i, u64 v) { rec[1 + i] = v; }
+  __device__ void ent(u32 i, u64 v) { rec[1 + np + i] = v; }
+  __device__ void desc(u32 i, u64 v) { rec[1 + i] = v; }
 };
+
+// A word's bytes staged in LDS (the keyspace tile); 8 readable bytes past any word.
+struct LWord {
+  const uint8_t* base;
+  u32 off;
+  __device__ __forceinline__ u32 at(u32 i) const { return base[off + i]; }
+  __device__ __forceinline__ u64 ld(u32 i, u32 n) const {
+    const u64 v = (u64)lds_ld4(base, off + i) | ((u64)lds_ld4(base, off + i + 4) << 32);
+    return keep_bytes64(v, n);
+  }
+};
+
+#define KS_WB 8192  // tile word bytes staged in LDS (larger tiles read global memory)
+
+template <class W>
+__device__ __forceinline__ u32 ks_classify(const W& wd, u64 L64, const Tab& T, const KsArgs& a, WordClass& C) {
+  if (L64 > A5X_LMAX_A && a.mx >= 1) return A5X_WF_DEFER;  // long words: the wave kernel
+  C = classify_word(wd, (u32)L64, T, a.mn, a.mx, A5X_RING_A - 16);
+  u32 f = C.flags;
+  if (C.ovf) atomicOr(a.err, A5X_DERR_OVF);
+  if ((f & A5X_WF_DEFER) || !(f & (A5X_WF_FAST | A5X_WF_RADIX | A5X_WF_ERR_OVF)))
+    f = A5X_WF_DEFER;  // capped windows, unit limits, non-FAST clusters: the DP kernel
+  return f;
+}
+
+template <class W>
+__device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const KsArgs& a, u32 f, u64* rec, u64* g) {
+  DevRecSink sk;
+  sk.g = g; sk.rec = rec; sk.np = ff_np(f);
+  const Plan P = plan_word<true>(wd, L, T, sk);
+  rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl, P.nbig, P.bstarts);
+  if (!P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
+}
 
 // One lane per word, one 256-word tile per workgroup iteration: classification,
 // closed-form (count, bytes), and for FAST words the plan record, packed densely
 // in word order inside the tile's record region (workgroup scan of the sizes).
+// The tile's word bytes are staged in LDS with 16-B loads when they fit KS_WB.
 __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 tb = (a.table_bytes + 15u) & ~15u;
-  u64* gbuf = (u64*)(smem + tb);                      // 256 x FW_UMAXR open-group entries
-  u32* wsum = (u32*)(smem + tb + 256 * FW_UMAXR * 8);  // per-wave sums of the scan
+  u64* gbuf = (u64*)(smem + tb);                        // 256 x FW_UMAXR open-group entries
+  u32* wsum = (u32*)(smem + tb + 256 * FW_UMAXR * 8);   // per-wave sums of the scan
+  uint8_t* wb = smem + tb + 256 * FW_UMAXR * 8 + 64;    // KS_WB + 32 tile bytes
   load_table(smem, a.table, a.table_bytes);
   __syncthreads();
   const Tab T = tab_view(smem);
@@ -188,25 +223,37 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const u64 w = tile * FW_TILE + tid;
     const bool valid = w < a.nw;
+    const u64 t0 = tile * FW_TILE, t1 = min(a.nw, t0 + FW_TILE);
+    const u64 A0 = a.woff[t0] & ~15ull, A1 = a.woff[t1];
+    const bool staged = A1 - A0 <= KS_WB;
+    if (staged) {
+      const uint4* src = (const uint4*)(a.words + A0);
+      const u32 nq = (u32)((A1 - A0 + 15) / 16);
+      for (u32 i = tid; i < nq + 2; i += 256) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (A0 + 16ull * (i + 1) <= A1) {
+          v = src[i];
+        } else if (i < nq) {  // the tile's last partial quad: never read past the batch
+          u32 x[4] = {0, 0, 0, 0};
+          for (u32 b = 0; A0 + 16ull * i + b < A1; b++) x[b >> 2] |= (u32)a.words[A0 + 16ull * i + b] << (8 * (b & 3));
+          v = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+        ((uint4*)wb)[i] = v;
+      }
+    }
+    __syncthreads();
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
     u32 f = 0;
+    u64 s = 0, L64 = 0;
+    LWord lw;
     GWord gw;
-    u32 L = 0;
     if (valid) {
-      const u64 s = a.woff[w], e = a.woff[w + 1];
-      const u64 L64 = e - s;
+      s = a.woff[w];
+      L64 = a.woff[w + 1] - s;
+      lw.base = wb; lw.off = (u32)(s - A0);
       gw.p = a.words + s;
-      L = (u32)min(L64, (u64)0xffffffffu);
-      if (L64 > A5X_LMAX_A && a.mx >= 1) {  // long words: the wave kernel (loops over positions)
-        f = A5X_WF_DEFER;
-      } else {
-        C = classify_word(gw, L, T, a.mn, a.mx, A5X_RING_A - 16);
-        f = C.flags;
-        if (C.ovf) atomicOr(a.err, A5X_DERR_OVF);
-        if ((f & A5X_WF_DEFER) || !(f & (A5X_WF_FAST | A5X_WF_RADIX | A5X_WF_ERR_OVF)))
-          f = A5X_WF_DEFER;  // capped windows, unit limits, non-FAST clusters: the DP kernel
-      }
+      f = staged ? ks_classify(lw, L64, T, a, C) : ks_classify(gw, L64, T, a, C);
     }
     // record sizes -> exclusive workgroup scan
     const bool fast = valid && (f & A5X_WF_FAST) && C.count > 0;
@@ -216,16 +263,12 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     __syncthreads();
     u32 base = 0;
     for (u32 k = 0; k < wv; k++) base += wsum[k];
-    __syncthreads();
     const u32 ro = base + inc - rs;
     bool built = false;
     if (fast && ro + rs <= FW_TILE_REC) {
       u64* rec = a.rec + tile * FW_TILE_REC + ro;
-      DevRecSink sk;
-      sk.g = gbuf + tid; sk.rec = rec; sk.ng = ff_ng(f);
-      const Plan P = plan_word<true>(gw, L, T, sk);
-      rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl);
-      if (!P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
+      if (staged) ks_build(lw, (u32)L64, T, a, f, rec, gbuf + tid);
+      else ks_build(gw, (u32)L64, T, a, f, rec, gbuf + tid);
       a.roff[w] = (u32)(tile * FW_TILE_REC + ro);
       built = true;
     }
@@ -243,6 +286,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       a.bytes[w] = (f & A5X_WF_DEFER) ? 0 : C.bytes;
       a.flags[w] = f;
     }
+    __syncthreads();  // wb / wsum are rewritten by the next tile
   }
 }
 
@@ -642,6 +686,9 @@ struct ExpArgs {
   u64* dbg;              // 8-word debug record of the first tripped guard
   const u64* rec;        // FAST plan records (k_keyspace_thread)
   const u32* roff;       // per word: record offset into rec
+  u64 rec_n;             // u64 in rec
+  u32 ablate;            // timing experiments only (A5X_ABLATE): 2 no ring
+                         // writes, 4 no global stores; output is garbage when set
 };
 
 // Record the first tripped guard (code + context) and flag the call as failed.
@@ -960,74 +1007,180 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 //           instruction, consecutive lanes consecutive addresses).
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
-#define FX_RING 2048  // per-wave output ring (bytes)
-#define FX_WREC 256   // window record budget (u64)
+#define FX_RING 2048  // per-wave linear output staging (bytes), then 4 trash dwords per lane
 #define FX_WW 32      // window words
+#define FX_NBE 256    // big entries per window (16 B each); [FX_ZBE] is the empty piece
+#define FX_ZBE (FX_NBE - 1)
 
 struct FXWin {
-  u64 rec[FX_WREC];   // the window's records
-  u64 wc0[FX_WW];     // first global candidate of word j
-  u32 winfo[FX_WW];   // record base (u64 index) | ng << 9 | np << 13 | lconst << 17
+  u64 rec[FX_WREC];        // the window's small-piece records; rec[FX_ZSLOT] = 0
+  uint4 be[FX_NBE];        // big entries: 15 content bytes, length in byte 15
+  // per word j, big piece b: {magic, (R - 1) | base << 8 | x << 16} at wi[j][b / 2].{xy|zw};
+  // x of piece 0 = bits 0-15 of the word's first candidate c0, x of piece 1 = c0
+  // bits 16-23 | big piece count << 8 (ranks are taken mod 2^24: FW_PMAX_CNT)
+  uint4 wi[FX_WW][2];
 };
-static_assert(FW_RMAX <= FX_WREC, "a FAST record must fit a window");
+static_assert(FW_RMAX < FX_ZSLOT && FB_EMAX < FX_ZBE, "a FAST record must fit a window");
 
 // Closed-form bytes of candidates [0, r) of a FAST word (candidate r <-> index r + 1
-// in the group mixed radix, group 0 least significant).  rec = the word's record
-// (LDS).  Wave-collective: lanes over the word's groups (ng <= FW_PMAX).
+// in the piece mixed radix, piece 0 least significant).  rec = the word's record
+// (LDS).  Wave-collective: lanes over the word's pieces (np <= FW_PMAX).
 __device__ u64 fast_prefix_bytes(const u64* rec, u64 r) {
   const u32 lane = lane_id();
-  const u64 hdr = rec[0];
-  const u32 ng = frh_ng(hdr);
+  const u32 np = frh_np(rec[0]);
   const u64 Y = r + 1;
   u64 Rl = 1, G = 0;
-  if (lane < ng) { G = rec[1 + lane]; Rl = frg_R(G); }
-  u64 inc = Rl;  // inclusive prefix product of R over groups
+  if (lane < np) { G = rec[1 + lane]; Rl = frd_R(G); }
+  u64 inc = Rl;  // inclusive prefix product of R over pieces
 #pragma unroll
   for (int d = 1; d < 16; d <<= 1) {
     const u64 y = shfl_up_u64(inc, d);
     if ((int)lane >= d) inc *= y;
   }
   i64 part = 0, base0 = 0;
-  if (lane < ng) {
+  if (lane < np) {
+    const u64* ent = rec + 1 + np + frd_ebase(G);
     const u64 Q = inc / Rl, full = Y / inc, rem = Y % inc;
-    const int l0 = (int)frg_len(G, 0);
+    const int l0 = (int)fw_len(ent[0]);
     base0 = l0;
     for (u32 v = 1; v < (u32)Rl; v++) {
       const u64 lo = (u64)v * Q;
       const u64 cnt = full * Q + (rem > lo ? min(Q, rem - lo) : 0);
-      part += ((i64)frg_len(G, v) - l0) * (i64)cnt;
+      part += ((i64)fw_len(ent[v]) - l0) * (i64)cnt;
     }
   }
-  // every candidate = lconst + digit-0 group lengths + deltas
-  const i64 lbase = wave_sum_i64(base0) + frh_lconst(hdr);
-  return (u64)((i64)r * lbase + wave_sum_i64(part));
+  // every candidate = the digit-0 piece lengths + deltas
+  return (u64)((i64)r * wave_sum_i64(base0) + wave_sum_i64(part));
 }
 
-// stream complete blocks [R.flushed, upto) (upto 16-aligned) of the ring
-__device__ __forceinline__ void fx_flush(Run& R, const u32* ring, const ExpArgs& a, u64 upto, u64 hi) {
+// Staging state of one wave (uniform): ring byte 0 <-> global byte B (16-aligned,
+// relative to out_base); bytes [lo, pos) belong to this wave's current run.
+struct FxRun {
+  u64 B, lo, pos;
+  u32 carry;  // bytes [pos & ~3, pos) of the unfinished dword (not yet in the ring)
+  bool open;
+};
+
+// Stream the complete 16-B blocks of [B, pos) and move the partial last block to
+// ring block 0.  The first block of a run may start before lo: byte-exact.
+__device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) {
   const u32 lane = lane_id();
-  const u32 nb = (u32)((upto - R.flushed) / 16);
-  for (u32 b = lane; b < nb; b += 64) {
-    const u64 X = R.flushed + (u64)b * 16;
-    const uint4 v = ((const uint4*)ring)[((u32)(X - R.base) / 16u) & (FX_RING / 16 - 1)];
-    store_block(a, X, v, R.lo, hi);
+  const u32 nb = uniform((u32)((R.pos - R.B) >> 4));
+  if (nb == 0) return;
+  const u64 B = uniform64(R.B);
+  if (B + 16ull * nb > a.out_cap) { guard_trip(a, 1, B, R.lo, R.pos, a.out_cap); R.B = B + 16ull * nb; return; }
+  const uint4* r4 = (const uint4*)ring;
+  if (a.ablate & 4u) {
+  } else if (B >= R.lo) {
+    for (u32 b = lane; b < nb; b += 64) *(uint4*)(a.out + B + 16ull * b) = r4[b];
+  } else {
+    for (u32 b = lane; b < nb; b += 64) store_block(a, B + 16ull * b, r4[b], R.lo, R.pos);
   }
-  R.flushed = upto;
+  if (lane == 0) {
+    const uint4 t = r4[nb];
+    ((uint4*)ring)[0] = t;
+  }
+  R.B = B + 16ull * nb;
+  WAVE_SYNC();
 }
 
-// write the carried partial dword, flush everything up to R.pos (tail block byte-exact)
-__device__ __forceinline__ void fx_close(Run& R, u32* ring, const ExpArgs& a, u32 carry) {
+// write the carried partial dword, flush everything up to pos (tail block byte-exact)
+__device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) {
   if (!R.open) return;
   if (R.pos & 3u) {
-    if (lane_id() == 0) ring[((u32)(R.pos - R.base) >> 2) & (FX_RING / 4 - 1)] = carry;
+    if (lane_id() == 0) ring[(u32)(R.pos - R.B) >> 2] = R.carry;
     WAVE_SYNC();
   }
-  const u64 full = R.pos & ~15ull;
-  if (full > R.flushed) fx_flush(R, ring, a, full, R.pos);
-  if (R.pos > R.flushed) fx_flush(R, ring, a, R.flushed + 16, R.pos);
+  fx_flush(R, ring, a);
+  if (R.pos > R.B && lane_id() == 0) store_block(a, R.B, ((const uint4*)ring)[0], max(R.lo, R.B), R.pos);
   WAVE_SYNC();
   R.open = false;
 }
+
+// Rounds of <= nl consecutive candidates [g, gend) of the window's k words; NB >=
+// every word's big piece count.
+template <int NB>
+__device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, const ExpArgs& a, FxRun& R, u64 g, u64 gend, u32 k,
+                                          u32 nl, u32 c0rel) {
+  const u32 lane = lane_id();
+  const u32 T = FX_RING / 4 + 4u * lane;  // the lane's 4 trash dwords
+  u32 jcur = 0;  // word holding the round's first candidate (uniform)
+  for (u64 rr = g; rr < gend; rr += nl) {
+    const u32 rrel = (u32)(rr - g);
+    const u32 nact = uniform((u32)min((u64)nl, gend - rr));
+    // word of each lane's candidate: count the word starts it has passed
+    u32 lo = jcur;
+    for (;;) {
+      const u32 jn = uniform(jcur + 1);
+      if (jn >= k) break;
+      const u32 sj = uniform(readlane_u32(c0rel, jn));
+      if (sj >= rrel + nact) break;
+      jcur = jn;
+      lo += (rrel + lane >= sj) ? 1u : 0u;
+    }
+    const uint4 b01 = F.wi[lo][0];
+    const uint4 b23 = NB > 2 ? F.wi[lo][1] : make_uint4(0, 0, 0, 0);
+    const u32 wc = (b01.y >> 16) | (((b01.w >> 16) & 255u) << 16);
+    const u32 nb = lane < nact ? (b01.w >> 24) & 7u : 0u;
+    // pass 1: big piece digits of n = rank + 1 -> entries, length
+    u32 n = (((u32)rr + lane - wc) & 0xFFFFFFu) + 1u;
+    uint4 e[NB];
+    u32 len = 0;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const u32 magic = b == 0 ? b01.x : b == 1 ? b01.z : b == 2 ? b23.x : b23.z;
+      const u32 rb = b == 0 ? b01.y : b == 1 ? b01.w : b == 2 ? b23.y : b23.w;
+      const u32 rm1 = rb & 63u;
+      const u32 q = rm1 ? __umulhi(n, magic) : n;  // R = 1: digit 0
+      const u32 d = n - __umul24(q, rm1 + 1u);
+      n = q;
+      const u32 idx = (u32)b < nb ? ((rb >> 8) & 255u) + d : (u32)FX_ZBE;
+      e[b] = F.be[idx];
+      len += e[b].w >> 24;
+    }
+    const u32 incl = wave_incl_scan_u32(len);
+    const u32 tot = lane63(incl);
+    const u32 o = (u32)(R.pos - R.B) + incl - len;
+    // pass 2: append the pieces as whole aligned dwords (see fb_put)
+    u32 pn = o & 3u, D = o >> 2, acc = 0, hd = 0;
+    u32 pv = lane == 0 ? (R.carry << ((32u - 8u * pn) & 31u)) : 0u;
+    bool hp = lane != 0 && pn != 0;
+    if (!(a.ablate & 2u)) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        const u32 ev[4] = {e[b].x, e[b].y, e[b].z, e[b].w};
+        fb_put(ev, pv, pn, D, hp, hd, acc, ring, T);
+      }
+    }
+    const u32 hnext = (u32)__shfl_down((int)hd, 1);
+    ring[(lane + 1 < nact && pn) ? D : T] = acc | hnext;
+    R.carry = readlane_u32(acc, nact - 1);
+    R.pos = uniform64(R.pos + tot);
+    WAVE_SYNC();
+    fx_flush(R, ring, a);
+  }
+}
+
+// Window metadata of words w .. w + FX_WW - 1 (lane j <-> word w + j, same keyspace
+// tile), all loads issued together; the next window's is prefetched during rounds.
+struct FxMeta {
+  u64 c0, c1, bo;
+  u32 fl, roff;
+};
+__device__ __forceinline__ FxMeta fx_meta(const ExpArgs& a, u64 w) {
+  const u32 lane = lane_id();
+  const u64 wl = w + lane;
+  const bool inb = lane < FX_WW && wl < a.nw && wl / FW_TILE == w / FW_TILE;
+  FxMeta m;
+  m.c0 = inb ? a.cand_off[wl] : ~0ull;
+  m.c1 = inb ? a.cand_off[wl + 1] : ~0ull;
+  m.fl = inb ? a.flags[wl] : 0u;
+  m.roff = inb ? a.roff[wl] : 0u;
+  m.bo = (lane == 0 && w < a.nw) ? a.byte_off[w] : 0;
+  return m;
+}
+
+#define FX_PF 256  // prefetched record u64 (2 x 16 B per lane)
 
 __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
@@ -1038,140 +1191,180 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
   if (w >= a.nw) { guard_trip(a, 2, chunk, w, g0, a.nw); return; }
   while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
   if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
+  if (lane == 0) { F.rec[FX_ZSLOT] = 0; F.be[FX_ZBE] = make_uint4(0, 0, 0, 0); }
   u64 g = g0;
-  Run R;
-  R.open = false;
-  u32 carry = 0;
+  FxRun R;
+  R.open = false; R.B = 0; R.lo = 0; R.pos = 0; R.carry = 0;
+  FxMeta M = fx_meta(a, w);
+  u64 pfb = ~0ull;  // records [pfb, pfb + FX_PF) prefetched into pf0 / pf1 (pfb even)
+  uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;
   STAMP_DECL
   while (g < g1) {
     if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
-    // ---- window: lane j <-> word w + j (same keyspace tile) ----
-    const u64 wl = w + lane;
-    const bool inb = lane < FX_WW && wl < a.nw && wl / FW_TILE == w / FW_TILE;
-    const u64 c0 = inb ? a.cand_off[wl] : ~0ull;
-    const u64 c1 = inb ? a.cand_off[wl + 1] : ~0ull;
-    const u32 fl = inb ? a.flags[wl] : 0u;
-    const bool hasc = inb && c1 > c0;
-    const bool fast = inb && (fl & A5X_WF_FAST) && c0 < g1;
+    // ---- window: lane j <-> word w + j ----
+    const u64 c0 = M.c0, c1 = M.c1;
+    const u32 fl = M.fl;
+    const bool hasc = c1 > c0 && c0 != ~0ull;
+    const bool fast = (fl & A5X_WF_FAST) && c0 < g1;
     const u32 rs = (fast && hasc) ? ff_rsize(fl) : 0u;
     const u32 incR = wave_incl_scan_u32(rs);
-    const bool ok = fast && incR <= FX_WREC;
+    const bool ok = fast && incR < FX_ZSLOT;
     const u64 badm = __ballot(!ok);
-    const u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
+    u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
     STAMP(0);
     if (k == 0) {
       // word w is a hole here (slow / BIG) or empty
       const u64 w0c1 = uniform64(c1);
-      if (w0c1 > g) {
-        fx_close(R, ring, a, carry);
+      if (w0c1 > g && w0c1 != ~0ull) {
+        fx_close(R, ring, a);
         g = min(w0c1, g1);
       }
       w++;
+      M = fx_meta(a, w);
       continue;
     }
-    // ---- records -> LDS (one contiguous range), word info ----
+    // ---- small records -> LDS (one contiguous range; prefetched when it continues the last) ----
     const u64 fm = __ballot(lane < k && rs > 0);
     if (fm == 0) {  // only words without candidates: skip them
       w += k;
+      M = fx_meta(a, w);
       continue;
     }
     const u32 jf = (u32)__builtin_ctzll(fm);
-    const u32 roff = (lane < k && rs > 0) ? a.roff[wl] : 0u;
-    const u64 src0 = (u64)readlane_u32(roff, jf);
+    const u64 src0 = (u64)readlane_u32(M.roff, jf);
     const u32 ntot = readlane_u32(incR, k - 1);
-    {
-      const uint4* src = (const uint4*)(a.rec + src0);  // records are 8-B aligned: copy u64 pairs
+    if (pfb <= src0 && src0 + ntot <= pfb + FX_PF) {
+      const u32 d = (u32)(src0 - pfb);  // 0 .. : the prefetched u64 i lands at F.rec[i - d]
+      const u32 i0 = 2 * lane, i1 = 2 * (lane + 64);
+      if (i0 >= d) F.rec[i0 - d] = ((u64)pf0.y << 32) | pf0.x;
+      if (i0 + 1 >= d) F.rec[i0 + 1 - d] = ((u64)pf0.w << 32) | pf0.z;
+      if (i1 - d < FX_ZSLOT) F.rec[i1 - d] = ((u64)pf1.y << 32) | pf1.x;
+      if (i1 + 1 - d < FX_ZSLOT) F.rec[i1 + 1 - d] = ((u64)pf1.w << 32) | pf1.z;
+    } else {
       const u64* s64 = a.rec + src0;
       if ((src0 & 1) == 0) {
+        const uint4* src = (const uint4*)s64;
         for (u32 i = lane; i < (ntot + 1) / 2; i += 64) ((uint4*)F.rec)[i] = src[i];
       } else {
         for (u32 i = lane; i < ntot; i += 64) F.rec[i] = s64[i];
       }
     }
     const u32 rb = incR - rs;
-    const u64 bo = (lane == 0) ? a.byte_off[w] : 0;
+    const u64 bo = M.bo;
     WAVE_SYNC();
-    u32 maxl = 0;
-    if (lane < k) {
-      F.wc0[lane] = c0;
-      u32 info = 0;
-      if (rs) {
-        const u64 hdr = F.rec[rb];
-        maxl = frh_maxl(hdr);
-        info = rb | (frh_ng(hdr) << 9) | (frh_np(hdr) << 13) | (frh_lconst(hdr) << 17);
-      }
-      F.winfo[lane] = info;
+    // ---- big pieces per word: R = product of the spanned small R ----
+    u64 hdr = 0;
+    u32 nbw = 0, R0 = 1, R1 = 1, R2 = 1, R3 = 1;
+    if (lane < k && rs) {
+      hdr = F.rec[rb];
+      nbw = frh_nbig(hdr);
+      R0 = fb_R(F.rec, rb, hdr, 0);
+      R1 = fb_R(F.rec, rb, hdr, 1);
+      R2 = fb_R(F.rec, rb, hdr, 2);
+      R3 = fb_R(F.rec, rb, hdr, 3);
     }
+    const u32 E = R0 + R1 + R2 + R3 - (FB_NMAX - nbw);  // fb_R = 1 past the last big piece
+    const u32 incE = wave_incl_scan_u32(E);
+    const u64 over = __ballot(lane < k && incE > FX_ZBE);
+    if (over) k = (u32)__builtin_ctzll(over);  // the window ends where the big entries do not fit
+    if (k == 0) { guard_trip(a, 6, chunk, w, E, incE); break; }
+    // ---- prefetch the next window: metadata, and records if they continue this window's ----
+    const FxMeta Mn = fx_meta(a, w + k);
+    {
+      const u64 nx = src0 + readlane_u32(incR, k - 1);
+      pfb = nx & ~1ull;
+      if (pfb + FX_PF <= a.rec_n) {
+        const uint4* src = (const uint4*)(a.rec + pfb);
+        pf0 = src[lane];
+        pf1 = src[lane + 64];
+      } else {
+        pfb = ~0ull;
+      }
+    }
+    const u32 maxl = lane < k ? frh_maxl(hdr) : 0u;
     const u32 winmax = wave_max_u32(maxl);
+    const u32 nbmax = wave_max_u32(lane < k ? nbw : 0u);
+    const u32 ebase = incE - E;
+    if (lane < k) {
+      const u32 b1 = ebase + R0, b2 = b1 + R1, b3 = b2 + R2;
+      const u32 c0lo = (u32)c0 & 0xFFFFFFu;
+      F.wi[lane][0] = make_uint4(fr_magic(R0), (R0 - 1u) | (ebase << 8) | ((c0lo & 0xFFFFu) << 16), fr_magic(R1),
+                                 (R1 - 1u) | (b1 << 8) | ((c0lo >> 16) << 16) | (nbw << 24));
+      F.wi[lane][1] = make_uint4(fr_magic(R2), (R2 - 1u) | (b2 << 8), fr_magic(R3), (R3 - 1u) | (b3 << 8));
+    }
+    WAVE_SYNC();
+    // ---- build the big entries: lanes over the window's entries ----
+    {
+      const u32 etot = readlane_u32(incE, k - 1);
+      const u32 est = lane < k ? ebase : 0xffffffffu;
+      u32 jb = 0;  // word of the pass's first entry (uniform)
+      for (u32 t0 = 0; t0 < etot; t0 += 64) {
+        const u32 t = t0 + lane;
+        u32 j = jb;
+        for (;;) {
+          const u32 jn = uniform(jb + 1);
+          if (jn >= k) break;
+          const u32 sj = uniform(readlane_u32(est, jn));
+          if (sj >= t0 + 64) break;
+          jb = jn;
+          j += (t >= sj) ? 1u : 0u;
+        }
+        // (cross-lane reads with every lane active: a bpermute from an inactive lane is garbage)
+        const u32 wrb = (u32)__shfl((int)rb, (int)j);
+        const u32 u = t - (u32)__shfl((int)ebase, (int)j);
+        const u32 nbj = (u32)__shfl((int)nbw, (int)j);
+        if (t < etot) {
+          // big piece b of word j holding entry u, and the combination c
+          const uint4 q01 = F.wi[j][0], q23 = F.wi[j][1];
+          const u32 b0 = (q01.y >> 8) & 255u;
+          const u32 s1 = ((q01.w >> 8) & 255u) - b0, s2 = ((q23.y >> 8) & 255u) - b0, s3 = ((q23.w >> 8) & 255u) - b0;
+          u32 b = 0, cb = 0;
+          if (nbj > 1 && u >= s1) { b = 1; cb = s1; }
+          if (nbj > 2 && u >= s2) { b = 2; cb = s2; }
+          if (nbj > 3 && u >= s3) { b = 3; cb = s3; }
+          u32 ent[4];
+          fb_entry(F.rec, wrb, b, u - cb, ent);
+          F.be[t] = make_uint4(ent[0], ent[1], ent[2], ent[3]);
+        }
+      }
+    }
     WAVE_SYNC();
     STAMP(1);
     // ---- run position of g ----
     const u64 wc0 = uniform64(c0);
     const u64 r0 = g - wc0;
     u64 pos = uniform64(bo) - a.out_base;
-    if (r0) pos += fast_prefix_bytes(F.rec + (F.winfo[0] & 511u), r0);
+    if (r0) pos += fast_prefix_bytes(F.rec + readlane_u32(rb, 0), r0);
     if (!R.open || R.pos != pos) {
-      fx_close(R, ring, a, carry);
-      run_open<FX_RING>(R, pos);
-      carry = 0;
+      fx_close(R, ring, a);
+      R.B = pos & ~15ull; R.lo = pos; R.pos = pos; R.carry = 0; R.open = true;
     }
     STAMP(2);
     // ---- rounds ----
     const u64 gend = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     const u32 nl = uniform(min(64u, (FX_RING - 32) / max(winmax, 1u)));
     const u32 c0rel = (lane < k) ? (u32)(c0 > g ? c0 - g : 0) : 0xffffffffu;
-    u32 jcur = 0;  // word holding the round's first candidate (uniform)
-    for (u64 rr = g; rr < gend; rr += nl) {
-      const u32 rrel = (u32)(rr - g);
-      const u32 nact = (u32)min((u64)nl, gend - rr);
-      const bool act = lane < nact;
-      // word of each lane's candidate: walk the (uniform) words starting in this round
-      u32 lo = jcur;
-      for (u32 j = jcur + 1; j < k; j++) {
-        const u32 sj = readlane_u32(c0rel, j);
-        if (sj >= rrel + nact) break;
-        if (rrel + lane >= sj) lo = j;
-        jcur = j;
-      }
-      const u32 info = F.winfo[lo];
-      const u64 wc = F.wc0[lo];
-      const u32 wrb = info & 511u, ng = (info >> 9) & 15u, np = (info >> 13) & 15u, lconst = info >> 17;
-      u64 f = 0;
-      u32 len = 0;
-      if (act) len = fw_pass1(F.rec + wrb + 1, ng, lconst, (u32)(rr + lane - wc + 1), f);
-      STAMP(3);
-      const u32 incl = wave_incl_scan_u32(len);
-      const u32 tot = lane63(incl);
-      const u32 o = (u32)(R.pos - R.base) + incl - len;
-      u32 acc = (lane == 0) ? carry : 0u, n = 0, head = 0, Dend = 0;
-      if (act) Dend = fw_pass2(F.rec + wrb + 1 + ng, np, f, o, ring, FX_RING / 4 - 1, lane != 0, &acc, &n, &head);
-      const u32 hnext = (u32)__shfl_down((int)head, 1);
-      if (act && lane + 1 < nact && n) ring[Dend & (FX_RING / 4 - 1)] = acc | hnext;
-      carry = readlane_u32(acc, nact - 1);
-      R.pos += tot;
-      STAMP(4);
-      WAVE_SYNC();
-      const u64 full = R.pos & ~15ull;
-      if (full > R.flushed) fx_flush(R, ring, a, full, R.pos);
-      STAMP(5);
-    }
+    if (nbmax <= 2) fx_rounds<2>(F, ring, a, R, g, gend, k, nl, c0rel);
+    else fx_rounds<FB_NMAX>(F, ring, a, R, g, gend, k, nl, c0rel);
+    STAMP(3);
     g = gend;
     w += k;
+    M = Mn;
     WAVE_SYNC();
   }
-  fx_close(R, ring, a, carry);
+  fx_close(R, ring, a);
   STAMP(6);
   STAMP_FLUSH();
 }
 
-__device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + (u32)sizeof(FXWin) + 15u) & ~15u; }
+__device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + 1024 + (u32)sizeof(FXWin) + 15u) & ~15u; }
 
 __global__ void __launch_bounds__(256) k_expand_fast(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   uint8_t* mine = smem + wv * lds_per_wave_fast();
   u32* ring = (u32*)mine;
-  FXWin& F = *(FXWin*)(mine + FX_RING);
+  FXWin& F = *(FXWin*)(mine + FX_RING + 1024);
   const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
   if (chunk * a.CH >= a.cand_end) return;
   expand_chunk_fast(F, ring, a, chunk);
@@ -1339,7 +1532,7 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
 }
 
 size_t a5x_keyspace_thread_lds(u32 table_bytes) {
-  return ((table_bytes + 15u) & ~15u) + FW_TILE * FW_UMAXR * 8 + 64;
+  return ((table_bytes + 15u) & ~15u) + FW_TILE * FW_UMAXR * 8 + 64 + KS_WB + 32;
 }
 
 size_t a5x_keyspace_wave_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + sizeof(LdsB); }
@@ -1385,7 +1578,7 @@ static ExpArgs exp_args(const A5xExpLaunch& L) {
   a.cand_off = L.cand_off; a.byte_off = L.byte_off; a.flags = L.flags; a.chunk_w0 = L.chunk_w0;
   a.chunk_kind = L.chunk_kind; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.out = L.out;
   a.out_base = L.out_base; a.out_cap = L.out_cap; a.mn = L.mn; a.mx = L.mx; a.err = L.err; a.dbg = L.dbg;
-  a.rec = L.rec; a.roff = L.roff;
+  a.rec = L.rec; a.roff = L.roff; a.ablate = L.ablate; a.rec_n = L.rec_n;
   return a;
 }
 
@@ -1393,7 +1586,7 @@ size_t a5x_expand_lds(u32 table_bytes, int kind, u32 waves) {
   const size_t tb = (table_bytes + 15u) & ~15u;
   if (kind == 2) return tb + ((A5X_RING_B + sizeof(LdsB) + 15u) & ~(size_t)15u);
   if (kind == 1) return tb + waves * ((A5X_RING_A + sizeof(LdsA) + 15u) & ~(size_t)15u);
-  return waves * ((FX_RING + sizeof(FXWin) + 15u) & ~(size_t)15u);
+  return waves * ((FX_RING + 1024 + sizeof(FXWin) + 15u) & ~(size_t)15u);
 }
 
 // kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b

@@ -73,38 +73,50 @@ A5X_HD u32 fastdiv_hd(u32 n, u32 magic, u32 shift) {
 // FAST plan records (built once per word by k_keyspace_thread, streamed by
 // k_expand_fast).  A record is a run of u64 in HBM:
 //   [0]               header  (fr_hdr)
-//   [1, 1+ng)         group descriptors, one per group piece (fr_group)
-//   [1+ng, 1+ng+ne)   piece entries: the R entries of a piece consecutive, pieces
+//   [1, 1+np)         piece descriptors, pieces in byte order (fr_desc)
+//   [1+np, 1+np+ne)   piece entries: the R entries of a piece consecutive, pieces
 //                     in order; entry = 7 content bytes + meta byte (len | (R-1) << 3)
 // A word is cut left to right into pieces of <= FW_PLEN bytes: a *group* piece
 // holds one or more consecutive substitution units (a key match with its R =
 // 1 + nvals choices, or a cluster of overlapping matches) with the literal bytes
 // around them, all R_1 x R_2 x ... <= FW_UMAXR combinations precombined; a
-// *literal* piece holds plain bytes.  Combination a_1 + R_1 (a_2 + R_2 (...)) of a
-// group is the mixed-radix digit order of its units (left unit least significant),
-// and groups are digits of the word's candidate index n = rank + 1 in the same
-// order, so candidate numbering equals the per-unit radix order of the other
-// expansion kernels.
+// *literal* piece holds plain bytes (R = 1).  Combination a_1 + R_1 (a_2 + ...)
+// of a group is the mixed-radix digit order of its units (left unit least
+// significant), and pieces are digits of the word's candidate index n = rank + 1
+// in the same order, so candidate numbering equals the per-unit radix order of
+// the other expansion kernels.
 // ---------------------------------------------------------------------------
 #define FW_PLEN 7    // bytes per piece
 #define FW_UMAXM 8   // matches per cluster unit
 #define FW_UMAXR 8   // choices per unit / group
-#define FW_PMAX 10   // pieces per word (6-bit digit|R-1 fields in one u64)
-#define FW_RMAX 256  // record u64 per word (window budget)
+#define FW_PMAX 8    // pieces per word
+#define FW_RMAX 250  // record u64 per word (window budget)
 #define FW_TILE 256  // words per keyspace tile (one workgroup)
 #define FW_TILE_REC (FW_TILE * 40)  // record u64 budget per tile (avg 320 B / word)
 #define FW_MAXL 1000 // longest candidate (+ newline) of a FAST word
-#define FW_PMAX_CNT (1u << 29)  // keyspace bound of the magic division (n * (R-1) < 2^32)
+#define FW_PMAX_CNT (1u << 24)  // candidates per FAST word: exact magic division (n (R-1) < 2^32)
+                                // and 24-bit digit products (v_mad_u32_u24)
+// big pieces (k_expand_fast window setup): consecutive small pieces combined into
+// <= FB_PLEN bytes with <= FB_RMAX combinations, entries of 16 B (15 bytes + length)
+#define FB_PLEN 15
+#define FB_RMAX 64
+#define FB_SPAN 4    // small pieces per big piece
+#define FB_NMAX 4    // big pieces per word
+#define FB_EMAX 254  // big entries per word (window budget)
 
 #define FW_M56 0x00FFFFFFFFFFFFFFull
 A5X_HD u64 fw_meta(u32 len, u32 R) { return (u64)(len | ((R - 1u) << 3)) << 56; }
 A5X_HD u32 fw_len(u64 e) { return (u32)(e >> 56) & 7u; }
 A5X_HD u64 keep_bytes64(u64 v, u32 n) { return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1ull)); }
 
-// header: np | ng << 4 | ne << 8 | lconst << 16 | maxl << 24 | minl << 36
-A5X_HD u64 fr_hdr(u32 np, u32 ng, u32 ne, u32 lconst, u32 maxl, u32 minl) {
-  return (u64)np | ((u64)ng << 4) | ((u64)ne << 8) | ((u64)lconst << 16) | ((u64)maxl << 24) | ((u64)minl << 36);
+// header: np | ng << 4 | ne << 8 | lconst << 16 | maxl << 24 | minl << 36 |
+//         nbig << 48 | first small piece of big pieces 1..3 << 51 (3 bits each)
+A5X_HD u64 fr_hdr(u32 np, u32 ng, u32 ne, u32 lconst, u32 maxl, u32 minl, u32 nbig = 0, u32 bstarts = 0) {
+  return (u64)np | ((u64)ng << 4) | ((u64)ne << 8) | ((u64)lconst << 16) | ((u64)maxl << 24) | ((u64)minl << 36) |
+         ((u64)nbig << 48) | ((u64)bstarts << 51);
 }
+A5X_HD u32 frh_nbig(u64 h) { return (u32)(h >> 48) & 7u; }
+A5X_HD u32 frh_bstart(u64 h, u32 b) { return b == 0 ? 0u : (b > 3 ? 15u : (u32)(h >> (51 + 3 * (b - 1))) & 7u); }
 A5X_HD u32 frh_np(u64 h) { return (u32)h & 15u; }
 A5X_HD u32 frh_ng(u64 h) { return (u32)(h >> 4) & 15u; }
 A5X_HD u32 frh_ne(u64 h) { return (u32)(h >> 8) & 255u; }
@@ -112,21 +124,27 @@ A5X_HD u32 frh_lconst(u64 h) { return (u32)(h >> 16) & 255u; }
 A5X_HD u32 frh_maxl(u64 h) { return (u32)(h >> 24) & 4095u; }
 A5X_HD u32 frh_minl(u64 h) { return (u32)(h >> 36) & 4095u; }
 
-// group: magic = ceil(2^32 / R) | 3-bit entry lengths << 32 | (R-1) << 56 | piece << 59.
-// q = umulhi(n, magic) = n / R exactly for n (R - 1) < 2^32 (FW_PMAX_CNT bound).
-A5X_HD u32 fr_magic(u32 R) { return (u32)((((u64)1 << 32) + R - 1) / R); }
-A5X_HD u64 fr_group(u32 R, u32 lens, u32 piece) {
-  return (u64)fr_magic(R) | ((u64)lens << 32) | ((u64)(R - 1) << 56) | ((u64)piece << 59);
+// piece descriptor: magic = ceil(2^32 / R) (0 for R = 1) | first entry (relative
+// to the entries) << 32 | (R-1) << 40 | (R == 1) << 63.  The digit of n is
+// d = n - q R with q = umulhi(n, magic) (+ n when R = 1): exact for n (R - 1) <
+// 2^32 (FW_PMAX_CNT bound).
+A5X_HD u32 fr_magic(u32 R) { return R > 1 ? (u32)((((u64)1 << 32) + R - 1) / R) : 0u; }
+A5X_HD u64 fr_desc(u32 R, u32 ebase) {
+  return (u64)fr_magic(R) | ((u64)(ebase & 255u) << 32) | ((u64)(R - 1) << 40) | ((u64)(R == 1) << 63);
 }
-A5X_HD u32 frg_R(u64 G) { return ((u32)(G >> 56) & 7u) + 1u; }
-A5X_HD u32 frg_len(u64 G, u32 d) { return (u32)(G >> (32 + 3 * d)) & 7u; }
-A5X_HD u32 frg_piece(u64 G) { return (u32)(G >> 59) & 15u; }
+A5X_HD u32 frd_R(u64 G) { return ((u32)(G >> 40) & 7u) + 1u; }
+A5X_HD u32 frd_ebase(u64 G) { return (u32)(G >> 32) & 255u; }
 
-// FAST flag fields (written by the keyspace pass): record size = 1 + ng + ne
+// FAST flag fields (written by the keyspace pass): record size = 1 + np + ne
 A5X_HD u32 ff_ng(u32 f) { return (f >> 10) & 31u; }
 A5X_HD u32 ff_ne(u32 f) { return (f >> 16) & 255u; }
 A5X_HD u32 ff_np(u32 f) { return (f >> 24) & 31u; }
-A5X_HD u32 ff_rsize(u32 f) { return 1u + ff_ng(f) + ff_ne(f); }
+A5X_HD u32 ff_rsize(u32 f) { return 1u + ff_np(f) + ff_ne(f); }
+
+// k_expand_fast window: records at wrec[0, FX_ZSLOT), wrec[FX_ZSLOT] = 0 (the
+// empty entry every piece past a word's last one reads).
+#define FX_WREC 256
+#define FX_ZSLOT 255
 
 // A word's bytes in global memory (or host memory).
 struct GWord {
@@ -306,25 +324,26 @@ A5X_HD u64 unit_choice(const W& wd, const Unit& U, const Tab& T, u32 a, u32& len
 // ---------------------------------------------------------------------------
 struct Plan {
   u32 np, ng, ne, lconst, maxl, minl;
+  u32 nbig, bstarts, bent;  // big pieces, their first small pieces (3 bits each), big entries
   bool ok;
 };
 
 // Record sinks.  gld/gst: the R <= FW_UMAXR entries of the open group (built in
-// place while units merge into it); ent(i, v): final entry i; grp(g, v): group g.
+// place while units merge into it); ent(i, v): final entry i; desc(i, v): piece i.
 struct NullSink {
   A5X_HD u64 gld(u32) const { return 0; }
   A5X_HD void gst(u32, u64) {}
   A5X_HD void ent(u32, u64) {}
-  A5X_HD void grp(u32, u64) {}
+  A5X_HD void desc(u32, u64) {}
 };
 struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
   u64* rec;
-  u32 ng;
+  u32 np;
   u64 g[FW_UMAXR];
   A5X_HD u64 gld(u32 a) const { return g[a]; }
   A5X_HD void gst(u32 a, u64 v) { g[a] = v; }
-  A5X_HD void ent(u32 i, u64 v) { rec[1 + ng + i] = v; }
-  A5X_HD void grp(u32 i, u64 v) { rec[1 + i] = v; }
+  A5X_HD void ent(u32 i, u64 v) { rec[1 + np + i] = v; }
+  A5X_HD void desc(u32 i, u64 v) { rec[1 + i] = v; }
 };
 
 // Cut a unit-radix word into pieces (see the record format above).  BUILD: also
@@ -334,14 +353,33 @@ template <bool BUILD, class W, class S>
 A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk) {
   Plan P;
   P.np = 0; P.ng = 0; P.ne = 0; P.lconst = 0; P.maxl = 0; P.minl = 0; P.ok = true;
+  P.nbig = 0; P.bstarts = 0; P.bent = 0;
   bool open = false;  // a group piece is being built
+  u32 bR = 1, bl = 0, bspan = 0;  // the big piece being filled
+  auto big_add = [&](u32 R, u32 maxlen) {  // small piece P.np (in order) joins a big piece
+    if (P.nbig && bl + maxlen <= FB_PLEN && bR * R <= FB_RMAX && bspan < FB_SPAN) {
+      P.bent += bR * R - bR;
+      bR *= R; bl += maxlen; bspan++;
+    } else {
+      if (P.nbig >= 1 && P.nbig <= 3) P.bstarts |= (P.np & 7u) << (3 * (P.nbig - 1));
+      P.nbig++;
+      P.bent += R;
+      bR = R; bl = maxlen; bspan = 1;
+    }
+  };
   u32 cR = 1, cmax = 0, cmin = 0, cpi = 0, cplen = 0;
   u32 prev = 0, p = 0;
   Unit U;
   auto close_group = [&]() {
     if constexpr (BUILD) {
       for (u32 a = 0; a < cR; a++) sk.ent(P.ne + a, sk.gld(a));
-      sk.grp(P.ng, fr_group(cR, cplen, cpi));
+      sk.desc(cpi, fr_desc(cR, P.ne));
+    }
+    {
+      const u32 np0 = P.np;
+      P.np = cpi;
+      big_add(cR, cmax);
+      P.np = np0;
     }
     P.ne += cR; P.ng++; P.maxl += cmax; P.minl += cmin;
     open = false;
@@ -352,7 +390,9 @@ A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk) {
       u64 v = nb ? wd.ld(off, nb) : 0ull;
       if (nl_last) v |= 10ull << (8 * nb);
       sk.ent(P.ne, v | fw_meta(n, 1));
+      sk.desc(P.np, fr_desc(1, P.ne));
     }
+    big_add(1, n);
     P.ne++; P.np++; P.lconst += n; P.maxl += n; P.minl += n;
   };
   while (P.ok && next_unit(wd, L, p, T, U)) {
@@ -494,8 +534,9 @@ A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx,
   const Plan PL = plan_word<false>(wd, L, T, ns);
   // minl >= 3: a candidate completes the dword that holds its first byte (see
   // fw_pass2); maxl bounds the per-round ring use
-  const bool fast = PL.ok && PL.np <= FW_PMAX && PL.ne <= 255 && 1 + PL.ng + PL.ne <= FW_RMAX &&
-                    PL.maxl <= FW_MAXL && PL.minl >= 3 && P <= FW_PMAX_CNT;
+  const bool fast = PL.ok && PL.np <= FW_PMAX && PL.ne <= 255 && 1 + PL.np + PL.ne <= FW_RMAX &&
+                    PL.maxl <= FW_MAXL && PL.minl >= 3 && P <= FW_PMAX_CNT && PL.nbig <= FB_NMAX &&
+                    PL.bent <= FB_EMAX;
   if (fast) {
     C.flags = (clusters ? 0u : (A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u))) | A5X_WF_FAST | (PL.ng << 10) |
               (PL.ne << 16) | (PL.np << 24);
@@ -509,54 +550,70 @@ A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx,
 // ---------------------------------------------------------------------------
 // k_expand_fast, per candidate (host replay in a5x_debug_plan_word)
 // ---------------------------------------------------------------------------
-// pass 1: group digits of n (= rank in the word + 1) -> per-piece fields
-// (digit | (R-1) << 3) << 6 piece; literal pieces keep field 0 (R = 1, entry 0).
-// Returns the candidate's length including '\n'.
-A5X_HD u32 fw_pass1(const u64* grp, u32 ng, u32 lconst, u32 n, u64& f) {
-  u32 len = lconst;
-  f = 0;
-  for (u32 i = 0; i < ng; i++) {
-    const u64 G = grp[i];
-    const u32 R = frg_R(G);
-    const u32 q = (u32)(((u64)n * (u32)G) >> 32);
-    const u32 d = n - q * R;
+// pass 1 over the window records wrec: word with its np piece descriptors at
+// wrec[ga, ga + np) and entries from wrec[wbe]; n = rank in the word + 1.  Each
+// piece takes its digit of n and selects its entry e[i].  NPM >= np fixed
+// iterations (so the descriptor and entry loads are issued back to back): pieces
+// past np select the empty entry wrec[FX_ZSLOT].  Returns the candidate's length
+// including '\n'.
+template <int NPM>
+A5X_HD u32 fw_pass1(const u64* wrec, u32 ga, u32 np, u32 wbe, u32 n, u64* e) {
+  u64 G[NPM];
+#pragma unroll
+  for (int i = 0; i < NPM; i++) G[i] = wrec[ga + i];  // past np: whatever follows (unused)
+  u32 idx[NPM];
+#pragma unroll
+  for (int i = 0; i < NPM; i++) {
+    const u32 ghi = (u32)(G[i] >> 32);
+    u32 q = (u32)(((u64)n * (u32)G[i]) >> 32);
+    q += n & (u32)((int)ghi >> 31);  // R = 1: q = n
+    const u32 d = n - q * (((ghi >> 8) & 7u) + 1u);
     n = q;
-    f |= (u64)(d | ((R - 1u) << 3)) << (6 * frg_piece(G));
-    len += frg_len(G, d);
+    idx[i] = (u32)i < np ? wbe + (ghi & 255u) + d : (u32)FX_ZSLOT;
+  }
+  u32 len = 0;
+#pragma unroll
+  for (int i = 0; i < NPM; i++) {
+    e[i] = wrec[idx[i]];
+    len += (u32)(e[i] >> 56) & 7u;
   }
   return len;
 }
 
-// pass 2: the candidate's pieces appended to the output as whole, aligned dwords
-// of a ring (u32 index & mask), no atomics.  The candidate starts at byte o (ring
-// relative); acc holds the n = o & 3 bytes before it: the previous candidate's
-// tail for a round's first lane (the carry), zeros otherwise.  Dword ownership:
-// the dword holding byte o belongs to the PREVIOUS candidate unless acc is the
-// carry (has_prev = false): it is returned in *head (zeros below o) for the
-// previous lane to merge into its last partial dword, which it writes.  Requires
-// the candidate to complete that dword (len >= 3, FAST minl).  Returns the ring
-// dword index of the unfinished last dword; *acc_io / *n_io = its bytes / count.
-A5X_HD u32 fw_pass2(const u64* ent, u32 np, u64 f, u32 o, u32* ring, u32 mask, bool has_prev, u32* acc_io,
-                    u32* n_io, u32* head) {
+// pass 2: the candidate's pieces e[0, NPM) appended to the output as whole,
+// aligned dwords of a ring, with plain stores and no atomics.  Byte o (ring
+// offset) is the candidate's first; acc holds the o & 3 bytes before it: the
+// previous candidate's tail for a round's first lane (the carry), zeros otherwise.
+// Dword ownership: the dword holding byte o belongs to the PREVIOUS candidate
+// unless acc is the carry (has_prev = false): it is returned in *head (zeros below
+// o) for the previous lane to merge into its last partial dword, which it writes.
+// Requires every candidate to complete that dword (len >= 3, FAST minl).  Stores
+// that are not due go to ring[trash] (a per-lane scratch dword): no branches.
+// Returns the ring dword of the unfinished last dword; *acc_io / *n_io = its
+// bytes / count.
+template <int NPM>
+A5X_HD u32 fw_pass2(const u64* e, u32 o, u32* ring, u32 trash, bool has_prev, u32* acc_io, u32* n_io, u32* head) {
   u32 acc = *acc_io, n = o & 3u, D = o >> 2;
   bool hp = has_prev && n != 0;
-  u32 hd = 0, row = 0;
-  for (u32 i = 0; i < np; i++) {
-    const u64 e = ent[row + ((u32)f & 7u)];
-    row += (((u32)f >> 3) & 7u) + 1u;
-    f >>= 6;
-    const u32 t = n + fw_len(e);
-    const u64 c = e & FW_M56;
-    const u32 sh = 8u * n;
-    const u64 lo = (u64)acc | (c << sh);
-    const u32 hi = (u32)((c >> 1) >> (63u - sh));  // bytes 8, 9 (c >> (64 - sh); 0 for sh = 0)
-    if (t >= 4u) {
-      if (hp) hd = (u32)lo;
-      else ring[D & mask] = (u32)lo;
-      hp = false;
-    }
-    if (t >= 8u) ring[(D + 1u) & mask] = (u32)(lo >> 32);
-    acc = t >= 8u ? hi : (t >= 4u ? (u32)(lo >> 32) : (u32)lo);
+  u32 hd = 0;
+#pragma unroll
+  for (int i = 0; i < NPM; i++) {
+    const u32 ehi = (u32)(e[i] >> 32);
+    const u32 t = n + ((ehi >> 24) & 7u);
+    const u32 chi = ehi & 0xFFFFFFu;
+    const u64 lo = ((((u64)chi << 32) | (u32)e[i]) << (8u * n)) | acc;
+    // bytes 8, 9 (only needed when t >= 8, i.e. n >= 1): chi >> (32 - 8n)
+#ifdef __HIP_DEVICE_COMPILE__
+    const u32 hi = __builtin_amdgcn_alignbyte(0u, chi, 0u - n);
+#else
+    const u32 hi = (u32)((((u64)chi << 32) >> (32u - 8u * (n & 3u))) >> 32);
+#endif
+    const bool c4 = t >= 4u, c8 = t >= 8u;
+    ring[(c4 && !hp) ? D : trash] = (u32)lo;
+    ring[c8 ? D + 1u : trash] = (u32)(lo >> 32);
+    hd = (c4 && hp) ? (u32)lo : hd;
+    hp = hp && !c4;
+    acc = c8 ? hi : (c4 ? (u32)(lo >> 32) : (u32)lo);
     D += t >> 2;
     n = t & 3u;
   }
@@ -564,4 +621,98 @@ A5X_HD u32 fw_pass2(const u64* ent, u32 np, u64 f, u32 o, u32* ring, u32 mask, b
   *n_io = n;
   *head = hd;
   return D;
+}
+
+// ---------------------------------------------------------------------------
+// Big pieces (k_expand_fast): the small pieces [bstart(b), bstart(b+1)) of a
+// word combined into one <= FB_PLEN-byte piece with R_b = product of their R
+// combinations (R_b <= FB_RMAX), stored as 16-B entries: bytes 0-14 content (zero
+// past the length), byte 15 = length.  Combination c of big piece b is the
+// mixed-radix digit vector of its small pieces (first small piece least
+// significant), so the big pieces are digits of n in the same order.
+// ---------------------------------------------------------------------------
+A5X_HD u32 fb_perm(u32 hi, u32 lo, u32 sel) {  // v_perm_b32 for selectors with bytes < 8
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+  const u64 v = ((u64)hi << 32) | lo;
+  u32 r = 0;
+  for (u32 i = 0; i < 4; i++) r |= (u32)((v >> (8 * ((sel >> (8 * i)) & 7u))) & 255u) << (8 * i);
+  return r;
+#endif
+}
+
+// R of big piece b of the word whose record is at wrec[wrb] (header h)
+A5X_HD u32 fb_R(const u64* wrec, u32 wrb, u64 h, u32 b) {
+  const u32 nb = frh_nbig(h), np = frh_np(h);
+  if (b >= nb) return 1;
+  const u32 s0 = frh_bstart(h, b), s1 = b + 1 < nb ? frh_bstart(h, b + 1) : np;
+  u32 R = 1;
+  for (u32 i = s0; i < s1 && i < FW_PMAX; i++) R *= frd_R(wrec[wrb + 1 + i]);
+  return R;
+}
+
+// entry c of big piece b (x, y, z, w = bytes 0-3, 4-7, 8-11, 12-14 + length)
+A5X_HD void fb_entry(const u64* wrec, u32 wrb, u32 b, u32 c, u32 out[4]) {
+  const u64 h = wrec[wrb];
+  const u32 nb = frh_nbig(h), np = frh_np(h);
+  const u32 sp0 = frh_bstart(h, b), sp1 = b + 1 < nb ? frh_bstart(h, b + 1) : np;
+  const u32 wbe = wrb + 1 + np;
+  u64 lo64 = 0, hi64 = 0;
+  u32 off = 0;
+#pragma unroll
+  for (u32 i = 0; i < FB_SPAN; i++) {
+    const bool valid = sp0 + i < sp1;
+    const u64 G = wrec[valid ? wrb + 1 + sp0 + i : (u32)FX_ZSLOT];
+    const u32 ghi = (u32)(G >> 32);
+    u32 q = (u32)(((u64)c * (u32)G) >> 32);
+    q += c & (u32)((int)ghi >> 31);  // R = 1: q = c
+    const u32 d = c - q * (((ghi >> 8) & 7u) + 1u);
+    c = q;
+    const u64 ev = wrec[valid ? wbe + (ghi & 255u) + d : (u32)FX_ZSLOT];
+    const u64 cv = ev & FW_M56;
+    if (off < 8) {
+      lo64 |= cv << (8 * off);
+      if (off) hi64 |= cv >> (64 - 8 * off);
+    } else {
+      hi64 |= cv << (8 * (off - 8));
+    }
+    off += fw_len(ev);
+  }
+  out[0] = (u32)lo64; out[1] = (u32)(lo64 >> 32); out[2] = (u32)hi64;
+  out[3] = ((u32)(hi64 >> 32) & 0xFFFFFFu) | (off << 24);
+}
+
+// One big piece appended to a candidate's output as whole, aligned dwords of a
+// ring: entry e (e[3] byte 3 = length) after the n pending bytes held in the TOP n
+// bytes of pv; complete dwords go to ring[D ..].  Dword ownership: the dword
+// holding a candidate's first byte belongs to the PREVIOUS candidate unless the
+// pending bytes are the carry; while hp is set, the first complete dword is kept in
+// hd (zeros below the candidate's first byte) for the previous lane to merge into
+// its last partial dword.  Stores that are not due go to ring[T + k] (the lane's 4
+// trash dwords): no branches.  acc = the unfinished dword (bottom-aligned n bytes).
+A5X_HD void fb_put(const u32 e[4], u32& pv, u32& n, u32& D, bool& hp, u32& hd, u32& acc, u32* ring, u32 T) {
+  const u32 sel = (u32)(0x0706050403020100ull >> (32u - 8u * n));  // bytes 4-n .. 7-n of {s_k, s_k-1}
+  const u32 s3 = e[3] & 0xFFFFFFu;
+  const u32 w0 = fb_perm(e[0], pv, sel);
+  const u32 w1 = fb_perm(e[1], e[0], sel);
+  const u32 w2 = fb_perm(e[2], e[1], sel);
+  const u32 w3 = fb_perm(s3, e[2], sel);
+  const u32 w4 = fb_perm(0u, s3, sel);
+  const u32 t = n + (e[3] >> 24);
+  const bool m1 = t >= 4u, m2 = t >= 8u, m3 = t >= 12u, m4 = t >= 16u;
+  ring[(m1 && !hp) ? D : T] = w0;
+  ring[(m2 ? D : T) + 1u] = w1;
+  ring[(m3 ? D : T) + 2u] = w2;
+  ring[(m4 ? D : T) + 3u] = w3;
+  hd = (m1 && hp) ? w0 : hd;
+  hp = hp && !m1;
+  u32 x = m1 ? w1 : w0;
+  x = m2 ? w2 : x;
+  x = m3 ? w3 : x;
+  x = m4 ? w4 : x;
+  acc = x;
+  n = t & 3u;
+  pv = acc << ((32u - 8u * n) & 31u);
+  D += t >> 2;
 }

@@ -5,9 +5,10 @@ import glob
 import sys
 
 tag = sys.argv[1]
+pat = f"{tag}*/run_counter_collection.csv" if "/" in tag else f"gpurun_out/pmc_{tag}_*/run_counter_collection.csv"
 agg = collections.defaultdict(float)
 disp = collections.defaultdict(set)
-for f in sorted(glob.glob(f"gpurun_out/pmc_{tag}_*/run_counter_collection.csv")):
+for f in sorted(glob.glob(pat)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0]
         agg[(k, r["Counter_Name"])] += float(r["Counter_Value"])
