@@ -31,7 +31,8 @@ struct A5xTableHdr {
   uint32_t max_klen;
   uint32_t max_vlen;
   uint32_t has_empty_key; // the map has "" (matters for -s only, main.go:315)
-  uint32_t pad[4];
+  uint32_t max_bucket;    // most keys sharing a first byte
+  uint32_t pad[3];
 };
 
 struct A5xKey {

@@ -82,7 +82,7 @@ struct a5x_ctx {
   uint32_t table_bytes = 0;
 
   DevBuf<uint64_t> count, bytes, cand_off, byte_off, scan_tmp, locate;
-  DevBuf<uint32_t> flags, defer, chunk_w0, chunk_kind, roff;
+  DevBuf<uint32_t> flags, defer, chunk_w0, chunk_kind, roff, cplx;
   DevBuf<uint64_t> rec;  // FAST plan records (keyspace tiles of FW_TILE_REC u64)
   uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] nslow, [16..31] guard record
   uint32_t* h_scalars = nullptr;  // pinned
@@ -260,6 +260,7 @@ int compile_table(a5x_ctx* c) {
   h.max_klen = max_klen;
   h.max_vlen = max_vlen;
   h.has_empty_key = t.index.count(std::string()) ? 1u : 0u;
+  for (int b = 0; b < 256; b++) h.max_bucket = std::max<uint32_t>(h.max_bucket, bucket[b + 1] - bucket[b]);
   if (h.total_bytes > A5X_TABLE_LDS_MAX)
     return fail(c, A5X_E_UNSUPPORTED, "device table is %u bytes (LDS staging max %u)", h.total_bytes,
                 (unsigned)A5X_TABLE_LDS_MAX);
@@ -320,6 +321,10 @@ int decode_dev_err(a5x_ctx* c, uint32_t e) {
   return fail(c, A5X_E_HIP, "device consistency error 0x%x", e);
 }
 
+// words with overlapping keys (or other irregular shapes) whose FAST records go to
+// fixed slots after the tile regions: at most this many per batch (the rest: slow path)
+uint32_t ks_cplx_cap(uint64_t nw) { return (uint32_t)std::min<uint64_t>(nw / 16 + 1024, 1u << 22); }
+
 struct Batch {  // device-side per-batch state after keyspace
   uint64_t total_cands = 0, total_bytes = 0;
   uint32_t nbig = 0, nslow = 0;
@@ -335,8 +340,9 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   if (nw > 0xffffffffull) return fail(c, A5X_E_ARG, "batch of %llu words (max 2^32-1)", (unsigned long long)nw);
   if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
       (rc = grow(c, c->defer, nw + 1)) || (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)) ||
-      (rc = grow(c, c->roff, nw + 1)) ||
-      (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC + 2)))
+      (rc = grow(c, c->roff, nw + 1)) || (rc = grow(c, c->cplx, nw + 1)) ||
+      (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC +
+                                (uint64_t)ks_cplx_cap(nw) * FW_RMAX + 2)))
     return rc;
   if (!d_cand_off) {
     if ((rc = grow(c, c->cand_off, nw + 1))) return rc;
@@ -355,6 +361,8 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
     K.defer_list = c->defer.p; K.defer_n = c->d_scalars; K.nbig = c->d_scalars + 1; K.err = c->d_scalars + 2;
     K.nslow = c->d_scalars + 3;
     K.rec = c->rec.p; K.roff = c->roff.p;
+    K.cplx_list = c->cplx.p; K.cplx_n = c->d_scalars + 4; K.cplx_cap = ks_cplx_cap(nw);
+    K.cplx_base = ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC;
     K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nw, (uint64_t)c->cus * 4));
     HIPCHK(c, a5x_launch_keyspace(K, st));
     HIPCHK(c, a5x_launch_scan(c->count.p, c->bytes.p, nw, d_cand_off, d_byte_off, c->scan_tmp.p,

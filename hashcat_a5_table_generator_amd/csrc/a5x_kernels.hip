@@ -158,7 +158,23 @@ struct KsArgs {
   u32* err;
   u64* rec;     // FAST plan records: tile t owns rec[t * FW_TILE_REC, (t + 1) * FW_TILE_REC)
   u32* roff;    // per word: record offset (u64 units) into rec
+  u32* cplx_list;  // words for k_keyspace_cplx
+  u32* cplx_n;
+  u32 cplx_cap;    // record slots (FW_RMAX u64 each) at rec + cplx_base
+  u64 cplx_base;
 };
+
+// Append the lanes with pred to list[*ctr ...] (one atomic per wave); returns the
+// lane's slot (valid where pred).  Every lane of the wave must call it.
+__device__ __forceinline__ u32 wave_append(bool pred, u32* ctr) {
+  const u64 m = __ballot(pred);
+  if (!m) return 0;
+  const u32 lane = lane_id(), leader = (u32)__builtin_ctzll(m);
+  u32 base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (u32)__popcll(m));
+  base = (u32)__shfl((int)base, (int)leader);
+  return base + (u32)__popcll(m & ((1ull << lane) - 1ull));
+}
 
 // The open group of plan_word lives in LDS (FW_UMAXR u64 per lane, lane-strided);
 // entries and group descriptors go straight to the word's record in HBM.
@@ -205,10 +221,58 @@ __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const
   if (!P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
 }
 
+// Position-synchronous word walk of k_keyspace_thread: every lane steps through byte
+// positions q = 0, 1, ... of its own word together (one fixed-size body per
+// position), so a wave of words costs max(L) steps instead of the union of 64
+// data-dependent loops.  At q: the keys of the first-byte bucket are compared (4
+// bytes at once; keys of <= 4 bytes); a lone match starts a unit handed to the
+// Planner (and the closed-form count).  Two matches at one position or a match
+// inside a unit's span (overlapping keys: clusters), or a key longer than 4 bytes
+// at q, make the word "complex": k_keyspace_cplx walks it with next_unit.
+template <bool COUNT, class PL>
+__device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 Lmax, u32 bmax, const Tab& T,
+                                         PL& pl, CountAcc& A, bool& cplx) {
+  u32 cur_end = 0;
+  for (u32 q = 0; q < Lmax; q++) {
+    const bool act = act0 && q < L && !cplx;
+    if (act) {
+      const u32 b = lw.at(q);
+      const u32 ks = T.bucket[b], ke = T.bucket[b + 1];
+      const u32 w4 = lds_ld4(lw.base, lw.off + q);
+      u32 nm = 0, kk = 0;
+      for (u32 i = 0; i < bmax; i++) {
+        const u32 k2 = ks + i;
+        if (k2 < ke) {
+          const A5xKey key = T.keys[k2];
+          const u32 kl = key.klen;
+          if (q + kl <= L) {
+            if (kl > 4) {
+              cplx = true;
+            } else {
+              const u32 m = kl >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kl)) - 1u);
+              if ((w4 & m) == T.ch[key.choice_base].first4) { nm++; kk = k2; }
+            }
+          }
+        }
+      }
+      if (nm > 1 || (nm == 1 && q < cur_end)) {
+        cplx = true;
+      } else if (nm == 1 && !cplx) {
+        Unit U;
+        lone_unit(T, q, kk, U);
+        if (COUNT) count_unit(A, U);
+        pl.unit(U);
+        cur_end = U.e;
+      }
+    }
+  }
+}
+
+
 // One lane per word, one 256-word tile per workgroup iteration: classification,
 // closed-form (count, bytes), and for FAST words the plan record, packed densely
 // in word order inside the tile's record region (workgroup scan of the sizes).
-// The tile's word bytes are staged in LDS with 16-B loads when they fit KS_WB.
+// The tile's word bytes are staged in LDS with 16-B loads.
 __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 tb = (a.table_bytes + 15u) & ~15u;
@@ -218,6 +282,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   load_table(smem, a.table, a.table_bytes);
   __syncthreads();
   const Tab T = tab_view(smem);
+  const u32 bmax = T.hdr->max_bucket;
   const u32 tid = threadIdx.x, lane = lane_id(), wv = tid / 64;
   const u64 ntiles = (a.nw + FW_TILE - 1) / FW_TILE;
   for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -242,21 +307,38 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       }
     }
     __syncthreads();
-    WordClass C;
-    C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
-    u32 f = 0;
     u64 s = 0, L64 = 0;
-    LWord lw;
-    GWord gw;
     if (valid) {
       s = a.woff[w];
       L64 = a.woff[w + 1] - s;
-      lw.base = wb; lw.off = (u32)(s - A0);
-      gw.p = a.words + s;
-      f = staged ? ks_classify(lw, L64, T, a, C) : ks_classify(gw, L64, T, a, C);
     }
-    // record sizes -> exclusive workgroup scan
-    const bool fast = valid && (f & A5X_WF_FAST) && C.count > 0;
+    const bool longw = valid && L64 > A5X_LMAX_A && a.mx >= 1;   // the wave DP kernel
+    const bool trivial = valid && (a.mx < 1 || L64 == 0);       // processWord emits nothing
+    bool cplx = valid && !longw && !trivial && !staged;
+    const bool psk = valid && !longw && !trivial && staged;
+    const u32 L = psk ? (u32)L64 : 0u;
+    LWord lw;
+    lw.base = wb; lw.off = psk ? (u32)(s - A0) : 0u;
+    // ---- pass 1: units -> counts + piece plan (count mode) ----
+    CountAcc A;
+    count_init(A, L);
+    NullSink ns;
+    Planner<false, LWord, NullSink> pl(lw, T, ns);
+    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx);
+    WordClass C;
+    C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
+    u32 f = 0;
+    if (psk && !cplx) {
+      pl.finish(L);
+      C = classify_finish(A, pl.P, L, a.mn, a.mx, A5X_RING_A - 16);
+      f = C.flags;
+      if (C.ovf) atomicOr(a.err, A5X_DERR_OVF);
+      if ((f & A5X_WF_DEFER) || !(f & (A5X_WF_FAST | A5X_WF_RADIX | A5X_WF_ERR_OVF))) f = A5X_WF_DEFER;
+    }
+    if (trivial) f = A5X_WF_RADIX | A5X_WF_FAST;
+    if (longw) f = A5X_WF_DEFER;
+    // ---- record sizes -> exclusive workgroup scan ----
+    const bool fast = psk && !cplx && (f & A5X_WF_FAST) && C.count > 0;
     const u32 rs = fast ? ff_rsize(f) : 0u;
     const u32 inc = wave_incl_scan_u32(rs);
     if (lane == 63) wsum[wv] = inc;
@@ -264,29 +346,78 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     u32 base = 0;
     for (u32 k = 0; k < wv; k++) base += wsum[k];
     const u32 ro = base + inc - rs;
-    bool built = false;
-    if (fast && ro + rs <= FW_TILE_REC) {
+    const bool build = fast && ro + rs <= FW_TILE_REC;
+    // ---- pass 2: the records of the FAST words (same walk, build mode) ----
+    {
       u64* rec = a.rec + tile * FW_TILE_REC + ro;
-      if (staged) ks_build(lw, (u32)L64, T, a, f, rec, gbuf + tid);
-      else ks_build(gw, (u32)L64, T, a, f, rec, gbuf + tid);
-      a.roff[w] = (u32)(tile * FW_TILE_REC + ro);
-      built = true;
+      DevRecSink sk;
+      sk.g = gbuf + tid; sk.rec = rec; sk.np = ff_np(f);
+      Planner<true, LWord, DevRecSink> pb(lw, T, sk);
+      CountAcc A2;
+      bool c2 = false;
+      psk_walk<false>(lw, L, build, wave_max_u32(build ? L : 0u), bmax, T, pb, A2, c2);
+      if (build) {
+        pb.finish(L);
+        const Plan& P = pb.P;
+        rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl, P.nbig, P.bstarts);
+        if (c2 || !P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
+        a.roff[w] = (u32)(tile * FW_TILE_REC + ro);
+      }
     }
-    if (valid) {
-      if ((f & A5X_WF_FAST) && C.count > 0 && !built) {
-        // the tile's record budget is spent: the slow path takes the word
-        f = C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
-      }
-      if (f & A5X_WF_DEFER) {
-        a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
-      } else if (!(f & (A5X_WF_FAST | A5X_WF_ERR_OVF))) {
-        atomicAdd(a.nslow, 1u);
-      }
+    if (fast && !build) {
+      // the tile's record budget is spent: the slow path takes the word
+      f = C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
+    }
+    // ---- lists (one atomic per wave each) and per-word results ----
+    const u32 ci = wave_append(cplx, a.cplx_list ? a.cplx_n : a.defer_n);
+    if (cplx) a.cplx_list[ci] = (u32)w;
+    const bool dfr = valid && !cplx && (f & A5X_WF_DEFER);
+    const u32 di = wave_append(dfr, a.defer_n);
+    if (dfr) a.defer_list[di] = (u32)w;
+    const bool slow = valid && !cplx && !(f & (A5X_WF_DEFER | A5X_WF_FAST | A5X_WF_ERR_OVF));
+    wave_append(slow, a.nslow);
+    if (valid && !cplx) {
       a.count[w] = (f & A5X_WF_DEFER) ? 0 : C.count;
       a.bytes[w] = (f & A5X_WF_DEFER) ? 0 : C.bytes;
       a.flags[w] = f;
     }
     __syncthreads();  // wb / wsum are rewritten by the next tile
+  }
+}
+
+// The complex words of k_keyspace_thread (overlapping keys, long keys, oversize
+// tiles), one lane per listed word: the general unit walk (next_unit) on global
+// bytes; FAST records go to fixed slots after the tile regions.
+__global__ void __launch_bounds__(256) k_keyspace_cplx(KsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const u32 tb = (a.table_bytes + 15u) & ~15u;
+  u64* gbuf = (u64*)(smem + tb);
+  load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  const u32 n = *a.cplx_n;
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const u64 w = a.cplx_list[i];
+    const u64 s = a.woff[w], L64 = a.woff[w + 1] - s;
+    GWord gw;
+    gw.p = a.words + s;
+    WordClass C;
+    C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
+    u32 f = ks_classify(gw, L64, T, a, C);
+    if ((f & A5X_WF_FAST) && C.count > 0) {
+      if (i < a.cplx_cap) {
+        u64* rec = a.rec + a.cplx_base + (u64)i * FW_RMAX;
+        ks_build(gw, (u32)L64, T, a, f, rec, gbuf + threadIdx.x);
+        a.roff[w] = (u32)(a.cplx_base + (u64)i * FW_RMAX);
+      } else {
+        f = C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
+      }
+    }
+    if (f & A5X_WF_DEFER) a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
+    else if (!(f & (A5X_WF_FAST | A5X_WF_ERR_OVF))) atomicAdd(a.nslow, 1u);
+    a.count[w] = (f & A5X_WF_DEFER) ? 0 : C.count;
+    a.bytes[w] = (f & A5X_WF_DEFER) ? 0 : C.bytes;
+    a.flags[w] = f;
   }
 }
 
@@ -1208,7 +1339,11 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     const bool fast = (fl & A5X_WF_FAST) && c0 < g1;
     const u32 rs = (fast && hasc) ? ff_rsize(fl) : 0u;
     const u32 incR = wave_incl_scan_u32(rs);
-    const bool ok = fast && incR < FX_ZSLOT;
+    // records must be one contiguous range (complex words have slots elsewhere)
+    const u64 rm = __ballot(rs > 0);
+    const u32 rbase = readlane_u32(M.roff, rm ? (u32)__builtin_ctzll(rm) : 0u);
+    const bool contig = rs == 0 || M.roff == rbase + (incR - rs);
+    const bool ok = fast && incR < FX_ZSLOT && contig;
     const u64 badm = __ballot(!ok);
     u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
     STAMP(0);
@@ -1523,8 +1658,12 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   a.mn = L.mn; a.mx = L.mx; a.count = L.count; a.bytes = L.bytes; a.flags = L.flags;
   a.defer_list = L.defer_list; a.defer_n = L.defer_n; a.nbig = L.nbig; a.nslow = L.nslow; a.err = L.err;
   a.rec = L.rec; a.roff = L.roff;
+  a.cplx_list = L.cplx_list; a.cplx_n = L.cplx_n; a.cplx_cap = L.cplx_cap; a.cplx_base = L.cplx_base;
   hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_keyspace_cplx, dim3(L.defer_blocks), dim3(256), ((L.table_bytes + 15u) & ~15u) + 256 * FW_UMAXR * 8, st, a);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t lds = ((L.table_bytes + 15u) & ~15u) + sizeof(LdsB);
   hipLaunchKernelGGL(k_keyspace_wave, dim3(L.defer_blocks), dim3(64), lds, st, a);
@@ -1638,6 +1777,8 @@ hipError_t a5x_set_kernel_attrs() {
   e = hipFuncSetAttribute((const void*)k_keyspace_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_keyspace_thread, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_keyspace_cplx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_locate, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;

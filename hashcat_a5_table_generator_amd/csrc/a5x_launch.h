@@ -20,8 +20,12 @@ struct A5xKsLaunch {
   uint32_t* nslow;
   uint32_t* err;
   uint32_t defer_blocks;
-  uint64_t* rec;   // FAST plan records (tile regions of FW_TILE_REC u64)
+  uint64_t* rec;   // FAST plan records (tile regions of FW_TILE_REC u64, then complex slots)
   uint32_t* roff;  // per-word record offsets
+  uint32_t* cplx_list;  // words for the general (per-lane walk) keyspace pass
+  uint32_t* cplx_n;
+  uint32_t cplx_cap;    // record slots of FW_RMAX u64 from rec + cplx_base
+  uint64_t cplx_base;
 };
 
 struct A5xExpLaunch {

@@ -346,45 +346,47 @@ struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
   A5X_HD void desc(u32 i, u64 v) { rec[1 + i] = v; }
 };
 
-// Cut a unit-radix word into pieces (see the record format above).  BUILD: also
-// write the entries and group descriptors through the sink (the header is the
-// caller's: fr_hdr of the returned Plan).
+// Cut a unit-radix word into pieces (see the record format above), one unit at a
+// time (unit() in word order, then finish()).  BUILD: also write the entries and
+// piece descriptors through the sink (the header is the caller's: fr_hdr of P).
+// Shared by the unit walk (plan_word) and the position-synchronous keyspace kernel.
 template <bool BUILD, class W, class S>
-A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk) {
+struct Planner {
+  const W& wd;
+  const Tab& T;
+  S& sk;
   Plan P;
-  P.np = 0; P.ng = 0; P.ne = 0; P.lconst = 0; P.maxl = 0; P.minl = 0; P.ok = true;
-  P.nbig = 0; P.bstarts = 0; P.bent = 0;
-  bool open = false;  // a group piece is being built
-  u32 bR = 1, bl = 0, bspan = 0;  // the big piece being filled
-  auto big_add = [&](u32 R, u32 maxlen) {  // small piece P.np (in order) joins a big piece
+  bool open;                    // a group piece is being built
+  u32 bR, bl, bspan;            // the big piece being filled
+  u32 cR, cmax, cmin, cpi, prev;
+
+  A5X_HD Planner(const W& w, const Tab& t, S& s) : wd(w), T(t), sk(s) {
+    P.np = 0; P.ng = 0; P.ne = 0; P.lconst = 0; P.maxl = 0; P.minl = 0; P.ok = true;
+    P.nbig = 0; P.bstarts = 0; P.bent = 0;
+    open = false; bR = 1; bl = 0; bspan = 0; cR = 1; cmax = 0; cmin = 0; cpi = 0; prev = 0;
+  }
+  A5X_HD void big_add(u32 R, u32 maxlen, u32 pi) {  // small piece pi (in order) joins a big piece
     if (P.nbig && bl + maxlen <= FB_PLEN && bR * R <= FB_RMAX && bspan < FB_SPAN) {
       P.bent += bR * R - bR;
       bR *= R; bl += maxlen; bspan++;
     } else {
-      if (P.nbig >= 1 && P.nbig <= 3) P.bstarts |= (P.np & 7u) << (3 * (P.nbig - 1));
+      if (P.nbig >= 1 && P.nbig <= 3) P.bstarts |= (pi & 7u) << (3 * (P.nbig - 1));
       P.nbig++;
       P.bent += R;
       bR = R; bl = maxlen; bspan = 1;
     }
-  };
-  u32 cR = 1, cmax = 0, cmin = 0, cpi = 0, cplen = 0;
-  u32 prev = 0, p = 0;
-  Unit U;
-  auto close_group = [&]() {
+  }
+  A5X_HD void close_group() {
     if constexpr (BUILD) {
-      for (u32 a = 0; a < cR; a++) sk.ent(P.ne + a, sk.gld(a));
+      for (u32 a = 0; a < FW_UMAXR; a++)
+        if (a < cR) sk.ent(P.ne + a, sk.gld(a));
       sk.desc(cpi, fr_desc(cR, P.ne));
     }
-    {
-      const u32 np0 = P.np;
-      P.np = cpi;
-      big_add(cR, cmax);
-      P.np = np0;
-    }
+    big_add(cR, cmax, cpi);
     P.ne += cR; P.ng++; P.maxl += cmax; P.minl += cmin;
     open = false;
-  };
-  auto literal = [&](u32 off, u32 n, bool nl_last) {  // one literal piece of n bytes
+  }
+  A5X_HD void literal(u32 off, u32 n, bool nl_last) {  // one literal piece of n bytes
     if constexpr (BUILD) {
       const u32 nb = nl_last ? n - 1 : n;
       u64 v = nb ? wd.ld(off, nb) : 0ull;
@@ -392,31 +394,30 @@ A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk) {
       sk.ent(P.ne, v | fw_meta(n, 1));
       sk.desc(P.np, fr_desc(1, P.ne));
     }
-    big_add(1, n);
+    big_add(1, n, P.np);
     P.ne++; P.np++; P.lconst += n; P.maxl += n; P.minl += n;
-  };
-  while (P.ok && next_unit(wd, L, p, T, U)) {
+  }
+  A5X_HD void unit(const Unit& U) {
+    if (!P.ok) return;
     const u32 Ru = U.R, ml = U.ml, run = U.s - prev;
-    if (!U.ok || ml > FW_PLEN || Ru > FW_UMAXR || Ru < 2) { P.ok = false; break; }
+    if (!U.ok || ml > FW_PLEN || Ru > FW_UMAXR || Ru < 2) { P.ok = false; return; }
     if (open && cmax + run + ml <= FW_PLEN && cR * Ru <= FW_UMAXR) {
-      // merge: entry a1 + cR * a2 = old[a1] ++ run ++ choice a2 (descending: in place)
+      // merge: entry a1 + cR * a2 = old[a1] ++ run ++ choice a2 (descending: in place;
+      // fixed trip count so lanes of a wave stay together)
       const u32 nR = cR * Ru;
       if constexpr (BUILD) {
-        u32 nplen = 0;
         const u64 rb = run ? wd.ld(prev, run) : 0ull;
-        for (int a2 = (int)Ru - 1; a2 >= 0; a2--) {
+        const u32 inv = (256u + cR - 1u) / cR;  // t / cR = (t * inv) >> 8 for t < 8
+        for (int t = FW_UMAXR - 1; t >= 0; t--) {
+          if ((u32)t >= nR) continue;
+          const u32 a2 = ((u32)t * inv) >> 8, a1 = (u32)t - a2 * cR;
           u32 cl = 0;
-          const u64 cv = unit_choice(wd, U, T, (u32)a2, cl);
-          for (int a1 = (int)cR - 1; a1 >= 0; a1--) {
-            const u64 old = sk.gld((u32)a1);
-            const u32 ol = fw_len(old);
-            const u32 nl = ol + run + cl;
-            const u64 v = (old & FW_M56) | (rb << (8 * ol)) | (cv << (8 * (ol + run)));
-            sk.gst((u32)a1 + cR * (u32)a2, (v & FW_M56) | fw_meta(nl, nR));
-            nplen |= nl << (3 * ((u32)a1 + cR * (u32)a2));
-          }
+          const u64 cv = unit_choice(wd, U, T, a2, cl);
+          const u64 old = sk.gld(a1);
+          const u32 ol = fw_len(old);
+          const u64 v = (old & FW_M56) | (rb << (8 * ol)) | (cv << (8 * (ol + run)));
+          sk.gst((u32)t, (v & FW_M56) | fw_meta(ol + run + cl, nR));
         }
-        cplen = nplen;
       }
       cR = nR; cmax += run + ml; cmin += run + U.mnl;
     } else {
@@ -427,48 +428,66 @@ A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk) {
         literal(off, n, false);
         off += n; rem -= n;
       }
-      open = true; cR = Ru; cmax = rem + ml; cmin = rem + U.mnl; cpi = P.np; cplen = 0;
+      open = true; cR = Ru; cmax = rem + ml; cmin = rem + U.mnl; cpi = P.np;
       P.np++;
       if constexpr (BUILD) {
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
-        for (u32 a = 0; a < Ru; a++) {
+        for (u32 a = 0; a < FW_UMAXR; a++) {
+          if (a >= Ru) continue;
           u32 cl = 0;
           const u64 cv = unit_choice(wd, U, T, a, cl);
           const u64 v = rb | (cv << (8 * rem));
           sk.gst(a, (v & FW_M56) | fw_meta(rem + cl, Ru));
-          cplen |= (rem + cl) << (3 * a);
         }
       }
     }
     prev = U.e;
   }
-  if (!P.ok) return P;
-  // tail bytes + '\n'
-  const u32 run = L - prev, tl = run + 1;
-  if (open && cmax + tl <= FW_PLEN) {
-    if constexpr (BUILD) {
-      const u64 tb = (run ? wd.ld(prev, run) : 0ull) | (10ull << (8 * run));
-      u32 nplen = 0;
-      for (u32 a = 0; a < cR; a++) {
-        const u64 old = sk.gld(a);
-        const u32 ol = fw_len(old);
-        sk.gst(a, ((old | (tb << (8 * ol))) & FW_M56) | fw_meta(ol + tl, cR));
-        nplen |= (ol + tl) << (3 * a);
+  A5X_HD void finish(u32 L) {  // tail bytes + '\n'
+    if (!P.ok) return;
+    const u32 run = L - prev, tl = run + 1;
+    if (open && cmax + tl <= FW_PLEN) {
+      if constexpr (BUILD) {
+        const u64 tb = (run ? wd.ld(prev, run) : 0ull) | (10ull << (8 * run));
+        for (u32 a = 0; a < FW_UMAXR; a++) {
+          if (a >= cR) continue;
+          const u64 old = sk.gld(a);
+          const u32 ol = fw_len(old);
+          sk.gst(a, ((old | (tb << (8 * ol))) & FW_M56) | fw_meta(ol + tl, cR));
+        }
       }
-      cplen = nplen;
-    }
-    cmax += tl; cmin += tl;
-    close_group();
-  } else {
-    if (open) close_group();
-    u32 off = prev, rem = tl;
-    while (rem) {
-      const u32 n = umin32(FW_PLEN, rem);
-      literal(off, n, n == rem);
-      off += n; rem -= n;
+      cmax += tl; cmin += tl;
+      close_group();
+    } else {
+      if (open) close_group();
+      u32 off = prev, rem = tl;
+      while (rem) {
+        const u32 n = umin32(FW_PLEN, rem);
+        literal(off, n, n == rem);
+        off += n; rem -= n;
+      }
     }
   }
-  return P;
+};
+
+template <bool BUILD, class W, class S>
+A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk) {
+  Planner<BUILD, W, S> pl(wd, T, sk);
+  u32 p = 0;
+  Unit U;
+  while (pl.P.ok && next_unit(wd, L, p, T, U)) pl.unit(U);
+  pl.finish(L);
+  return pl.P;
+}
+
+// The unit of a lone match of key k at position s (next_unit's single-match case).
+A5X_HD void lone_unit(const Tab& T, u32 s, u32 k, Unit& U) {
+  const A5xKey key = T.keys[k];
+  U.s = s; U.e = s + key.klen; U.nm = 1;
+  U.key = k; U.k = 0; U.m0 = 0; U.m1 = 0;
+  U.R = key.nvals + 1u; U.ml = key.maxclen; U.mnl = key.minclen;
+  U.spos = key.sum_dpos; U.sneg = key.sum_dneg; U.maxd = key.maxdelta;
+  U.ok = true;
 }
 
 // ---------------------------------------------------------------------------
@@ -481,70 +500,96 @@ struct WordClass {
   bool clusters;   // the word has overlapping-key units (the slow path needs the DP)
 };
 
-// ringmax: the slow kernel's per-wave ring (a radix word's longest candidate must fit)
-template <class W>
-A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx, u32 ringmax) {
+// Closed-form keyspace accumulated unit by unit (P = product of R,
+// bytes = (P - 1)(L + 1) + signed length deltas), plus the word-shape facts the
+// class decision needs.
+struct CountAcc {
+  u64 P, Dp, Dn;
+  u32 nmatch, nunits, maxl;
+  bool bin, clusters, ok, ovf;
+};
+A5X_HD void count_init(CountAcc& A, u32 L) {
+  A.P = 1; A.Dp = 0; A.Dn = 0; A.nmatch = 0; A.nunits = 0; A.maxl = L + 1;
+  A.bin = true; A.clusters = false; A.ok = true; A.ovf = false;
+}
+A5X_HD void count_unit(CountAcc& A, const Unit& U) {
+  A.nunits++;
+  A.nmatch += U.nm;
+  if (U.k) {
+    A.clusters = true;
+    if (!U.ok) A.ok = false;
+  }
+  const u64 R = U.R;
+  // sum over the unit's choices of (|choice| - span), split by sign
+  A.Dp = add_ovf(mul_ovf(A.Dp, R, A.ovf), mul_ovf(A.P, U.spos, A.ovf), A.ovf);
+  A.Dn = add_ovf(mul_ovf(A.Dn, R, A.ovf), mul_ovf(A.P, U.sneg, A.ovf), A.ovf);
+  A.P = mul_ovf(A.P, R, A.ovf);
+  if (U.k || U.R != 2) A.bin = false;
+  if (U.maxd > 0) A.maxl += (u32)U.maxd;
+}
+
+// The class decision from the accumulated units and the piece plan.  ringmax: the
+// slow kernel's per-wave ring (a radix word's longest candidate must fit).
+A5X_HD WordClass classify_finish(const CountAcc& A, const Plan& PL, u32 L, int mn, int mx, u32 ringmax) {
   WordClass C;
-  C.count = 0; C.bytes = 0; C.flags = 0; C.ovf = false; C.clusters = false;
-  if (mx < 1 || L == 0) {  // processWord emits nothing
+  C.count = 0; C.bytes = 0; C.flags = 0; C.ovf = false; C.clusters = A.clusters;
+  if (A.ok && A.nunits == 0) {
     C.flags = A5X_WF_RADIX | A5X_WF_FAST;
     return C;
   }
-  u32 p = 0, nmatch = 0, maxl = L + 1, nunits = 0;
-  bool bin = true, clusters = false, ok = true, ovf = false;
-  u64 P = 1, Dp = 0, Dn = 0;
-  Unit U;
-  while (next_unit(wd, L, p, T, U)) {
-    nunits++;
-    nmatch += U.nm;
-    if (U.k) {
-      clusters = true;
-      if (!U.ok) { ok = false; break; }
-    }
-    const u64 R = U.R;
-    // sum over the unit's choices of (|choice| - span), split by sign
-    Dp = add_ovf(mul_ovf(Dp, R, ovf), mul_ovf(P, U.spos, ovf), ovf);
-    Dn = add_ovf(mul_ovf(Dn, R, ovf), mul_ovf(P, U.sneg, ovf), ovf);
-    P = mul_ovf(P, R, ovf);
-    if (U.k || U.R != 2) bin = false;
-    if (U.maxd > 0) maxl += (u32)U.maxd;
-  }
-  C.clusters = clusters;
-  if (ok && nunits == 0) {
-    C.flags = A5X_WF_RADIX | A5X_WF_FAST;
-    return C;
-  }
-  const bool freew = (mn <= 1) && ((i64)nmatch <= (i64)mx);
-  if (!ok || !freew || ovf || P > (1ull << 32) || maxl > ringmax) {
+  const bool freew = (mn <= 1) && ((i64)A.nmatch <= (i64)mx);
+  if (!A.ok || !freew || A.ovf || A.P > (1ull << 32) || A.maxl > ringmax) {
     C.flags = A5X_WF_DEFER;
     return C;
   }
   bool o2 = false;
-  const u64 cnt = P - 1;
-  u64 byt = add_ovf(mul_ovf(cnt, (u64)L + 1, o2), Dp, o2);
-  if (byt < Dn) o2 = true;
-  byt -= Dn;
+  const u64 cnt = A.P - 1;
+  u64 byt = add_ovf(mul_ovf(cnt, (u64)L + 1, o2), A.Dp, o2);
+  if (byt < A.Dn) o2 = true;
+  byt -= A.Dn;
   if (o2) {
     C.flags = A5X_WF_ERR_OVF;
     C.ovf = true;
     return C;
   }
   C.count = cnt; C.bytes = byt;
-  NullSink ns;
-  const Plan PL = plan_word<false>(wd, L, T, ns);
   // minl >= 3: a candidate completes the dword that holds its first byte (see
-  // fw_pass2); maxl bounds the per-round ring use
+  // fb_put); maxl bounds the per-round ring use
   const bool fast = PL.ok && PL.np <= FW_PMAX && PL.ne <= 255 && 1 + PL.np + PL.ne <= FW_RMAX &&
-                    PL.maxl <= FW_MAXL && PL.minl >= 3 && P <= FW_PMAX_CNT && PL.nbig <= FB_NMAX &&
+                    PL.maxl <= FW_MAXL && PL.minl >= 3 && A.P <= FW_PMAX_CNT && PL.nbig <= FB_NMAX &&
                     PL.bent <= FB_EMAX;
   if (fast) {
-    C.flags = (clusters ? 0u : (A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u))) | A5X_WF_FAST | (PL.ng << 10) |
+    C.flags = (A.clusters ? 0u : (A5X_WF_RADIX | (A.bin ? A5X_WF_BIN : 0u))) | A5X_WF_FAST | (PL.ng << 10) |
               (PL.ne << 16) | (PL.np << 24);
   } else {
     // the slow kernel re-derives the word (radix or DP walk); clusters need its DP
-    C.flags = clusters ? 0u : (A5X_WF_RADIX | (bin ? A5X_WF_BIN : 0u));
+    C.flags = A.clusters ? 0u : (A5X_WF_RADIX | (A.bin ? A5X_WF_BIN : 0u));
   }
   return C;
+}
+
+// One walk over the units: counts and the piece plan (count mode) together.
+template <class W>
+A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx, u32 ringmax) {
+  if (mx < 1 || L == 0) {  // processWord emits nothing
+    WordClass C;
+    C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
+    C.flags = A5X_WF_RADIX | A5X_WF_FAST;
+    return C;
+  }
+  CountAcc A;
+  count_init(A, L);
+  NullSink ns;
+  Planner<false, W, NullSink> pl(wd, T, ns);
+  u32 p = 0;
+  Unit U;
+  while (next_unit(wd, L, p, T, U)) {
+    count_unit(A, U);
+    if (!A.ok) break;
+    pl.unit(U);
+  }
+  pl.finish(L);
+  return classify_finish(A, pl.P, L, mn, mx, ringmax);
 }
 
 // ---------------------------------------------------------------------------
