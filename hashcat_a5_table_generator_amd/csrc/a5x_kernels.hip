@@ -1138,13 +1138,15 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 //           instruction, consecutive lanes consecutive addresses).
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
-#define FX_RING 2048  // per-wave linear output staging (bytes), then 4 trash dwords per lane
+#define FX_RING 4096  // per-wave linear output staging (bytes), then 4 trash dwords per lane;
+                      // its upper half also holds the window's small records during setup
 #define FX_WW 32      // window words
 #define FX_NBE 256    // big entries per window (16 B each); [FX_ZBE] is the empty piece
 #define FX_ZBE (FX_NBE - 1)
 
+// The window's small-piece records live in the ring's upper half during the window
+// setup (rec[FX_ZSLOT] = 0); the rounds then reuse those bytes as output staging.
 struct FXWin {
-  u64 rec[FX_WREC];        // the window's small-piece records; rec[FX_ZSLOT] = 0
   uint4 be[FX_NBE];        // big entries: 15 content bytes, length in byte 15
   // per word j, big piece b: {magic, (R - 1) | base << 8 | x << 16} at wi[j][b / 2].{xy|zw};
   // x of piece 0 = bits 0-15 of the word's first candidate c0, x of piece 1 = c0
@@ -1228,46 +1230,54 @@ __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) 
   R.open = false;
 }
 
-// Rounds of <= nl consecutive candidates [g, gend) of the window's k words; NB >=
-// every word's big piece count.
-template <int NB>
+// Rounds of <= K nl consecutive candidates [g, gend) of the window's k words: lane
+// L takes candidates K L .. K L + K - 1 of the round (one contiguous output run);
+// NB >= every word's big piece count.
+template <int NB, int K>
 __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, const ExpArgs& a, FxRun& R, u64 g, u64 gend, u32 k,
                                           u32 nl, u32 c0rel) {
   const u32 lane = lane_id();
   const u32 T = FX_RING / 4 + 4u * lane;  // the lane's 4 trash dwords
   u32 jcur = 0;  // word holding the round's first candidate (uniform)
-  for (u64 rr = g; rr < gend; rr += nl) {
+  for (u64 rr = g; rr < gend; rr += (u64)K * nl) {
     const u32 rrel = (u32)(rr - g);
-    const u32 nact = uniform((u32)min((u64)nl, gend - rr));
-    // word of each lane's candidate: count the word starts it has passed
-    u32 lo = jcur;
+    const u32 ncand = uniform((u32)min((u64)K * nl, gend - rr));
+    const u32 nact = (ncand + K - 1) / K;  // lanes with at least one candidate
+    // word of each candidate: count the word starts it has passed
+    u32 lo[K];
+#pragma unroll
+    for (int c = 0; c < K; c++) lo[c] = jcur;
     for (;;) {
       const u32 jn = uniform(jcur + 1);
       if (jn >= k) break;
       const u32 sj = uniform(readlane_u32(c0rel, jn));
-      if (sj >= rrel + nact) break;
+      if (sj >= rrel + ncand) break;
       jcur = jn;
-      lo += (rrel + lane >= sj) ? 1u : 0u;
+#pragma unroll
+      for (int c = 0; c < K; c++) lo[c] += (rrel + K * lane + c >= sj) ? 1u : 0u;
     }
-    const uint4 b01 = F.wi[lo][0];
-    const uint4 b23 = NB > 2 ? F.wi[lo][1] : make_uint4(0, 0, 0, 0);
-    const u32 wc = (b01.y >> 16) | (((b01.w >> 16) & 255u) << 16);
-    const u32 nb = lane < nact ? (b01.w >> 24) & 7u : 0u;
     // pass 1: big piece digits of n = rank + 1 -> entries, length
-    u32 n = (((u32)rr + lane - wc) & 0xFFFFFFu) + 1u;
-    uint4 e[NB];
+    uint4 e[K][NB];
     u32 len = 0;
 #pragma unroll
-    for (int b = 0; b < NB; b++) {
-      const u32 magic = b == 0 ? b01.x : b == 1 ? b01.z : b == 2 ? b23.x : b23.z;
-      const u32 rb = b == 0 ? b01.y : b == 1 ? b01.w : b == 2 ? b23.y : b23.w;
-      const u32 rm1 = rb & 63u;
-      const u32 q = rm1 ? __umulhi(n, magic) : n;  // R = 1: digit 0
-      const u32 d = n - __umul24(q, rm1 + 1u);
-      n = q;
-      const u32 idx = (u32)b < nb ? ((rb >> 8) & 255u) + d : (u32)FX_ZBE;
-      e[b] = F.be[idx];
-      len += e[b].w >> 24;
+    for (int c = 0; c < K; c++) {
+      const uint4 b01 = F.wi[lo[c]][0];
+      const uint4 b23 = NB > 2 ? F.wi[lo[c]][1] : make_uint4(0, 0, 0, 0);
+      const u32 wc = (b01.y >> 16) | (((b01.w >> 16) & 255u) << 16);
+      const u32 nb = K * lane + c < ncand ? (b01.w >> 24) & 7u : 0u;
+      u32 n = (((u32)rr + K * lane + c - wc) & 0xFFFFFFu) + 1u;
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        const u32 magic = b == 0 ? b01.x : b == 1 ? b01.z : b == 2 ? b23.x : b23.z;
+        const u32 rb = b == 0 ? b01.y : b == 1 ? b01.w : b == 2 ? b23.y : b23.w;
+        const u32 rm1 = rb & 63u;
+        const u32 q = rm1 ? __umulhi(n, magic) : n;  // R = 1: digit 0
+        const u32 d = n - __umul24(q, rm1 + 1u);
+        n = q;
+        const u32 idx = (u32)b < nb ? ((rb >> 8) & 255u) + d : (u32)FX_ZBE;
+        e[c][b] = F.be[idx];
+        len += e[c][b].w >> 24;
+      }
     }
     const u32 incl = wave_incl_scan_u32(len);
     const u32 tot = lane63(incl);
@@ -1278,9 +1288,12 @@ __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, const ExpArgs& a,
     bool hp = lane != 0 && pn != 0;
     if (!(a.ablate & 2u)) {
 #pragma unroll
-      for (int b = 0; b < NB; b++) {
-        const u32 ev[4] = {e[b].x, e[b].y, e[b].z, e[b].w};
-        fb_put(ev, pv, pn, D, hp, hd, acc, ring, T);
+      for (int c = 0; c < K; c++) {
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+          const u32 ev[4] = {e[c][b].x, e[c][b].y, e[c][b].z, e[c][b].w};
+          fb_put(ev, pv, pn, D, hp, hd, acc, ring, T);
+        }
       }
     }
     const u32 hnext = (u32)__shfl_down((int)hd, 1);
@@ -1315,6 +1328,7 @@ __device__ __forceinline__ FxMeta fx_meta(const ExpArgs& a, u64 w) {
 
 __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
+  u64* const rec = (u64*)(ring + FX_RING / 8);  // ring bytes [FX_RING / 2, FX_RING)
   const u64 g0 = max(a.cand_begin, chunk * a.CH);
   const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
   if (g0 >= g1) return;
@@ -1322,7 +1336,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
   if (w >= a.nw) { guard_trip(a, 2, chunk, w, g0, a.nw); return; }
   while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
   if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
-  if (lane == 0) { F.rec[FX_ZSLOT] = 0; F.be[FX_ZBE] = make_uint4(0, 0, 0, 0); }
+  if (lane == 0) F.be[FX_ZBE] = make_uint4(0, 0, 0, 0);
   u64 g = g0;
   FxRun R;
   R.open = false; R.B = 0; R.lo = 0; R.pos = 0; R.carry = 0;
@@ -1369,34 +1383,35 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     const u64 src0 = (u64)readlane_u32(M.roff, jf);
     const u32 ntot = readlane_u32(incR, k - 1);
     if (pfb <= src0 && src0 + ntot <= pfb + FX_PF) {
-      const u32 d = (u32)(src0 - pfb);  // 0 .. : the prefetched u64 i lands at F.rec[i - d]
+      const u32 d = (u32)(src0 - pfb);  // 0 .. : the prefetched u64 i lands at rec[i - d]
       const u32 i0 = 2 * lane, i1 = 2 * (lane + 64);
-      if (i0 >= d) F.rec[i0 - d] = ((u64)pf0.y << 32) | pf0.x;
-      if (i0 + 1 >= d) F.rec[i0 + 1 - d] = ((u64)pf0.w << 32) | pf0.z;
-      if (i1 - d < FX_ZSLOT) F.rec[i1 - d] = ((u64)pf1.y << 32) | pf1.x;
-      if (i1 + 1 - d < FX_ZSLOT) F.rec[i1 + 1 - d] = ((u64)pf1.w << 32) | pf1.z;
+      if (i0 >= d) rec[i0 - d] = ((u64)pf0.y << 32) | pf0.x;
+      if (i0 + 1 >= d) rec[i0 + 1 - d] = ((u64)pf0.w << 32) | pf0.z;
+      if (i1 - d < FX_ZSLOT) rec[i1 - d] = ((u64)pf1.y << 32) | pf1.x;
+      if (i1 + 1 - d < FX_ZSLOT) rec[i1 + 1 - d] = ((u64)pf1.w << 32) | pf1.z;
     } else {
       const u64* s64 = a.rec + src0;
       if ((src0 & 1) == 0) {
         const uint4* src = (const uint4*)s64;
-        for (u32 i = lane; i < (ntot + 1) / 2; i += 64) ((uint4*)F.rec)[i] = src[i];
+        for (u32 i = lane; i < (ntot + 1) / 2; i += 64) ((uint4*)rec)[i] = src[i];
       } else {
-        for (u32 i = lane; i < ntot; i += 64) F.rec[i] = s64[i];
+        for (u32 i = lane; i < ntot; i += 64) rec[i] = s64[i];
       }
     }
     const u32 rb = incR - rs;
     const u64 bo = M.bo;
+    if (lane == 0) rec[FX_ZSLOT] = 0;
     WAVE_SYNC();
     // ---- big pieces per word: R = product of the spanned small R ----
     u64 hdr = 0;
     u32 nbw = 0, R0 = 1, R1 = 1, R2 = 1, R3 = 1;
     if (lane < k && rs) {
-      hdr = F.rec[rb];
+      hdr = rec[rb];
       nbw = frh_nbig(hdr);
-      R0 = fb_R(F.rec, rb, hdr, 0);
-      R1 = fb_R(F.rec, rb, hdr, 1);
-      R2 = fb_R(F.rec, rb, hdr, 2);
-      R3 = fb_R(F.rec, rb, hdr, 3);
+      R0 = fb_R(rec, rb, hdr, 0);
+      R1 = fb_R(rec, rb, hdr, 1);
+      R2 = fb_R(rec, rb, hdr, 2);
+      R3 = fb_R(rec, rb, hdr, 3);
     }
     const u32 E = R0 + R1 + R2 + R3 - (FB_NMAX - nbw);  // fb_R = 1 past the last big piece
     const u32 incE = wave_incl_scan_u32(E);
@@ -1458,7 +1473,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
           if (nbj > 2 && u >= s2) { b = 2; cb = s2; }
           if (nbj > 3 && u >= s3) { b = 3; cb = s3; }
           u32 ent[4];
-          fb_entry(F.rec, wrb, b, u - cb, ent);
+          fb_entry(rec, wrb, b, u - cb, ent);
           F.be[t] = make_uint4(ent[0], ent[1], ent[2], ent[3]);
         }
       }
@@ -1469,7 +1484,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     const u64 wc0 = uniform64(c0);
     const u64 r0 = g - wc0;
     u64 pos = uniform64(bo) - a.out_base;
-    if (r0) pos += fast_prefix_bytes(F.rec + readlane_u32(rb, 0), r0);
+    if (r0) pos += fast_prefix_bytes(rec + readlane_u32(rb, 0), r0);
     if (!R.open || R.pos != pos) {
       fx_close(R, ring, a);
       R.B = pos & ~15ull; R.lo = pos; R.pos = pos; R.carry = 0; R.open = true;
@@ -1477,10 +1492,14 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     STAMP(2);
     // ---- rounds ----
     const u64 gend = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
-    const u32 nl = uniform(min(64u, (FX_RING - 32) / max(winmax, 1u)));
     const u32 c0rel = (lane < k) ? (u32)(c0 > g ? c0 - g : 0) : 0xffffffffu;
-    if (nbmax <= 2) fx_rounds<2>(F, ring, a, R, g, gend, k, nl, c0rel);
-    else fx_rounds<FB_NMAX>(F, ring, a, R, g, gend, k, nl, c0rel);
+    if (nbmax <= 2) {
+      const u32 nl = uniform(min(64u, (FX_RING - 32) / max(winmax, 1u)));
+      fx_rounds<2, 1>(F, ring, a, R, g, gend, k, nl, c0rel);
+    } else {
+      const u32 nl = uniform(min(64u, (FX_RING - 32) / max(winmax, 1u)));
+      fx_rounds<FB_NMAX, 1>(F, ring, a, R, g, gend, k, nl, c0rel);
+    }
     STAMP(3);
     g = gend;
     w += k;
