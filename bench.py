@@ -213,6 +213,8 @@ def main():
                 "ms_per_launch": ms_exp,
                 "ms_per_launch_max_rank": ms_exp_max,
                 "ms_keyspace_scan_plan": ms_ks,
+                "words_slow_path": int(stats[-1]["words_slow"]),
+                "words_big_path": int(stats[-1]["words_pass_b"]),
                 "algorithmic_bytes_per_launch": tb,
             },
             "cpu_baseline": None,

@@ -41,7 +41,7 @@ class Stats(ctypes.Structure):
     _fields_ = [
         ("candidates", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("words", ctypes.c_uint64),
         ("words_pass_b", ctypes.c_uint64), ("ms_keyspace", ctypes.c_double), ("ms_expand", ctypes.c_double),
-        ("ms_total", ctypes.c_double), ("expand_launches", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+        ("ms_total", ctypes.c_double), ("expand_launches", ctypes.c_uint32), ("words_slow", ctypes.c_uint32),
     ]
 
     def as_dict(self) -> dict:

@@ -82,9 +82,10 @@ struct a5x_ctx {
   uint32_t table_bytes = 0;
 
   DevBuf<uint64_t> count, bytes, cand_off, byte_off, scan_tmp, locate;
-  DevBuf<uint32_t> flags, defer, chunk_w0, chunk_kind, roff, cplx;
+  DevBuf<uint32_t> flags, defer, chunk_w0, slow_list, big_list, roff, cplx;
+  DevBuf<uint64_t> segs;  // slow / BIG segment items
   DevBuf<uint64_t> rec;  // FAST plan records (keyspace tiles of FW_TILE_REC u64)
-  uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] nslow, [16..31] guard record
+  uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] nslow, [4] cplx_n, [5] slow segs, [6] BIG segs, [16..31] guard record
   uint32_t* h_scalars = nullptr;  // pinned
   uint64_t* h_totals = nullptr;   // pinned [0] cands [1] bytes [2..3] locate
 
@@ -95,7 +96,8 @@ struct a5x_ctx {
   size_t h_out_cap = 0;
 
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint64_t chunk = 32768;     // candidates per expand wave
+  uint64_t seg = 1024;        // candidates per per-word-path segment (a radix round there costs ~64x a FAST one)
+  uint64_t chunk = 8192;      // candidates per expand wave (sweep on C3: 8192 < 16384 < 32768 ms)
   uint32_t waves_per_block = 4;
   uint32_t ablate = 0;        // A5X_ABLATE (timing experiments only)
 };
@@ -341,6 +343,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
       (rc = grow(c, c->defer, nw + 1)) || (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)) ||
       (rc = grow(c, c->roff, nw + 1)) || (rc = grow(c, c->cplx, nw + 1)) ||
+      (rc = grow(c, c->slow_list, nw + 1)) || (rc = grow(c, c->big_list, nw + 1)) ||
       (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC +
                                 (uint64_t)ks_cplx_cap(nw) * FW_RMAX + 2)))
     return rc;
@@ -360,6 +363,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
     K.mn = mn; K.mx = mx; K.count = c->count.p; K.bytes = c->bytes.p; K.flags = c->flags.p;
     K.defer_list = c->defer.p; K.defer_n = c->d_scalars; K.nbig = c->d_scalars + 1; K.err = c->d_scalars + 2;
     K.nslow = c->d_scalars + 3;
+    K.slow_list = c->slow_list.p; K.big_list = c->big_list.p;
     K.rec = c->rec.p; K.roff = c->roff.p;
     K.cplx_list = c->cplx.p; K.cplx_n = c->d_scalars + 4; K.cplx_cap = ks_cplx_cap(nw);
     K.cplx_base = ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC;
@@ -410,7 +414,7 @@ A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   memset(&E, 0, sizeof E);
   E.table = c->d_table; E.table_bytes = c->table_bytes; E.words = d_words; E.woff = d_woff; E.nw = nw;
   E.cand_off = B.cand_off; E.byte_off = B.byte_off; E.flags = c->flags.p; E.chunk_w0 = c->chunk_w0.p;
-  E.chunk_kind = c->chunk_kind.p; E.CH = c->chunk; E.mn = mn; E.mx = mx; E.err = c->d_scalars + 2;
+  E.CH = c->chunk; E.SEG = c->seg; E.mn = mn; E.mx = mx; E.err = c->d_scalars + 2;
   E.dbg = (uint64_t*)(c->d_scalars + 16);
   E.waves_per_block = c->waves_per_block;
   E.rec = c->rec.p; E.roff = c->roff.p; E.rec_n = c->rec.cap;
@@ -460,6 +464,7 @@ int a5x_create(int device, a5x_ctx** out) {
     return A5X_E_HIP;
   }
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
+  if (const char* e = getenv("A5X_SEG")) c->seg = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_ABLATE")) c->ablate = (uint32_t)atoi(e);
   if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   *out = c;
@@ -472,7 +477,8 @@ void a5x_destroy(a5x_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   release(c->count); release(c->bytes); release(c->cand_off); release(c->byte_off); release(c->scan_tmp);
-  release(c->locate); release(c->flags); release(c->defer); release(c->chunk_w0); release(c->chunk_kind);
+  release(c->locate); release(c->flags); release(c->defer); release(c->chunk_w0); release(c->slow_list); release(c->big_list);
+  release(c->segs);
   release(c->s_words); release(c->s_out); release(c->s_woff);
   if (c->d_table) (void)hipFree(c->d_table);
   if (c->d_scalars) (void)hipFree(c->d_scalars);
@@ -658,16 +664,36 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   E.out_base = b0;
   E.out_cap = out_cap;
   const uint64_t nchunks = (B.total_cands + c->chunk - 1) / c->chunk;
-  if ((rc = grow(c, c->chunk_w0, nchunks + 1)) || (rc = grow(c, c->chunk_kind, nchunks + 1))) return rc;
+  if ((rc = grow(c, c->chunk_w0, nchunks + 1))) return rc;
   E.chunk_w0 = c->chunk_w0.p;
-  E.chunk_kind = c->chunk_kind.p;
-  const bool other = B.nbig || B.nslow;
-  if (other) HIPCHK(c, hipMemsetAsync(c->chunk_kind.p, 0, (nchunks + 1) * 4, st));
-  HIPCHK(c, a5x_launch_plan(B.cand_off, c->flags.p, nw, c->chunk, c->chunk_w0.p, c->chunk_kind.p, st));
+  // slow / BIG words: (word, CH-candidate segment) items, slow from segs[0], BIG
+  // from segs[sbound]; a word adds at most ceil(range / CH) + 1 segments
+  const uint64_t rng_segs = (ce - cb) / c->seg + 1;
+  const uint64_t sbound = B.nslow ? B.nslow + rng_segs : 0;
+  const uint64_t bbound = B.nbig ? B.nbig + rng_segs : 0;
+  if (sbound + bbound > 0xffffffffull)
+    return fail(c, A5X_E_CAPACITY, "call range needs more than 2^32 slow-path segments (lower A5X_CHUNK range)");
+  if (B.nslow || B.nbig) {
+    if ((rc = grow(c, c->segs, sbound + bbound + 1))) return rc;
+    HIPCHK(c, hipMemsetAsync(c->d_scalars + 5, 0, 8, st));
+  }
+  if (B.nslow)
+    HIPCHK(c, a5x_launch_segments(c->slow_list.p, c->d_scalars + 3, B.nslow, B.cand_off, cb, ce, c->seg,
+                                  c->segs.p, c->d_scalars + 5, st));
+  if (B.nbig)
+    HIPCHK(c, a5x_launch_segments(c->big_list.p, c->d_scalars + 1, B.nbig, B.cand_off, cb, ce, c->seg,
+                                  c->segs.p + sbound, c->d_scalars + 6, st));
+  HIPCHK(c, a5x_launch_plan(B.cand_off, nw, c->chunk, c->chunk_w0.p, st));
   HIPCHK(c, hipEventRecord(c->ev[1], st));
   HIPCHK(c, a5x_launch_expand(E, 0, st));
-  if (B.nslow) HIPCHK(c, a5x_launch_expand(E, 1, st));
-  if (B.nbig) HIPCHK(c, a5x_launch_expand(E, 2, st));
+  if (B.nslow) {
+    E.segs = c->segs.p; E.nsegs = c->d_scalars + 5; E.nsegs_bound = sbound;
+    HIPCHK(c, a5x_launch_expand(E, 1, st));
+  }
+  if (B.nbig) {
+    E.segs = c->segs.p + sbound; E.nsegs = c->d_scalars + 6; E.nsegs_bound = bbound;
+    HIPCHK(c, a5x_launch_expand(E, 2, st));
+  }
   HIPCHK(c, hipEventRecord(c->ev[2], st));
   HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
@@ -682,7 +708,7 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     stats->ms_total = t;
     stats->words_pass_b = B.nbig;
     stats->expand_launches = 1 + (B.nslow ? 1 : 0) + (B.nbig ? 1 : 0);
-    stats->pad = 0;
+    stats->words_slow = B.nslow;
   }
   return A5X_OK;
 }
@@ -799,7 +825,7 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   const Tab T = tab_view(c->blob.data());
   const WordClass C = classify_word(gw, (u32)len, T, mn, mx, A5X_RING_A - 16);
   info[0] = C.count; info[1] = C.bytes; info[2] = C.flags;
-  if (!(C.flags & A5X_WF_FAST) || C.count == 0) return A5X_OK;
+  if (!(C.flags & A5X_WF_FAST) || C.count == 0 || !out) return A5X_OK;  // no out: classification only
   // the record exactly as k_keyspace_thread builds it, placed as a one-word window
   std::vector<u64> wrec(FX_WREC + FW_PMAX + 16, 0);
   ArraySink sk;

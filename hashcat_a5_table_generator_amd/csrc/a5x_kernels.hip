@@ -155,6 +155,8 @@ struct KsArgs {
   u32* defer_n;
   u32* nbig;
   u32* nslow;
+  u32* big_list;   // words for k_expand_b (index = *nbig at append)
+  u32* slow_list;  // words for k_expand_slow (index = *nslow at append)
   u32* err;
   u64* rec;     // FAST plan records: tile t owns rec[t * FW_TILE_REC, (t + 1) * FW_TILE_REC)
   u32* roff;    // per word: record offset (u64 units) into rec
@@ -176,12 +178,19 @@ __device__ __forceinline__ u32 wave_append(bool pred, u32* ctr) {
   return base + (u32)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-// The open group of plan_word lives in LDS (FW_UMAXR u64 per lane, lane-strided);
+// k_keyspace_thread's open group holds KS_GCAP entries (a unit with more choices
+// makes the word complex: k_keyspace_cplx plans it with FW_UMAXR)
+#define KS_GCAP 8
+
+// The open group of plan_word lives in LDS (<= FW_UMAXR u64 per lane, lane-strided);
 // entries and group descriptors go straight to the word's record in HBM.
 struct DevRecSink {
   u64* g;       // LDS: g[a * 256]
+  u64* c;       // LDS: cluster choices c[a * 256] (k_keyspace_cplx only)
   u64* rec;     // global record base
   u32 np;
+  __device__ u64* cbuf() const { return c; }
+  __device__ u32 cstride() const { return 256u; }
   __device__ u64 gld(u32 a) const { return g[a * 256u]; }
   __device__ void gst(u32 a, u64 v) { g[a * 256u] = v; }
   __device__ void ent(u32 i, u64 v) { rec[1 + np + i] = v; }
@@ -215,7 +224,7 @@ __device__ __forceinline__ u32 ks_classify(const W& wd, u64 L64, const Tab& T, c
 template <class W>
 __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const KsArgs& a, u32 f, u64* rec, u64* g) {
   DevRecSink sk;
-  sk.g = g; sk.rec = rec; sk.np = ff_np(f);
+  sk.g = g; sk.c = g + 256 * FW_UMAXR; sk.rec = rec; sk.np = ff_np(f);
   const Plan P = plan_word<true>(wd, L, T, sk);
   rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl, P.nbig, P.bstarts);
   if (!P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
@@ -260,9 +269,13 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
       } else if (nm == 1 && !cplx) {
         Unit U;
         lone_unit(T, q, kk, U);
-        if (COUNT) count_unit(A, U);
-        pl.unit(U);
-        cur_end = U.e;
+        if (U.R > KS_GCAP) {
+          cplx = true;
+        } else {
+          if (COUNT) count_unit(A, U);
+          pl.unit(U);
+          cur_end = U.e;
+        }
       }
     }
   }
@@ -276,9 +289,9 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
 __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 tb = (a.table_bytes + 15u) & ~15u;
-  u64* gbuf = (u64*)(smem + tb);                        // 256 x FW_UMAXR open-group entries
-  u32* wsum = (u32*)(smem + tb + 256 * FW_UMAXR * 8);   // per-wave sums of the scan
-  uint8_t* wb = smem + tb + 256 * FW_UMAXR * 8 + 64;    // KS_WB + 32 tile bytes
+  u64* gbuf = (u64*)(smem + tb);                       // 256 x KS_GCAP open-group entries
+  u32* wsum = (u32*)(smem + tb + 256 * KS_GCAP * 8);   // per-wave sums of the scan
+  uint8_t* wb = smem + tb + 256 * KS_GCAP * 8 + 64;    // KS_WB + 32 tile bytes
   load_table(smem, a.table, a.table_bytes);
   __syncthreads();
   const Tab T = tab_view(smem);
@@ -323,7 +336,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     CountAcc A;
     count_init(A, L);
     NullSink ns;
-    Planner<false, LWord, NullSink> pl(lw, T, ns);
+    Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
     psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx);
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
@@ -351,8 +364,8 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     {
       u64* rec = a.rec + tile * FW_TILE_REC + ro;
       DevRecSink sk;
-      sk.g = gbuf + tid; sk.rec = rec; sk.np = ff_np(f);
-      Planner<true, LWord, DevRecSink> pb(lw, T, sk);
+      sk.g = gbuf + tid; sk.c = sk.g; sk.rec = rec; sk.np = ff_np(f);  // no clusters here
+      Planner<true, LWord, DevRecSink, KS_GCAP> pb(lw, T, sk);
       CountAcc A2;
       bool c2 = false;
       psk_walk<false>(lw, L, build, wave_max_u32(build ? L : 0u), bmax, T, pb, A2, c2);
@@ -375,7 +388,8 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     const u32 di = wave_append(dfr, a.defer_n);
     if (dfr) a.defer_list[di] = (u32)w;
     const bool slow = valid && !cplx && !(f & (A5X_WF_DEFER | A5X_WF_FAST | A5X_WF_ERR_OVF));
-    wave_append(slow, a.nslow);
+    const u32 si = wave_append(slow, a.nslow);
+    if (slow) a.slow_list[si] = (u32)w;
     if (valid && !cplx) {
       a.count[w] = (f & A5X_WF_DEFER) ? 0 : C.count;
       a.bytes[w] = (f & A5X_WF_DEFER) ? 0 : C.bytes;
@@ -414,7 +428,7 @@ __global__ void __launch_bounds__(256) k_keyspace_cplx(KsArgs a) {
       }
     }
     if (f & A5X_WF_DEFER) a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
-    else if (!(f & (A5X_WF_FAST | A5X_WF_ERR_OVF))) atomicAdd(a.nslow, 1u);
+    else if (!(f & (A5X_WF_FAST | A5X_WF_ERR_OVF))) a.slow_list[atomicAdd(a.nslow, 1u)] = (u32)w;
     a.count[w] = (f & A5X_WF_DEFER) ? 0 : C.count;
     a.bytes[w] = (f & A5X_WF_DEFER) ? 0 : C.bytes;
     a.flags[w] = f;
@@ -676,8 +690,8 @@ __global__ void __launch_bounds__(64) k_keyspace_wave(KsArgs a) {
       // would pass A (smaller LDS budget) handle it?
       bool fitsA = I.L <= A5X_LMAX_A && I.nmatch <= A5X_MLMAX_A && I.maxlen <= A5X_RING_A - 16 &&
                    (I.cls != A5X_WF_GENERAL || (u64)(I.nev + 1) * I.W <= A5X_DPENT_A);
-      if (I.cls && !fitsA) { f |= A5X_WF_BIG; atomicAdd(a.nbig, 1u); }
-      else if (I.cls) atomicAdd(a.nslow, 1u);
+      if (I.cls && !fitsA) { f |= A5X_WF_BIG; a.big_list[atomicAdd(a.nbig, 1u)] = w; }
+      else if (I.cls) a.slow_list[atomicAdd(a.nslow, 1u)] = w;
       if (I.cls && (!I.fits || I.maxlen > A5X_RING_B - 16)) {
         f |= A5X_WF_ERR_BIG | ((I.fits ? 5u : I.why) << 16) | (min(I.W, 255u) << 24);
         atomicOr(a.err, A5X_DERR_BIG);
@@ -777,19 +791,38 @@ __global__ void __launch_bounds__(SCAN_BLOCK) k_scan_down(const u64* ca, const u
 // ---------------------------------------------------------------------------
 // Chunk planner: chunk c covers global candidates [c*CH, (c+1)*CH)
 // ---------------------------------------------------------------------------
-// chunk_kind[c] bit 0: the chunk holds candidates of a slow (non-FAST) word,
-// bit 1: of a BIG word.  Only written when such words exist (host zeroes it).
-__global__ void __launch_bounds__(256) k_plan(const u64* cand_off, const u32* flags, u64 nw, u64 CH, u32* chunk_w0,
-                                              u32* chunk_kind) {
+__global__ void __launch_bounds__(256) k_plan(const u64* cand_off, u64 nw, u64 CH, u32* chunk_w0) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
     const u64 a = cand_off[w], b = cand_off[w + 1];
     if (b <= a) continue;
     for (u64 c = (a + CH - 1) / CH; c * CH < b; c++) chunk_w0[c] = (u32)w;
-    const u32 f = flags[w];
-    const u32 kind = (f & A5X_WF_BIG) ? 2u : ((f & A5X_WF_FAST) ? 0u : 1u);
-    if (kind)
-      for (u64 c = a / CH; c * CH < b; c++) atomicOr(&chunk_kind[c], kind);
+  }
+}
+
+// Segments of the listed (slow or BIG) words: word w's candidates inside the call's
+// range [cb, ce), cut into pieces of CH; item = w | s << 32 (order is irrelevant).
+__global__ void __launch_bounds__(256) k_segments(const u32* list, const u32* list_n, const u64* cand_off, u64 cb,
+                                                  u64 ce, u64 CH, u64* segs, u32* nsegs) {
+  const u32 n = *list_n;
+  const u32 stride = gridDim.x * blockDim.x;
+  const u32 i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  for (u32 ib = i0 - lane_id(); ib < n; ib += stride) {  // whole waves (wave_append)
+    const u32 i = ib + lane_id();
+    u64 k = 0;
+    u32 w = 0;
+    if (i < n) {
+      w = list[i];
+      const u64 lo = max(cb, cand_off[w]), hi = min(ce, cand_off[w + 1]);
+      k = hi > lo ? (hi - lo + CH - 1) / CH : 0;
+    }
+    // per-wave base: exclusive scan of k (k < 2^32 since a word has < 2^32 candidates)
+    const u32 incl = wave_incl_scan_u32((u32)k);
+    u32 base = 0;
+    if (lane_id() == 63 && incl) base = atomicAdd(nsegs, incl);
+    base = readlane_u32(base, 63);
+    const u32 o = base + incl - (u32)k;
+    for (u64 t = 0; t < k; t++) segs[o + t] = (u64)w | (t << 32);
   }
 }
 
@@ -806,9 +839,11 @@ struct ExpArgs {
   const u64* byte_off;   // n+1, exclusive prefix of bytes
   const u32* flags;
   const u32* chunk_w0;
-  const u32* chunk_kind;
+  const u64* segs;       // k_expand_slow / k_expand_b work items (k_segments)
+  const u32* nsegs;
   u64 cand_begin, cand_end;  // global candidate range of this call
   u64 CH;
+  u64 SEG;               // candidates per k_segments item
   uint8_t* out;
   u64 out_base;          // byte_off value that maps to out[0]
   u64 out_cap;           // bytes writable at out
@@ -1524,36 +1559,19 @@ __global__ void __launch_bounds__(256) k_expand_fast(ExpArgs a) {
   expand_chunk_fast(F, ring, a, chunk);
 }
 
-// k_expand_slow: non-FAST, non-BIG words (overlapping keys, capped windows,
-// fanout > 3, ...) one word at a time through wave_setup; everything else is a hole.
+// k_expand_slow / k_expand_b: one k_segments item (a slow or BIG word's run of <= CH
+// candidates inside the call's range) per wave, through wave_setup.
 template <int LMAX, int MLMAX, int DPENT, u32 RING>
-__device__ void expand_chunk_kind(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab& T, const ExpArgs& a,
-                                  u64 chunk, bool bigpass) {
-  const u64 g0 = max(a.cand_begin, chunk * a.CH);
-  const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
-  if (g0 >= g1) return;
-  u64 w = a.chunk_w0[chunk];
-  if (w >= a.nw) { guard_trip(a, 2, chunk, w, g0, a.nw); return; }
-  while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
-  if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
-  u64 r = g0 - a.cand_off[w];
-  u64 g = g0;
+__device__ void expand_segment(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab& T, const ExpArgs& a, u64 item) {
+  const u64 w = (u32)item, s = item >> 32;
+  if (w >= a.nw) { guard_trip(a, 2, item, w, s, a.nw); return; }
+  const u64 c0 = a.cand_off[w], c1 = a.cand_off[w + 1];
+  const u64 lo = max(a.cand_begin, c0) + s * a.SEG;
+  const u64 hi = min(min(a.cand_end, c1), lo + a.SEG);
+  if (lo >= hi) { guard_trip(a, 3, item, w, lo, hi); return; }
   Run R;
   R.open = false;
-  while (g < g1) {
-    if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
-    const u64 cnt = a.cand_off[w + 1] - a.cand_off[w];
-    if (cnt == 0) { w++; continue; }
-    const u64 nhere = min(cnt - r, g1 - g);
-    const u32 fl = a.flags[w];
-    const bool mine = bigpass ? (fl & A5X_WF_BIG) != 0 : !(fl & (A5X_WF_BIG | A5X_WF_FAST));
-    if (!mine) {
-      run_close<RING>(R, ring, a);
-    } else if (!expand_word<LMAX, MLMAX, DPENT, RING>(S, ring, T, a, R, w, r, nhere, cnt)) {
-      break;
-    }
-    g += nhere; w++; r = 0;
-  }
+  expand_word<LMAX, MLMAX, DPENT, RING>(S, ring, T, a, R, w, lo - c0, hi - lo, c1 - c0);
   run_close<RING>(R, ring, a);
 }
 
@@ -1570,10 +1588,9 @@ __global__ void __launch_bounds__(256) k_expand_slow(ExpArgs a) {
   for (u32 i = lane_id(); i < A5X_RING_A / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   const Tab T = tab_view(smem);
-  const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
-  if (chunk * a.CH >= a.cand_end) return;
-  if (!(a.chunk_kind[chunk] & 1u)) return;
-  expand_chunk_kind<A5X_LMAX_A, A5X_MLMAX_A, A5X_DPENT_A, A5X_RING_A>(S, ring, T, a, chunk, false);
+  const u32 n = *a.nsegs;
+  for (u32 i = blockIdx.x * nwv + wv; i < n; i += gridDim.x * nwv)
+    expand_segment<A5X_LMAX_A, A5X_MLMAX_A, A5X_DPENT_A, A5X_RING_A>(S, ring, T, a, a.segs[i]);
 }
 
 __global__ void __launch_bounds__(64) k_expand_b(ExpArgs a) {
@@ -1585,10 +1602,9 @@ __global__ void __launch_bounds__(64) k_expand_b(ExpArgs a) {
   for (u32 i = lane_id(); i < A5X_RING_B / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   const Tab T = tab_view(smem);
-  const u64 chunk = a.cand_begin / a.CH + blockIdx.x;
-  if (chunk * a.CH >= a.cand_end) return;
-  if (!(a.chunk_kind[chunk] & 2u)) return;
-  expand_chunk_kind<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B, A5X_RING_B>(S, ring, T, a, chunk, true);
+  const u32 n = *a.nsegs;
+  for (u32 i = blockIdx.x; i < n; i += gridDim.x)
+    expand_segment<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B, A5X_RING_B>(S, ring, T, a, a.segs[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1676,12 +1692,13 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
   a.mn = L.mn; a.mx = L.mx; a.count = L.count; a.bytes = L.bytes; a.flags = L.flags;
   a.defer_list = L.defer_list; a.defer_n = L.defer_n; a.nbig = L.nbig; a.nslow = L.nslow; a.err = L.err;
+  a.big_list = L.big_list; a.slow_list = L.slow_list;
   a.rec = L.rec; a.roff = L.roff;
   a.cplx_list = L.cplx_list; a.cplx_n = L.cplx_n; a.cplx_cap = L.cplx_cap; a.cplx_base = L.cplx_base;
   hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_keyspace_cplx, dim3(L.defer_blocks), dim3(256), ((L.table_bytes + 15u) & ~15u) + 256 * FW_UMAXR * 8, st, a);
+  hipLaunchKernelGGL(k_keyspace_cplx, dim3(L.defer_blocks), dim3(256), ((L.table_bytes + 15u) & ~15u) + 2 * 256 * FW_UMAXR * 8, st, a);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t lds = ((L.table_bytes + 15u) & ~15u) + sizeof(LdsB);
@@ -1690,7 +1707,7 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
 }
 
 size_t a5x_keyspace_thread_lds(u32 table_bytes) {
-  return ((table_bytes + 15u) & ~15u) + FW_TILE * FW_UMAXR * 8 + 64 + KS_WB + 32;
+  return ((table_bytes + 15u) & ~15u) + FW_TILE * KS_GCAP * 8 + 64 + KS_WB + 32;
 }
 
 size_t a5x_keyspace_wave_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + sizeof(LdsB); }
@@ -1723,10 +1740,15 @@ hipError_t a5x_launch_scan(const u64* ca, const u64* cb, u64 n, u64* outa, u64* 
   return hipGetLastError();
 }
 
-hipError_t a5x_launch_plan(const u64* cand_off, const u32* flags, u64 nw, u64 CH, u32* chunk_w0, u32* chunk_kind,
-                           hipStream_t st) {
-  hipLaunchKernelGGL(k_plan, dim3(blocks_for(nw, 256, 65536)), dim3(256), 0, st, cand_off, flags, nw, CH, chunk_w0,
-                     chunk_kind);
+hipError_t a5x_launch_plan(const u64* cand_off, u64 nw, u64 CH, u32* chunk_w0, hipStream_t st) {
+  hipLaunchKernelGGL(k_plan, dim3(blocks_for(nw, 256, 65536)), dim3(256), 0, st, cand_off, nw, CH, chunk_w0);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_segments(const u32* list, const u32* list_n, u32 n_bound, const u64* cand_off, u64 cb, u64 ce,
+                               u64 CH, u64* segs, u32* nsegs, hipStream_t st) {
+  hipLaunchKernelGGL(k_segments, dim3(blocks_for(n_bound, 256, 4096)), dim3(256), 0, st, list, list_n, cand_off, cb,
+                     ce, CH, segs, nsegs);
   return hipGetLastError();
 }
 
@@ -1734,7 +1756,7 @@ static ExpArgs exp_args(const A5xExpLaunch& L) {
   ExpArgs a;
   a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
   a.cand_off = L.cand_off; a.byte_off = L.byte_off; a.flags = L.flags; a.chunk_w0 = L.chunk_w0;
-  a.chunk_kind = L.chunk_kind; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.out = L.out;
+  a.segs = L.segs; a.nsegs = L.nsegs; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.SEG = L.SEG; a.out = L.out;
   a.out_base = L.out_base; a.out_cap = L.out_cap; a.mn = L.mn; a.mx = L.mx; a.err = L.err; a.dbg = L.dbg;
   a.rec = L.rec; a.roff = L.roff; a.ablate = L.ablate; a.rec_n = L.rec_n;
   return a;
@@ -1758,9 +1780,11 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   if (kind == 0)
     hipLaunchKernelGGL(k_expand_fast, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);
   else if (kind == 1)
-    hipLaunchKernelGGL(k_expand_slow, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 1, waves), st, a);
+    hipLaunchKernelGGL(k_expand_slow, dim3(blocks_for(L.nsegs_bound, waves, 65536)), dim3(64 * waves),
+                       a5x_expand_lds(L.table_bytes, 1, waves), st, a);
   else
-    hipLaunchKernelGGL(k_expand_b, dim3((u32)nchunks), dim3(64), a5x_expand_lds(L.table_bytes, 2, 1), st, a);
+    hipLaunchKernelGGL(k_expand_b, dim3(blocks_for(L.nsegs_bound, 1, 65536)), dim3(64), a5x_expand_lds(L.table_bytes, 2, 1),
+                       st, a);
   return hipGetLastError();
 }
 

@@ -18,6 +18,8 @@ struct A5xKsLaunch {
   uint32_t* defer_n;
   uint32_t* nbig;
   uint32_t* nslow;
+  uint32_t* big_list;   // nw entries each
+  uint32_t* slow_list;
   uint32_t* err;
   uint32_t defer_blocks;
   uint64_t* rec;   // FAST plan records (tile regions of FW_TILE_REC u64, then complex slots)
@@ -38,9 +40,12 @@ struct A5xExpLaunch {
   const uint64_t* byte_off;
   const uint32_t* flags;
   const uint32_t* chunk_w0;
-  const uint32_t* chunk_kind;
+  const uint64_t* segs;    // k_expand_slow / k_expand_b items (a5x_launch_segments)
+  const uint32_t* nsegs;   // device count of segs
+  uint64_t nsegs_bound;    // host bound on *nsegs (grid size)
   uint64_t cand_begin, cand_end;
   uint64_t CH;
+  uint64_t SEG;  // candidates per slow / BIG segment
   uint8_t* out;
   uint64_t out_base;
   uint64_t out_cap;
@@ -62,8 +67,11 @@ size_t a5x_keyspace_thread_lds(uint32_t table_bytes);
 uint64_t a5x_scan_tmp_elems(uint64_t n);
 hipError_t a5x_launch_scan(const uint64_t* ca, const uint64_t* cb, uint64_t n, uint64_t* outa, uint64_t* outb,
                            uint64_t* tmp, uint32_t* err, hipStream_t st);
-hipError_t a5x_launch_plan(const uint64_t* cand_off, const uint32_t* flags, uint64_t nw, uint64_t CH,
-                           uint32_t* chunk_w0, uint32_t* chunk_kind, hipStream_t st);
+hipError_t a5x_launch_plan(const uint64_t* cand_off, uint64_t nw, uint64_t CH, uint32_t* chunk_w0, hipStream_t st);
+// (word, segment) items of the listed words' candidates in [cb, ce), CH per segment
+hipError_t a5x_launch_segments(const uint32_t* list, const uint32_t* list_n, uint32_t n_bound,
+                               const uint64_t* cand_off, uint64_t cb, uint64_t ce, uint64_t CH, uint64_t* segs,
+                               uint32_t* nsegs, hipStream_t st);
 size_t a5x_expand_lds(uint32_t table_bytes, int kind, uint32_t waves);
 // kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b (pass B)
 hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st);

@@ -88,7 +88,7 @@ A5X_HD u32 fastdiv_hd(u32 n, u32 magic, u32 shift) {
 // ---------------------------------------------------------------------------
 #define FW_PLEN 7    // bytes per piece
 #define FW_UMAXM 8   // matches per cluster unit
-#define FW_UMAXR 8   // choices per unit / group
+#define FW_UMAXR 16  // choices per unit / group (4-bit R-1 fields)
 #define FW_PMAX 8    // pieces per word
 #define FW_RMAX 250  // record u64 per word (window budget)
 #define FW_TILE 256  // words per keyspace tile (one workgroup)
@@ -132,7 +132,7 @@ A5X_HD u32 fr_magic(u32 R) { return R > 1 ? (u32)((((u64)1 << 32) + R - 1) / R) 
 A5X_HD u64 fr_desc(u32 R, u32 ebase) {
   return (u64)fr_magic(R) | ((u64)(ebase & 255u) << 32) | ((u64)(R - 1) << 40) | ((u64)(R == 1) << 63);
 }
-A5X_HD u32 frd_R(u64 G) { return ((u32)(G >> 40) & 7u) + 1u; }
+A5X_HD u32 frd_R(u64 G) { return ((u32)(G >> 40) & 31u) + 1u; }
 A5X_HD u32 frd_ebase(u64 G) { return (u32)(G >> 32) & 255u; }
 
 // FAST flag fields (written by the keyspace pass): record size = 1 + np + ne
@@ -197,10 +197,12 @@ A5X_HD u32 unit_mpos(const Unit& U, u32 j) { return U.s + ((u32)((j < 4 ? U.m0 :
 
 // Enumerate the choices of a cluster in a fixed order (match subsets by increasing
 // bitmask, then values as an odometer, first match fastest); choice 0 is the empty
-// subset.  target < 0: statistics only (R, ml, spos, sneg, maxd, ok); else stop at
+// subset.  target -1: statistics only (R, ml, spos, sneg, maxd, ok); target -2:
+// also every choice a into content[a * cstride] (bytes | len << 56); else stop at
 // choice `target` and return its bytes (len <= FW_PLEN) in *content / *len.
 template <class W>
-A5X_HD void cluster_choices(const W& wd, Unit& U, const Tab& T, int target, u64* content, u32* len) {
+A5X_HD void cluster_choices(const W& wd, Unit& U, const Tab& T, int target, u64* content, u32* len,
+                            u32 cstride = 1) {
   const u32 span = U.e - U.s;
   u32 R = 0, ml = 0, mnl = 0xffffffffu, spos = 0, sneg = 0;
   int maxd = -(int)span;
@@ -242,6 +244,7 @@ A5X_HD void cluster_choices(const W& wd, Unit& U, const Tab& T, int target, u64*
         U.ok = true;
         return;
       }
+      if (target == -2) content[R * cstride] = keep_bytes64(v, n) | ((u64)n << 56);
       R++;
       ml = umax32(ml, n);
       mnl = umin32(mnl, n);
@@ -319,6 +322,15 @@ A5X_HD u64 unit_choice(const W& wd, const Unit& U, const Tab& T, u32 a, u32& len
   return v;
 }
 
+// unit_choice with a cluster's choices already enumerated into cb (stride cs)
+template <class W>
+A5X_HD u64 unit_choice_b(const W& wd, const Unit& U, const Tab& T, u32 a, u32& len, const u64* cb, u32 cs) {
+  if (U.k == 0) return unit_choice(wd, U, T, a, len);
+  const u64 e = cb[a * cs];
+  len = (u32)(e >> 56);
+  return e & FW_M56;
+}
+
 // ---------------------------------------------------------------------------
 // piece plan -> record
 // ---------------------------------------------------------------------------
@@ -330,7 +342,10 @@ struct Plan {
 
 // Record sinks.  gld/gst: the R <= FW_UMAXR entries of the open group (built in
 // place while units merge into it); ent(i, v): final entry i; desc(i, v): piece i.
+// cbuf / cstride: where a cluster unit's choices are enumerated once (BUILD only).
 struct NullSink {
+  A5X_HD u64* cbuf() const { return nullptr; }
+  A5X_HD u32 cstride() const { return 1; }
   A5X_HD u64 gld(u32) const { return 0; }
   A5X_HD void gst(u32, u64) {}
   A5X_HD void ent(u32, u64) {}
@@ -339,7 +354,9 @@ struct NullSink {
 struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
   u64* rec;
   u32 np;
-  u64 g[FW_UMAXR];
+  u64 g[FW_UMAXR], c[FW_UMAXR];
+  A5X_HD u64* cbuf() { return c; }
+  A5X_HD u32 cstride() const { return 1; }
   A5X_HD u64 gld(u32 a) const { return g[a]; }
   A5X_HD void gst(u32 a, u64 v) { g[a] = v; }
   A5X_HD void ent(u32 i, u64 v) { rec[1 + np + i] = v; }
@@ -350,7 +367,7 @@ struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
 // time (unit() in word order, then finish()).  BUILD: also write the entries and
 // piece descriptors through the sink (the header is the caller's: fr_hdr of P).
 // Shared by the unit walk (plan_word) and the position-synchronous keyspace kernel.
-template <bool BUILD, class W, class S>
+template <bool BUILD, class W, class S, u32 CAP = FW_UMAXR>
 struct Planner {
   const W& wd;
   const Tab& T;
@@ -378,7 +395,7 @@ struct Planner {
   }
   A5X_HD void close_group() {
     if constexpr (BUILD) {
-      for (u32 a = 0; a < FW_UMAXR; a++)
+      for (u32 a = 0; a < CAP; a++)
         if (a < cR) sk.ent(P.ne + a, sk.gld(a));
       sk.desc(cpi, fr_desc(cR, P.ne));
     }
@@ -400,19 +417,28 @@ struct Planner {
   A5X_HD void unit(const Unit& U) {
     if (!P.ok) return;
     const u32 Ru = U.R, ml = U.ml, run = U.s - prev;
-    if (!U.ok || ml > FW_PLEN || Ru > FW_UMAXR || Ru < 2) { P.ok = false; return; }
-    if (open && cmax + run + ml <= FW_PLEN && cR * Ru <= FW_UMAXR) {
+    if (!U.ok || ml > FW_PLEN || Ru > CAP || Ru < 2) { P.ok = false; return; }
+    u64* cb = nullptr;
+    u32 cs = 1;
+    if constexpr (BUILD) {
+      if (U.k) {  // cluster: all choices once (unit_choice would re-enumerate per entry)
+        cb = sk.cbuf(); cs = sk.cstride();
+        Unit V = U;
+        cluster_choices(wd, V, T, -2, cb, nullptr, cs);
+      }
+    }
+    if (open && cmax + run + ml <= FW_PLEN && cR * Ru <= CAP) {
       // merge: entry a1 + cR * a2 = old[a1] ++ run ++ choice a2 (descending: in place;
       // fixed trip count so lanes of a wave stay together)
       const u32 nR = cR * Ru;
       if constexpr (BUILD) {
         const u64 rb = run ? wd.ld(prev, run) : 0ull;
-        const u32 inv = (256u + cR - 1u) / cR;  // t / cR = (t * inv) >> 8 for t < 8
-        for (int t = FW_UMAXR - 1; t >= 0; t--) {
+        const u32 inv = (256u + cR - 1u) / cR;  // t / cR = (t * inv) >> 8 for t < 16
+        for (int t = CAP - 1; t >= 0; t--) {
           if ((u32)t >= nR) continue;
           const u32 a2 = ((u32)t * inv) >> 8, a1 = (u32)t - a2 * cR;
           u32 cl = 0;
-          const u64 cv = unit_choice(wd, U, T, a2, cl);
+          const u64 cv = unit_choice_b(wd, U, T, a2, cl, cb, cs);
           const u64 old = sk.gld(a1);
           const u32 ol = fw_len(old);
           const u64 v = (old & FW_M56) | (rb << (8 * ol)) | (cv << (8 * (ol + run)));
@@ -432,10 +458,10 @@ struct Planner {
       P.np++;
       if constexpr (BUILD) {
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
-        for (u32 a = 0; a < FW_UMAXR; a++) {
+        for (u32 a = 0; a < CAP; a++) {
           if (a >= Ru) continue;
           u32 cl = 0;
-          const u64 cv = unit_choice(wd, U, T, a, cl);
+          const u64 cv = unit_choice_b(wd, U, T, a, cl, cb, cs);
           const u64 v = rb | (cv << (8 * rem));
           sk.gst(a, (v & FW_M56) | fw_meta(rem + cl, Ru));
         }
@@ -449,7 +475,7 @@ struct Planner {
     if (open && cmax + tl <= FW_PLEN) {
       if constexpr (BUILD) {
         const u64 tb = (run ? wd.ld(prev, run) : 0ull) | (10ull << (8 * run));
-        for (u32 a = 0; a < FW_UMAXR; a++) {
+        for (u32 a = 0; a < CAP; a++) {
           if (a >= cR) continue;
           const u64 old = sk.gld(a);
           const u32 ol = fw_len(old);
@@ -612,7 +638,7 @@ A5X_HD u32 fw_pass1(const u64* wrec, u32 ga, u32 np, u32 wbe, u32 n, u64* e) {
     const u32 ghi = (u32)(G[i] >> 32);
     u32 q = (u32)(((u64)n * (u32)G[i]) >> 32);
     q += n & (u32)((int)ghi >> 31);  // R = 1: q = n
-    const u32 d = n - q * (((ghi >> 8) & 7u) + 1u);
+    const u32 d = n - q * (((ghi >> 8) & 31u) + 1u);
     n = q;
     idx[i] = (u32)i < np ? wbe + (ghi & 255u) + d : (u32)FX_ZSLOT;
   }
@@ -712,7 +738,7 @@ A5X_HD void fb_entry(const u64* wrec, u32 wrb, u32 b, u32 c, u32 out[4]) {
     const u32 ghi = (u32)(G >> 32);
     u32 q = (u32)(((u64)c * (u32)G) >> 32);
     q += c & (u32)((int)ghi >> 31);  // R = 1: q = c
-    const u32 d = c - q * (((ghi >> 8) & 7u) + 1u);
+    const u32 d = c - q * (((ghi >> 8) & 31u) + 1u);
     c = q;
     const u64 ev = wrec[valid ? wbe + (ghi & 255u) + d : (u32)FX_ZSLOT];
     const u64 cv = ev & FW_M56;

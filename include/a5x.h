@@ -75,7 +75,7 @@ typedef struct a5x_stats {
   double ms_expand;     /* device time: expansion kernels only (HIP events) */
   double ms_total;      /* device time of the whole call */
   uint32_t expand_launches;
-  uint32_t pad;
+  uint32_t words_slow;   /* words expanded by the per-word (non-FAST) pass */
 } a5x_stats;
 
 /* ---- context ------------------------------------------------------------ */

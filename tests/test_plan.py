@@ -89,6 +89,10 @@ def test_plan_clusters_czech_german():
     for w in [b"strasse", b"ss", b"sss", b"ssss", b"masse", b"assa", b"sassafras", b"Strasse", b"kiss", b"ssx"]:
         kinds[check_word(ctx, sub, w)] += 1
     assert kinds["fast"] >= 6
+    # 'sss' clusters: 12 choices (s, ss overlap) -> one unit of R = 12 > 8, FAST
+    for w in [b"xsssy", b"asssbsssc", b"sssss", b"kissssa"]:
+        kinds[check_word(ctx, sub, w)] += 1
+    assert check_word(ctx, sub, b"zvasssgkpg") == "fast"
     ctx.close()
 
 
