@@ -1173,14 +1173,16 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 //           instruction, consecutive lanes consecutive addresses).
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
-#define FX_RING 4096  // per-wave linear output staging (bytes), then 4 trash dwords per lane;
-                      // its upper half also holds the window's small records during setup
+#define FX_RING 2048  // per-wave linear output staging (bytes), then 4 trash dwords per lane;
+                      // during the window setup bytes [16, 16 + 8 FX_WREC) hold the window's
+                      // small records (ring block 0 keeps the run's partial block)
 #define FX_WW 32      // window words
 #define FX_NBE 256    // big entries per window (16 B each); [FX_ZBE] is the empty piece
 #define FX_ZBE (FX_NBE - 1)
 
-// The window's small-piece records live in the ring's upper half during the window
-// setup (rec[FX_ZSLOT] = 0); the rounds then reuse those bytes as output staging.
+// The window's small-piece records live in the ring (from byte 16, on into the
+// trash dwords) during the window setup (rec[FX_ZSLOT] = 0); the rounds then reuse
+// those bytes as output staging.
 struct FXWin {
   uint4 be[FX_NBE];        // big entries: 15 content bytes, length in byte 15
   // per word j, big piece b: {magic, (R - 1) | base << 8 | x << 16} at wi[j][b / 2].{xy|zw};
@@ -1189,6 +1191,7 @@ struct FXWin {
   uint4 wi[FX_WW][2];
 };
 static_assert(FW_RMAX < FX_ZSLOT && FB_EMAX < FX_ZBE, "a FAST record must fit a window");
+static_assert(16 + 8 * FX_WREC <= FX_RING + 1024, "window records must fit the ring + trash dwords");
 
 // Closed-form bytes of candidates [0, r) of a FAST word (candidate r <-> index r + 1
 // in the piece mixed radix, piece 0 least significant).  rec = the word's record
@@ -1363,7 +1366,7 @@ __device__ __forceinline__ FxMeta fx_meta(const ExpArgs& a, u64 w) {
 
 __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
-  u64* const rec = (u64*)(ring + FX_RING / 8);  // ring bytes [FX_RING / 2, FX_RING)
+  u64* const rec = (u64*)(ring + 4);  // ring bytes [16, 16 + 8 FX_WREC)
   const u64 g0 = max(a.cand_begin, chunk * a.CH);
   const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
   if (g0 >= g1) return;
@@ -1548,7 +1551,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
 
 __device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + 1024 + (u32)sizeof(FXWin) + 15u) & ~15u; }
 
-__global__ void __launch_bounds__(256) k_expand_fast(ExpArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_expand_fast(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   uint8_t* mine = smem + wv * lds_per_wave_fast();

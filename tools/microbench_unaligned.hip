@@ -24,6 +24,7 @@ __global__ void k_check(uint8_t* out, u32 b3, u32 b11, u32 b1) {
   for (u32 k = 0; k < 8; k++) v |= (u64)(uint8_t)(l * 8 + k) << (8 * k);
   const u32 off = b3 + b11 * l;  // 11 > 8: no overlap
   *(u64*)(lds + off) = v;
+  if (l < 36) *(uint4*)(lds + 1400 + 17 * l + b1) = make_uint4(l * 4 + 0x01010101u, l * 4 + 0x02020202u, l, ~l);  // 16 B at stride 17
   const u32 off2 = 1024 + 5 * l + b1;  // 4-byte writes at stride 5
   *(u32*)(lds + off2) = (u32)v;
   __syncthreads();
@@ -56,6 +57,8 @@ __global__ void __launch_bounds__(256) k_rate(int iters, u32* sink) {
     if (KIND == 7) my[o & 8191u] = (uint8_t)v;                                                       // ds_write_b8
     if (KIND == 8) *(uint16_t*)(my + (o & 8191u)) = (uint16_t)v;                                     // b16 unaligned
     if (KIND == 9) *(uint4*)(my + (o & 8191u & ~15u)) = make_uint4((u32)v, (u32)(v >> 32), 1u, 2u);  // b128 aligned
+    if (KIND == 10) *(uint4*)(my + (o & 8191u)) = make_uint4((u32)v, (u32)(v >> 32), 1u, 2u);        // b128 unaligned
+    if (KIND == 11) *(uint2*)(my + (o & 8191u)) = make_uint2((u32)v, (u32)(v >> 32));               // b64 unaligned (uint2)
     o += len * 8;  // lanes ~ stride 16 B apart, moving on
     v = v * 0x9E3779B97F4A7C15ull + 1;
   }
@@ -81,6 +84,10 @@ int main() {
   // the 4-byte stride-5 writes: byte 1024+5l+1+k = (l*8+k) for k<4, later lanes don't overlap (5>4)
   for (u32 l = 0; l < 64; l++)
     for (u32 k = 0; k < 4; k++) if (h[1024 + 5 * l + 1 + k] != (uint8_t)(l * 8 + k)) bad++;
+  for (u32 l = 0; l < 22; l++) {  // 1400 + 17*l + 1 .. +16 within the 2048 dump for l < 38
+    u32 x[4] = {l * 4 + 0x01010101u, l * 4 + 0x02020202u, l, ~l};
+    if (memcmp(h + 1400 + 17 * l + 1, x, 16)) bad++;
+  }
   // gaps untouched
   if (h[0] != 0xee || h[1] != 0xee || h[2] != 0xee || h[11] != 0xee || h[13] != 0xee) bad++;
   printf("unaligned LDS check: %s (%d bad bytes)\n", bad ? "FAIL" : "OK", bad);
@@ -95,9 +102,10 @@ int main() {
   CHECK(hipEventCreate(&b));
   const char* names[] = {"ds_write_b64 unaligned", "ds_write_b32 unaligned", "ds_write_b64 aligned  ",
                          "ds_or_b32 aligned     ", "ds_read_b32 unaligned ", "ds_read_b128 aligned  ",
-                         "ds_or_b64 aligned     ", "ds_write_b8           ", "ds_write_b16 unaligned", "ds_write_b128 aligned "};
+                         "ds_or_b64 aligned     ", "ds_write_b8           ", "ds_write_b16 unaligned", "ds_write_b128 aligned ",
+                         "ds_write_b128 unalign ", "ds_write_b64 unal (u2)"};
   const int iters = 8192;
-  for (int kind = 0; kind < 10; kind++) {
+  for (int kind = 0; kind < 12; kind++) {
     for (int bpc : {2, 4}) {
       const int blocks = cus * bpc;
       auto launch = [&]() {
@@ -112,6 +120,8 @@ int main() {
           case 7: hipLaunchKernelGGL(k_rate<7>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
           case 8: hipLaunchKernelGGL(k_rate<8>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
           case 9: hipLaunchKernelGGL(k_rate<9>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
+          case 10: hipLaunchKernelGGL(k_rate<10>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
+          case 11: hipLaunchKernelGGL(k_rate<11>, dim3(blocks), dim3(256), 0, 0, iters, sink); break;
         }
       };
       launch();
