@@ -825,7 +825,7 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   const Tab T = tab_view(c->blob.data());
   const WordClass C = classify_word(gw, (u32)len, T, mn, mx, A5X_RING_A - 16);
   info[0] = C.count; info[1] = C.bytes; info[2] = C.flags;
-  if (!(C.flags & A5X_WF_FAST) || C.count == 0 || !out) return A5X_OK;  // no out: classification only
+  if (!(C.flags & A5X_WF_FAST) || C.count == 0) return A5X_OK;
   // the record exactly as k_keyspace_thread builds it, placed as a one-word window
   std::vector<u64> wrec(FX_WREC + FW_PMAX + 16, 0);
   ArraySink sk;
@@ -835,6 +835,8 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   wrec[FX_ZSLOT] = 0;
   if (!P.ok || P.ng != ff_ng(C.flags) || P.ne != ff_ne(C.flags) || P.np != ff_np(C.flags))
     return fail(c, A5X_E_BOUNDS, "piece plan disagrees with the keyspace fields");
+  info[2] |= (uint64_t)P.nbig << 32 | (uint64_t)P.bent << 40;  // diagnostics: big pieces / entries
+  if (!out) return A5X_OK;  // no out: classification and plan only
   // big pieces and their entries as the k_expand_fast window setup builds them
   u32 Rb[FB_NMAX], base[FB_NMAX], E = 0;
   std::vector<u32> be(4 * 256, 0);

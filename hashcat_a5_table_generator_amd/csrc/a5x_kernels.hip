@@ -853,7 +853,7 @@ struct ExpArgs {
   const u64* rec;        // FAST plan records (k_keyspace_thread)
   const u32* roff;       // per word: record offset into rec
   u64 rec_n;             // u64 in rec
-  u32 ablate;            // timing experiments only (A5X_ABLATE): 2 no ring
+  u32 ablate;            // timing experiments only (A5X_ABLATE): 8 no rounds, 2 no ring
                          // writes, 4 no global stores; output is garbage when set
 };
 
@@ -1173,7 +1173,7 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 //           instruction, consecutive lanes consecutive addresses).
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
-#define FX_RING 2048  // per-wave linear output staging (bytes), then 4 trash dwords per lane;
+#define FX_RING 4096  // per-wave linear output staging (bytes), then 4 trash dwords per lane;
                       // during the window setup bytes [16, 16 + 8 FX_WREC) hold the window's
                       // small records (ring block 0 keeps the run's partial block)
 #define FX_WW 32      // window words
@@ -1268,23 +1268,82 @@ __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) 
   R.open = false;
 }
 
-// Rounds of <= K nl consecutive candidates [g, gend) of the window's k words: lane
-// L takes candidates K L .. K L + K - 1 of the round (one contiguous output run);
-// NB >= every word's big piece count.
+// One round: candidates [rr, rr + ncand); lane L takes candidates K L .. K L + K - 1
+// (one contiguous output run; candidate c of the lane in window word lo[c]).  NB >=
+// the big piece count of every word in the round.
 template <int NB, int K>
-__device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, const ExpArgs& a, FxRun& R, u64 g, u64 gend, u32 k,
-                                          u32 nl, u32 c0rel) {
+__device__ __forceinline__ void fx_round(FXWin& F, u32* ring, const ExpArgs& a, FxRun& R, u64 rr, u32 ncand,
+                                         const u32 (&lo)[K]) {
   const u32 lane = lane_id();
   const u32 T = FX_RING / 4 + 4u * lane;  // the lane's 4 trash dwords
+  const u32 nact = (ncand + K - 1) / K;     // lanes with at least one candidate
+  // pass 1: big piece digits of n = rank + 1 -> entries, length
+  uint4 e[K][NB];
+  u32 len = 0;
+#pragma unroll
+  for (int c = 0; c < K; c++) {
+    const uint4 b01 = F.wi[lo[c]][0];
+    const uint4 b23 = NB > 2 ? F.wi[lo[c]][1] : make_uint4(0, 0, 0, 0);
+    const u32 wc = (b01.y >> 16) | (((b01.w >> 16) & 255u) << 16);
+    const u32 nb = K * lane + c < ncand ? (b01.w >> 24) & 7u : 0u;
+    u32 n = (((u32)rr + K * lane + c - wc) & 0xFFFFFFu) + 1u;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const u32 magic = b == 0 ? b01.x : b == 1 ? b01.z : b == 2 ? b23.x : b23.z;
+      const u32 rb = b == 0 ? b01.y : b == 1 ? b01.w : b == 2 ? b23.y : b23.w;
+      const u32 rm1 = rb & 63u;
+      // R = 1 (magic 0): q = n, digit 0; branch-free
+      const u32 q = __umulhi(n, magic) + (magic ? 0u : n);
+      const u32 d = n - __umul24(q, rm1 + 1u);
+      n = q;
+      const u32 idx = (u32)b < nb ? ((rb >> 8) & 255u) + d : (u32)FX_ZBE;
+      e[c][b] = F.be[idx];
+      len += e[c][b].w >> 24;
+    }
+  }
+  const u32 incl = wave_incl_scan_u32(len);
+  const u32 tot = lane63(incl);
+  const u32 o = (u32)(R.pos - R.B) + incl - len;
+  // pass 2: append the pieces as whole aligned dwords (see fb_put)
+  u32 pn = o & 3u, D = o >> 2, acc = 0, hd = 0;
+  u32 pv = lane == 0 ? (R.carry << ((32u - 8u * pn) & 31u)) : 0u;
+  bool hp = lane != 0 && pn != 0;
+  if (!(a.ablate & 2u)) {
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        const u32 ev[4] = {e[c][b].x, e[c][b].y, e[c][b].z, e[c][b].w};
+        fb_put(ev, pv, pn, D, hp, hd, acc, ring, T);
+      }
+    }
+  }
+  const u32 hnext = (u32)__shfl_down((int)hd, 1);
+  ring[(lane + 1 < nact && pn) ? D : T] = acc | hnext;
+  R.carry = readlane_u32(acc, nact - 1);
+  R.pos = uniform64(R.pos + tot);
+  WAVE_SYNC();
+  fx_flush(R, ring, a);
+}
+
+// Rounds of <= K nl consecutive candidates [g, gend) of the window's k words.  K = 1:
+// each round runs the body for the largest big piece count among the words it
+// spans (m3 / m4: window words with >= 3 / 4 big pieces); K = 2: no word of the
+// window has more than 2 big pieces.
+template <int K>
+__device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, const ExpArgs& a, FxRun& R, u64 g, u64 gend, u32 k,
+                                          u32 nl, u32 c0rel, u64 m3, u64 m4) {
+  const u32 lane = lane_id();
+  if (a.ablate & 8u) return;  // timing: window setup only
   u32 jcur = 0;  // word holding the round's first candidate (uniform)
   for (u64 rr = g; rr < gend; rr += (u64)K * nl) {
     const u32 rrel = (u32)(rr - g);
     const u32 ncand = uniform((u32)min((u64)K * nl, gend - rr));
-    const u32 nact = (ncand + K - 1) / K;  // lanes with at least one candidate
     // word of each candidate: count the word starts it has passed
     u32 lo[K];
 #pragma unroll
     for (int c = 0; c < K; c++) lo[c] = jcur;
+    const u32 jf = jcur;
     for (;;) {
       const u32 jn = uniform(jcur + 1);
       if (jn >= k) break;
@@ -1294,52 +1353,14 @@ __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, const ExpArgs& a,
 #pragma unroll
       for (int c = 0; c < K; c++) lo[c] += (rrel + K * lane + c >= sj) ? 1u : 0u;
     }
-    // pass 1: big piece digits of n = rank + 1 -> entries, length
-    uint4 e[K][NB];
-    u32 len = 0;
-#pragma unroll
-    for (int c = 0; c < K; c++) {
-      const uint4 b01 = F.wi[lo[c]][0];
-      const uint4 b23 = NB > 2 ? F.wi[lo[c]][1] : make_uint4(0, 0, 0, 0);
-      const u32 wc = (b01.y >> 16) | (((b01.w >> 16) & 255u) << 16);
-      const u32 nb = K * lane + c < ncand ? (b01.w >> 24) & 7u : 0u;
-      u32 n = (((u32)rr + K * lane + c - wc) & 0xFFFFFFu) + 1u;
-#pragma unroll
-      for (int b = 0; b < NB; b++) {
-        const u32 magic = b == 0 ? b01.x : b == 1 ? b01.z : b == 2 ? b23.x : b23.z;
-        const u32 rb = b == 0 ? b01.y : b == 1 ? b01.w : b == 2 ? b23.y : b23.w;
-        const u32 rm1 = rb & 63u;
-        const u32 q = rm1 ? __umulhi(n, magic) : n;  // R = 1: digit 0
-        const u32 d = n - __umul24(q, rm1 + 1u);
-        n = q;
-        const u32 idx = (u32)b < nb ? ((rb >> 8) & 255u) + d : (u32)FX_ZBE;
-        e[c][b] = F.be[idx];
-        len += e[c][b].w >> 24;
-      }
+    if (K == 2) {
+      fx_round<2, K>(F, ring, a, R, rr, ncand, lo);
+    } else {
+      const u64 span = ((2ull << (jcur - jf)) - 1ull) << jf;  // words jf .. jcur
+      if (span & m4) fx_round<4, K>(F, ring, a, R, rr, ncand, lo);
+      else if (span & m3) fx_round<3, K>(F, ring, a, R, rr, ncand, lo);
+      else fx_round<2, K>(F, ring, a, R, rr, ncand, lo);
     }
-    const u32 incl = wave_incl_scan_u32(len);
-    const u32 tot = lane63(incl);
-    const u32 o = (u32)(R.pos - R.B) + incl - len;
-    // pass 2: append the pieces as whole aligned dwords (see fb_put)
-    u32 pn = o & 3u, D = o >> 2, acc = 0, hd = 0;
-    u32 pv = lane == 0 ? (R.carry << ((32u - 8u * pn) & 31u)) : 0u;
-    bool hp = lane != 0 && pn != 0;
-    if (!(a.ablate & 2u)) {
-#pragma unroll
-      for (int c = 0; c < K; c++) {
-#pragma unroll
-        for (int b = 0; b < NB; b++) {
-          const u32 ev[4] = {e[c][b].x, e[c][b].y, e[c][b].z, e[c][b].w};
-          fb_put(ev, pv, pn, D, hp, hd, acc, ring, T);
-        }
-      }
-    }
-    const u32 hnext = (u32)__shfl_down((int)hd, 1);
-    ring[(lane + 1 < nact && pn) ? D : T] = acc | hnext;
-    R.carry = readlane_u32(acc, nact - 1);
-    R.pos = uniform64(R.pos + tot);
-    WAVE_SYNC();
-    fx_flush(R, ring, a);
   }
 }
 
@@ -1440,6 +1461,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     const u64 bo = M.bo;
     if (lane == 0) rec[FX_ZSLOT] = 0;
     WAVE_SYNC();
+    STAMP(4);
     // ---- big pieces per word: R = product of the spanned small R ----
     u64 hdr = 0;
     u32 nbw = 0, R0 = 1, R1 = 1, R2 = 1, R3 = 1;
@@ -1471,7 +1493,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     }
     const u32 maxl = lane < k ? frh_maxl(hdr) : 0u;
     const u32 winmax = wave_max_u32(maxl);
-    const u32 nbmax = wave_max_u32(lane < k ? nbw : 0u);
+    const u64 m3 = __ballot(lane < k && nbw >= 3), m4 = __ballot(lane < k && nbw >= 4);
     const u32 ebase = incE - E;
     if (lane < k) {
       const u32 b1 = ebase + R0, b2 = b1 + R1, b3 = b2 + R2;
@@ -1481,6 +1503,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
       F.wi[lane][1] = make_uint4(fr_magic(R2), (R2 - 1u) | (b2 << 8), fr_magic(R3), (R3 - 1u) | (b3 << 8));
     }
     WAVE_SYNC();
+    STAMP(5);
     // ---- build the big entries: lanes over the window's entries ----
     {
       const u32 etot = readlane_u32(incE, k - 1);
@@ -1531,12 +1554,12 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     // ---- rounds ----
     const u64 gend = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     const u32 c0rel = (lane < k) ? (u32)(c0 > g ? c0 - g : 0) : 0xffffffffu;
-    if (nbmax <= 2) {
-      const u32 nl = uniform(min(64u, (FX_RING - 32) / max(winmax, 1u)));
-      fx_rounds<2, 1>(F, ring, a, R, g, gend, k, nl, c0rel);
+    if (m3 == 0) {
+      const u32 nl = uniform(min(64u, (FX_RING - 32) / (2u * max(winmax, 1u))));
+      fx_rounds<2>(F, ring, a, R, g, gend, k, nl, c0rel, m3, m4);
     } else {
       const u32 nl = uniform(min(64u, (FX_RING - 32) / max(winmax, 1u)));
-      fx_rounds<FB_NMAX, 1>(F, ring, a, R, g, gend, k, nl, c0rel);
+      fx_rounds<1>(F, ring, a, R, g, gend, k, nl, c0rel, m3, m4);
     }
     STAMP(3);
     g = gend;

@@ -155,7 +155,8 @@ A5X_API int a5x_debug_stamps(unsigned long long* out16, int reset);
 /* Test hook (CPU test suite): run the device keyspace classification and the FAST
  * piece plan of ONE word on the host (the same a5x_plan.h code the kernels run)
  * and, for FAST words, replay passes 1-2 of k_expand_fast into out.  info[0..3] =
- * {count, bytes, flags, bytes written}.  Never called by a5x_expand*: it checks the
+ * {count, bytes, flags | big pieces << 32 | big entries << 40, bytes written};
+ * out = NULL: classification and plan only.  Never called by a5x_expand*: it checks the
  * plan, it is not a compute path. */
 A5X_API int a5x_debug_plan_word(a5x_ctx* ctx, const uint8_t* word, size_t len, int min_sub, int max_sub,
                                 uint8_t* out, size_t cap, uint64_t* info);

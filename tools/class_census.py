@@ -30,12 +30,17 @@ def main():
     buf = data.tobytes()
     tot = {"fast": [0, 0], "slow": [0, 0], "defer": [0, 0]}
     slow = []
+    nbh, nbc = {}, {}
     for i in range(n):
         w = buf[offs[i]:offs[i + 1]]
         wb = w + b"\0" * 16
         rc = L.a5x_debug_plan_word(h, wb, len(w), 0, 15, None, 0, info.ctypes.data)
         assert rc == 0, L.a5x_last_error(h)
-        f = int(info[2])
+        f = int(info[2]) & 0xFFFFFFFF
+        if f & FAST:
+            nb = (int(info[2]) >> 32) & 0xFF
+            nbh[nb] = nbh.get(nb, 0) + 1
+            nbc[nb] = nbc.get(nb, 0) + int(info[0])
         k = "fast" if f & FAST else ("defer" if f & DEFER else "slow")
         tot[k][0] += 1
         tot[k][1] += int(info[0])
@@ -43,6 +48,8 @@ def main():
             slow.append((int(info[0]), w, f))
     for k, (a, b) in tot.items():
         print(f"{k:6s} words {a:8d}  candidates {b:12d}")
+    for nb in sorted(nbh):
+        print(f"  FAST words with {nb} big pieces: {nbh[nb]:8d} words, {nbc[nb]:12d} candidates")
     slow.sort(reverse=True)
     for c, w, f in slow[:25]:
         print(f"  {c:10d}  {w!r:20s} flags {f:#010x}")

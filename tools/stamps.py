@@ -23,7 +23,7 @@ L = _lib.load()
 assert L.a5x_debug_stamps(buf, 1) == 0, "not a diagnostic build"
 st = ctx.expand_device(dw.ptr, do.ptr, n, out.ptr, tb)
 assert L.a5x_debug_stamps(buf, 1) == 0
-names = ["meta", "records", "prefix/open", "rounds", "-", "-", "close", "-", "-"]
+names = ["meta", "big entries", "prefix/open", "rounds", "records load", "fb_R/wi/prefetch", "close", "-", "-"]
 tot = sum(buf[i] for i in range(9))
 print(f"{wl}: {n} words {tc} cands, expand {st['ms_expand']:.2f} ms; wave-cycles total {tot:.3e}")
 for i, nm in enumerate(names):
