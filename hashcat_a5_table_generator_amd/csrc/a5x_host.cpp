@@ -831,7 +831,7 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   ArraySink sk;
   sk.rec = wrec.data(); sk.np = ff_np(C.flags);
   const Plan P = plan_word<true>(gw, (u32)len, T, sk);
-  wrec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl, P.nbig, P.bstarts);
+  wrec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
   wrec[FX_ZSLOT] = 0;
   if (!P.ok || P.ng != ff_ng(C.flags) || P.ne != ff_ne(C.flags) || P.np != ff_np(C.flags))
     return fail(c, A5X_E_BOUNDS, "piece plan disagrees with the keyspace fields");
@@ -842,6 +842,7 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   std::vector<u32> be(4 * 256, 0);
   for (u32 b = 0; b < FB_NMAX; b++) {
     Rb[b] = fb_R(wrec.data(), 0, wrec[0], b);
+    if (Rb[b] != frh_R(wrec[0], b)) return fail(c, A5X_E_BOUNDS, "header R of big piece %u: %u != %u", b, frh_R(wrec[0], b), Rb[b]);
     base[b] = E;
     if (b < P.nbig) E += Rb[b];
   }

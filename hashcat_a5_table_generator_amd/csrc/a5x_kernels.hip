@@ -226,7 +226,7 @@ __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const
   DevRecSink sk;
   sk.g = g; sk.c = g + 256 * FW_UMAXR; sk.rec = rec; sk.np = ff_np(f);
   const Plan P = plan_word<true>(wd, L, T, sk);
-  rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl, P.nbig, P.bstarts);
+  rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
   if (!P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
 }
 
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       if (build) {
         pb.finish(L);
         const Plan& P = pb.P;
-        rec[0] = fr_hdr(P.np, P.ng, P.ne, P.lconst, P.maxl, P.minl, P.nbig, P.bstarts);
+        rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
         if (c2 || !P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
         a.roff[w] = (u32)(tile * FW_TILE_REC + ro);
       }
@@ -1176,6 +1176,7 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #define FX_RING 4096  // per-wave linear output staging (bytes), then 4 trash dwords per lane;
                       // during the window setup bytes [16, 16 + 8 FX_WREC) hold the window's
                       // small records (ring block 0 keeps the run's partial block)
+#define FX_TRASH 512  // trash dwords after the ring (64 lanes + 3, 4-B lane stride)
 #define FX_WW 32      // window words
 #define FX_NBE 256    // big entries per window (16 B each); [FX_ZBE] is the empty piece
 #define FX_ZBE (FX_NBE - 1)
@@ -1189,9 +1190,10 @@ struct FXWin {
   // x of piece 0 = bits 0-15 of the word's first candidate c0, x of piece 1 = c0
   // bits 16-23 | big piece count << 8 (ranks are taken mod 2^24: FW_PMAX_CNT)
   uint4 wi[FX_WW][2];
+  u32 mag[FB_RMAX + 4];    // fr_magic(R), R <= FB_RMAX
 };
 static_assert(FW_RMAX < FX_ZSLOT && FB_EMAX < FX_ZBE, "a FAST record must fit a window");
-static_assert(16 + 8 * FX_WREC <= FX_RING + 1024, "window records must fit the ring + trash dwords");
+static_assert(16 + 8 * FX_WREC <= FX_RING, "window records must fit the ring");
 
 // Closed-form bytes of candidates [0, r) of a FAST word (candidate r <-> index r + 1
 // in the piece mixed radix, piece 0 least significant).  rec = the word's record
@@ -1199,25 +1201,26 @@ static_assert(16 + 8 * FX_WREC <= FX_RING + 1024, "window records must fit the r
 __device__ u64 fast_prefix_bytes(const u64* rec, u64 r) {
   const u32 lane = lane_id();
   const u32 np = frh_np(rec[0]);
-  const u64 Y = r + 1;
-  u64 Rl = 1, G = 0;
+  const u32 Y = (u32)r + 1u;  // <= P <= FW_PMAX_CNT: 32-bit arithmetic throughout
+  u32 Rl = 1;
+  u64 G = 0;
   if (lane < np) { G = rec[1 + lane]; Rl = frd_R(G); }
-  u64 inc = Rl;  // inclusive prefix product of R over pieces
+  u32 inc = Rl;  // inclusive prefix product of R over pieces
 #pragma unroll
   for (int d = 1; d < 16; d <<= 1) {
-    const u64 y = shfl_up_u64(inc, d);
+    const u32 y = (u32)__shfl_up((int)inc, d);
     if ((int)lane >= d) inc *= y;
   }
   i64 part = 0, base0 = 0;
   if (lane < np) {
     const u64* ent = rec + 1 + np + frd_ebase(G);
-    const u64 Q = inc / Rl, full = Y / inc, rem = Y % inc;
+    const u32 Q = inc / Rl, full = Y / inc, rem = Y - full * inc;
     const int l0 = (int)fw_len(ent[0]);
     base0 = l0;
-    for (u32 v = 1; v < (u32)Rl; v++) {
-      const u64 lo = (u64)v * Q;
-      const u64 cnt = full * Q + (rem > lo ? min(Q, rem - lo) : 0);
-      part += ((i64)fw_len(ent[v]) - l0) * (i64)cnt;
+    for (u32 v = 1; v < Rl; v++) {
+      const u32 lo = v * Q;
+      const u32 cnt = full * Q + (rem > lo ? min(Q, rem - lo) : 0u);
+      part += (i64)((int)fw_len(ent[v]) - l0) * (i64)cnt;
     }
   }
   // every candidate = the digit-0 piece lengths + deltas
@@ -1275,7 +1278,8 @@ template <int NB, int K>
 __device__ __forceinline__ void fx_round(FXWin& F, u32* ring, const ExpArgs& a, FxRun& R, u64 rr, u32 ncand,
                                          const u32 (&lo)[K]) {
   const u32 lane = lane_id();
-  const u32 T = FX_RING / 4 + 4u * lane;  // the lane's 4 trash dwords
+  const u32 T = FX_RING / 4 + lane;  // the lane's trash dwords T .. T+3 (overlapping the next
+                                     // lanes': garbage; one store instruction hits consecutive dwords)
   const u32 nact = (ncand + K - 1) / K;     // lanes with at least one candidate
   // pass 1: big piece digits of n = rank + 1 -> entries, length
   uint4 e[K][NB];
@@ -1396,6 +1400,8 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
   while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
   if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
   if (lane == 0) F.be[FX_ZBE] = make_uint4(0, 0, 0, 0);
+  F.mag[lane] = fr_magic(lane);
+  if (lane == 0) F.mag[FB_RMAX] = fr_magic(FB_RMAX);
   u64 g = g0;
   FxRun R;
   R.open = false; R.B = 0; R.lo = 0; R.pos = 0; R.carry = 0;
@@ -1468,10 +1474,10 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     if (lane < k && rs) {
       hdr = rec[rb];
       nbw = frh_nbig(hdr);
-      R0 = fb_R(rec, rb, hdr, 0);
-      R1 = fb_R(rec, rb, hdr, 1);
-      R2 = fb_R(rec, rb, hdr, 2);
-      R3 = fb_R(rec, rb, hdr, 3);
+      R0 = frh_R(hdr, 0);
+      R1 = frh_R(hdr, 1);
+      R2 = frh_R(hdr, 2);
+      R3 = frh_R(hdr, 3);
     }
     const u32 E = R0 + R1 + R2 + R3 - (FB_NMAX - nbw);  // fb_R = 1 past the last big piece
     const u32 incE = wave_incl_scan_u32(E);
@@ -1498,9 +1504,9 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     if (lane < k) {
       const u32 b1 = ebase + R0, b2 = b1 + R1, b3 = b2 + R2;
       const u32 c0lo = (u32)c0 & 0xFFFFFFu;
-      F.wi[lane][0] = make_uint4(fr_magic(R0), (R0 - 1u) | (ebase << 8) | ((c0lo & 0xFFFFu) << 16), fr_magic(R1),
+      F.wi[lane][0] = make_uint4(F.mag[R0], (R0 - 1u) | (ebase << 8) | ((c0lo & 0xFFFFu) << 16), F.mag[R1],
                                  (R1 - 1u) | (b1 << 8) | ((c0lo >> 16) << 16) | (nbw << 24));
-      F.wi[lane][1] = make_uint4(fr_magic(R2), (R2 - 1u) | (b2 << 8), fr_magic(R3), (R3 - 1u) | (b3 << 8));
+      F.wi[lane][1] = make_uint4(F.mag[R2], (R2 - 1u) | (b2 << 8), F.mag[R3], (R3 - 1u) | (b3 << 8));
     }
     WAVE_SYNC();
     STAMP(5);
@@ -1572,14 +1578,14 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
   STAMP_FLUSH();
 }
 
-__device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + 1024 + (u32)sizeof(FXWin) + 15u) & ~15u; }
+__device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + FX_TRASH + (u32)sizeof(FXWin) + 15u) & ~15u; }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_expand_fast(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   uint8_t* mine = smem + wv * lds_per_wave_fast();
   u32* ring = (u32*)mine;
-  FXWin& F = *(FXWin*)(mine + FX_RING + 1024);
+  FXWin& F = *(FXWin*)(mine + FX_RING + FX_TRASH);
   const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
   if (chunk * a.CH >= a.cand_end) return;
   expand_chunk_fast(F, ring, a, chunk);
@@ -1792,7 +1798,7 @@ size_t a5x_expand_lds(u32 table_bytes, int kind, u32 waves) {
   const size_t tb = (table_bytes + 15u) & ~15u;
   if (kind == 2) return tb + ((A5X_RING_B + sizeof(LdsB) + 15u) & ~(size_t)15u);
   if (kind == 1) return tb + waves * ((A5X_RING_A + sizeof(LdsA) + 15u) & ~(size_t)15u);
-  return waves * ((FX_RING + 1024 + sizeof(FXWin) + 15u) & ~(size_t)15u);
+  return waves * ((FX_RING + FX_TRASH + sizeof(FXWin) + 15u) & ~(size_t)15u);
 }
 
 // kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b

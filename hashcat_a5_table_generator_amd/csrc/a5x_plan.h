@@ -109,20 +109,20 @@ A5X_HD u64 fw_meta(u32 len, u32 R) { return (u64)(len | ((R - 1u) << 3)) << 56; 
 A5X_HD u32 fw_len(u64 e) { return (u32)(e >> 56) & 7u; }
 A5X_HD u64 keep_bytes64(u64 v, u32 n) { return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1ull)); }
 
-// header: np | ng << 4 | ne << 8 | lconst << 16 | maxl << 24 | minl << 36 |
-//         nbig << 48 | first small piece of big pieces 1..3 << 51 (3 bits each)
-A5X_HD u64 fr_hdr(u32 np, u32 ng, u32 ne, u32 lconst, u32 maxl, u32 minl, u32 nbig = 0, u32 bstarts = 0) {
-  return (u64)np | ((u64)ng << 4) | ((u64)ne << 8) | ((u64)lconst << 16) | ((u64)maxl << 24) | ((u64)minl << 36) |
-         ((u64)nbig << 48) | ((u64)bstarts << 51);
+// header: np | ng << 4 | ne << 8 | maxl << 16 | nbig << 28 | first small piece of
+//         big pieces 1..3 << 31 (3 bits each) | R - 1 of big pieces 0..3 << 40 (6 bits
+//         each; 0 past nbig, i.e. R = 1)
+A5X_HD u64 fr_hdr(u32 np, u32 ng, u32 ne, u32 maxl, u32 nbig, u32 bstarts, u32 bRp) {
+  return (u64)np | ((u64)ng << 4) | ((u64)ne << 8) | ((u64)maxl << 16) | ((u64)nbig << 28) | ((u64)bstarts << 31) |
+         ((u64)bRp << 40);
 }
-A5X_HD u32 frh_nbig(u64 h) { return (u32)(h >> 48) & 7u; }
-A5X_HD u32 frh_bstart(u64 h, u32 b) { return b == 0 ? 0u : (b > 3 ? 15u : (u32)(h >> (51 + 3 * (b - 1))) & 7u); }
+A5X_HD u32 frh_nbig(u64 h) { return (u32)(h >> 28) & 7u; }
+A5X_HD u32 frh_bstart(u64 h, u32 b) { return b == 0 ? 0u : (b > 3 ? 15u : (u32)(h >> (31 + 3 * (b - 1))) & 7u); }
 A5X_HD u32 frh_np(u64 h) { return (u32)h & 15u; }
 A5X_HD u32 frh_ng(u64 h) { return (u32)(h >> 4) & 15u; }
 A5X_HD u32 frh_ne(u64 h) { return (u32)(h >> 8) & 255u; }
-A5X_HD u32 frh_lconst(u64 h) { return (u32)(h >> 16) & 255u; }
-A5X_HD u32 frh_maxl(u64 h) { return (u32)(h >> 24) & 4095u; }
-A5X_HD u32 frh_minl(u64 h) { return (u32)(h >> 36) & 4095u; }
+A5X_HD u32 frh_maxl(u64 h) { return (u32)(h >> 16) & 4095u; }
+A5X_HD u32 frh_R(u64 h, u32 b) { return ((u32)(h >> (40 + 6 * b)) & 63u) + 1u; }  // R of big piece b
 
 // piece descriptor: magic = ceil(2^32 / R) (0 for R = 1) | first entry (relative
 // to the entries) << 32 | (R-1) << 40 | (R == 1) << 63.  The digit of n is
@@ -337,6 +337,7 @@ A5X_HD u64 unit_choice_b(const W& wd, const Unit& U, const Tab& T, u32 a, u32& l
 struct Plan {
   u32 np, ng, ne, lconst, maxl, minl;
   u32 nbig, bstarts, bent;  // big pieces, their first small pieces (3 bits each), big entries
+  u32 bRp;                  // R - 1 of big pieces 0..3 (6 bits each)
   bool ok;
 };
 
@@ -379,7 +380,7 @@ struct Planner {
 
   A5X_HD Planner(const W& w, const Tab& t, S& s) : wd(w), T(t), sk(s) {
     P.np = 0; P.ng = 0; P.ne = 0; P.lconst = 0; P.maxl = 0; P.minl = 0; P.ok = true;
-    P.nbig = 0; P.bstarts = 0; P.bent = 0;
+    P.nbig = 0; P.bstarts = 0; P.bent = 0; P.bRp = 0;
     open = false; bR = 1; bl = 0; bspan = 0; cR = 1; cmax = 0; cmin = 0; cpi = 0; prev = 0;
   }
   A5X_HD void big_add(u32 R, u32 maxlen, u32 pi) {  // small piece pi (in order) joins a big piece
@@ -391,6 +392,10 @@ struct Planner {
       P.nbig++;
       P.bent += R;
       bR = R; bl = maxlen; bspan = 1;
+    }
+    if (P.nbig <= FB_NMAX) {
+      const u32 sh = 6u * (P.nbig - 1u);
+      P.bRp = (P.bRp & ~(63u << sh)) | (((bR - 1u) & 63u) << sh);
     }
   }
   A5X_HD void close_group() {
