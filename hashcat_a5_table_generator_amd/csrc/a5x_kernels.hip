@@ -238,9 +238,13 @@ __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const
 // Planner (and the closed-form count).  Two matches at one position or a match
 // inside a unit's span (overlapping keys: clusters), or a key longer than 4 bytes
 // at q, make the word "complex": k_keyspace_cplx walks it with next_unit.
+// ulog (count pass only): the lane's lone units as (q << 10 | key) at ulog[i * 256];
+// nlog = their number, KS_ULOG + 1 when they do not fit (the build pass re-walks).
+#define KS_ULOG 16
 template <bool COUNT, class PL>
 __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 Lmax, u32 bmax, const Tab& T,
-                                         PL& pl, CountAcc& A, bool& cplx) {
+                                         PL& pl, CountAcc& A, bool& cplx, uint16_t* ulog = nullptr,
+                                         u32* nlog = nullptr) {
   u32 cur_end = 0;
   for (u32 q = 0; q < Lmax; q++) {
     const bool act = act0 && q < L && !cplx;
@@ -275,6 +279,11 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
           if (COUNT) count_unit(A, U);
           pl.unit(U);
           cur_end = U.e;
+          if (COUNT && ulog) {
+            const bool fits = *nlog < KS_ULOG && kk < 1024u && q < 64u;
+            if (fits) ulog[*nlog * 256u] = (uint16_t)((q << 10) | kk);
+            *nlog = fits ? *nlog + 1u : (u32)KS_ULOG + 1u;
+          }
         }
       }
     }
@@ -292,6 +301,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   u64* gbuf = (u64*)(smem + tb);                       // 256 x KS_GCAP open-group entries
   u32* wsum = (u32*)(smem + tb + 256 * KS_GCAP * 8);   // per-wave sums of the scan
   uint8_t* wb = smem + tb + 256 * KS_GCAP * 8 + 64;    // KS_WB + 32 tile bytes
+  uint16_t* ulog = (uint16_t*)(wb + KS_WB + 32) + threadIdx.x;  // KS_ULOG x 256 unit log
   load_table(smem, a.table, a.table_bytes);
   __syncthreads();
   const Tab T = tab_view(smem);
@@ -337,7 +347,8 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     count_init(A, L);
     NullSink ns;
     Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
-    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx);
+    u32 nlog = 0;
+    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, ulog, &nlog);
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
     u32 f = 0;
@@ -368,7 +379,19 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       Planner<true, LWord, DevRecSink, KS_GCAP> pb(lw, T, sk);
       CountAcc A2;
       bool c2 = false;
-      psk_walk<false>(lw, L, build, wave_max_u32(build ? L : 0u), bmax, T, pb, A2, c2);
+      // replay the logged units (no second byte walk); words with more units re-walk
+      const bool replay = nlog <= KS_ULOG;
+      const u32 nrep = build && replay ? nlog : 0u;
+      for (u32 i = 0; i < wave_max_u32(nrep); i++) {
+        if (i < nrep) {
+          const u32 e = ulog[i * 256u];
+          Unit U;
+          lone_unit(T, e >> 10, e & 1023u, U);
+          pb.unit(U);
+        }
+      }
+      const bool walk = build && !replay;
+      psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2);
       if (build) {
         pb.finish(L);
         const Plan& P = pb.P;
@@ -1739,7 +1762,7 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
 }
 
 size_t a5x_keyspace_thread_lds(u32 table_bytes) {
-  return ((table_bytes + 15u) & ~15u) + FW_TILE * KS_GCAP * 8 + 64 + KS_WB + 32;
+  return ((table_bytes + 15u) & ~15u) + FW_TILE * KS_GCAP * 8 + 64 + KS_WB + 32 + FW_TILE * KS_ULOG * 2;
 }
 
 size_t a5x_keyspace_wave_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + sizeof(LdsB); }
