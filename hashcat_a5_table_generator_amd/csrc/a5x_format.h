@@ -86,3 +86,57 @@ enum : uint32_t {
 #define A5X_RING_B 16384
 #define A5X_CMAX 63            // max DP columns-1 (count window)
 #define A5X_TABLE_LDS_MAX 32768
+
+// ---------------------------------------------------------------------------
+// "Mode table" for the -r / -s / -s -r engines (main.go:208-440), staged into LDS
+// by a5x_modes.hip.  Keys are sorted bytewise (Go sort.Strings, main.go:327), so
+//   * the sorted pattern list of a word = the set bits of a key bitmap in index
+//     order (processWordSubstituteAll, main.go:310-327);
+//   * keys sharing a first byte are contiguous, and the keys matching at one
+//     word position come out in increasing length (they are all prefixes of the
+//     same suffix), i.e. in the j-loop order of validSubstitutionPositions
+//     (main.go:288-293);
+//   * an empty key (matched by -s at every position, main.go:315) is key 0.
+//
+//   A5xMHdr (64 B) | u16 bucket[257] (non-empty keys with first byte b:
+//   [bucket[b], bucket[b+1])) | A5xMKey keys[nkeys] | A5xMVal vals[nvals] | blob
+// ---------------------------------------------------------------------------
+#define A5X_MTAB_MAGIC 0x4D354131u  // "1A5M"
+#define A5X_MTAB_LDS_MAX 32768     // staging limit (bytes; + the 26 KB work area < 64 KB)
+#define A5X_MTAB_KEYS_MAX 4096     // key bitmap of 128 dwords
+
+struct A5xMHdr {
+  uint32_t magic;
+  uint32_t total_bytes;  // multiple of 16
+  uint32_t nkeys;
+  uint32_t nvals;
+  uint32_t off_bucket;
+  uint32_t off_keys;
+  uint32_t off_vals;
+  uint32_t off_blob;
+  uint32_t has_empty;    // key 0 is ""
+  uint32_t pad[7];
+};
+
+struct A5xMKey {
+  uint32_t key_off;   // blob offset of the key bytes
+  uint16_t klen;
+  uint16_t nvals;     // values in (-t file, line) order (main.go:141, 48)
+  uint32_t val_base;  // vals[val_base + v] = value v
+  uint32_t pad;
+};
+
+struct A5xMVal {
+  uint32_t off;  // blob offset
+  uint32_t len;
+};
+
+static_assert(sizeof(A5xMHdr) == 64, "mhdr");
+static_assert(sizeof(A5xMKey) == 16, "mkey");
+static_assert(sizeof(A5xMVal) == 8, "mval");
+
+// Limits of the -r / -s / -s -r device engines (a5x_modes.hip).
+#define A5X_M_LMAX 128    // word bytes
+#define A5X_M_CBUF 128    // candidate buffer per lane: candidates <= 127 bytes
+#define A5X_M_NMAX 63     // sorted patterns (-s) or match positions (-r) per word
+#define A5X_M_DPMAX 1024  // DP entries (patterns/positions + 1) x (count window + 1)

@@ -80,6 +80,16 @@ struct a5x_ctx {
   uint8_t* d_table = nullptr;
   size_t d_table_cap = 0;
   uint32_t table_bytes = 0;
+  // -r / -s / -s -r engines (a5x_modes.hip): sorted mode table + per-item state
+  bool mtable_dirty = true;
+  std::vector<uint8_t> mblob;
+  uint8_t* d_mtab = nullptr;
+  size_t d_mtab_cap = 0;
+  uint32_t mtab_bytes = 0;
+  DevBuf<uint64_t> m_nseg, m_seg_off, m_seg_bytes, m_seg_boff, m_tmp;
+  DevBuf<uint32_t> m_item_w;
+  uint64_t m_items = 0;
+  uint64_t mseg = 1024;  // candidates per mode-engine item
 
   DevBuf<uint64_t> count, bytes, cand_off, byte_off, scan_tmp, locate;
   DevBuf<uint32_t> flags, defer, chunk_w0, slow_list, big_list, roff, cplx;
@@ -296,10 +306,6 @@ int upload_table(a5x_ctx* c) {
 
 int check_mode(a5x_ctx* c, int mode) {
   if (mode < 0 || mode > 3) return fail(c, A5X_E_ARG, "bad mode %d", mode);
-  if (mode != A5X_MODE_DEFAULT)
-    return fail(c, A5X_E_UNSUPPORTED,
-                "mode %d (-r/-s) is not implemented on the device in this build; only processWord (default)",
-                mode);
   return A5X_OK;
 }
 
@@ -314,6 +320,16 @@ int decode_dev_err(a5x_ctx* c, uint32_t e) {
                 (unsigned long long)d[3], (unsigned long long)d[4], (unsigned long long)d[5],
                 (unsigned long long)d[6]);
   }
+  if (e & 128u)
+    return fail(c, A5X_E_BOUNDS,
+                "panic: runtime error: slice bounds out of range (processWordReverse, main.go:255: a negative "
+                "actualStart from the running offset)");
+  if (e & 64u)
+    return fail(c, A5X_E_UNSUPPORTED,
+                "a word exceeds the -r/-s engine limits (length <= %d B, <= %d patterns/positions, DP <= %d "
+                "entries, <= %d keys)", A5X_M_LMAX, A5X_M_NMAX, A5X_M_DPMAX, A5X_MTAB_KEYS_MAX);
+  if (e & 256u)
+    return fail(c, A5X_E_UNSUPPORTED, "a -r/-s candidate is longer than %d bytes (device limit)", A5X_M_CBUF - 1);
   if (e & 2u) return fail(c, A5X_E_OVERFLOW, "a word's keyspace overflows 64 bits");
   if (e & 16u) return fail(c, A5X_E_OVERFLOW, "batch keyspace overflows 64 bits");
   if (e & 4u)
@@ -422,6 +438,264 @@ A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   return E;
 }
 
+
+// ---------------------------------------------------------------------------
+// -r / -s / -s -r engines (a5x_modes.hip)
+// ---------------------------------------------------------------------------
+
+// The sorted mode table of a5x_format.h (keys in Go sort.Strings order, main.go:327).
+int compile_mtable(a5x_ctx* c) {
+  const Table& t = c->table;
+  std::vector<uint32_t> order(t.keys.size());
+  for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return t.keys[a] < t.keys[b]; });
+  if (order.size() > A5X_MTAB_KEYS_MAX)
+    return fail(c, A5X_E_UNSUPPORTED, "table has %zu keys (-r/-s device engines: max %d)", order.size(),
+                A5X_MTAB_KEYS_MAX);
+  std::vector<A5xMKey> keys;
+  std::vector<A5xMVal> vals;
+  std::vector<uint8_t> blob;
+  std::vector<uint16_t> bucket(257, 0);
+  uint32_t has_empty = 0;
+  for (uint32_t i : order) {
+    const std::string& k = t.keys[i];
+    if (k.empty()) has_empty = 1;  // sorts first: key 0
+    else bucket[(uint8_t)k[0] + 1]++;
+    A5xMKey K;
+    memset(&K, 0, sizeof K);
+    if (k.size() > 65535 || t.vals[i].size() > 65535) return fail(c, A5X_E_UNSUPPORTED, "table key too large");
+    K.key_off = (uint32_t)blob.size();
+    K.klen = (uint16_t)k.size();
+    K.nvals = (uint16_t)t.vals[i].size();
+    K.val_base = (uint32_t)vals.size();
+    blob.insert(blob.end(), k.begin(), k.end());
+    for (auto& v : t.vals[i]) {
+      A5xMVal V;
+      V.off = (uint32_t)blob.size();
+      V.len = (uint32_t)v.size();
+      blob.insert(blob.end(), v.begin(), v.end());
+      vals.push_back(V);
+    }
+    keys.push_back(K);
+  }
+  bucket[0] = (uint16_t)has_empty;
+  for (int b = 0; b < 256; b++) bucket[b + 1] += bucket[b];
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  A5xMHdr h;
+  memset(&h, 0, sizeof h);
+  h.magic = A5X_MTAB_MAGIC;
+  h.nkeys = (uint32_t)keys.size();
+  h.nvals = (uint32_t)vals.size();
+  h.has_empty = has_empty;
+  h.off_bucket = sizeof(A5xMHdr);
+  h.off_keys = (uint32_t)al16(h.off_bucket + 257 * sizeof(uint16_t));
+  h.off_vals = (uint32_t)al16(h.off_keys + keys.size() * sizeof(A5xMKey));
+  h.off_blob = (uint32_t)al16(h.off_vals + vals.size() * sizeof(A5xMVal));
+  const size_t total = al16(h.off_blob + blob.size() + 8);
+  if (total > A5X_MTAB_LDS_MAX)
+    return fail(c, A5X_E_UNSUPPORTED, "mode table is %zu bytes (-r/-s LDS staging max %d)", total,
+                A5X_MTAB_LDS_MAX);
+  h.total_bytes = (uint32_t)total;
+  c->mblob.assign(total, 0);
+  memcpy(c->mblob.data(), &h, sizeof h);
+  memcpy(c->mblob.data() + h.off_bucket, bucket.data(), 257 * sizeof(uint16_t));
+  if (!keys.empty()) memcpy(c->mblob.data() + h.off_keys, keys.data(), keys.size() * sizeof(A5xMKey));
+  if (!vals.empty()) memcpy(c->mblob.data() + h.off_vals, vals.data(), vals.size() * sizeof(A5xMVal));
+  if (!blob.empty()) memcpy(c->mblob.data() + h.off_blob, blob.data(), blob.size());
+  c->mtab_bytes = (uint32_t)total;
+  return A5X_OK;
+}
+
+int upload_mtable(a5x_ctx* c) {
+  if (c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (c->table.keys.empty()) return fail(c, A5X_E_NOTABLE, "no substitution table loaded");
+  if (!c->mtable_dirty) return A5X_OK;
+  int rc = compile_mtable(c);
+  if (rc) return rc;
+  if (c->d_mtab_cap < c->mblob.size()) {
+    if (c->d_mtab) (void)hipFree(c->d_mtab);
+    c->d_mtab = nullptr;
+    HIPCHK(c, hipMalloc((void**)&c->d_mtab, c->mblob.size()));
+    c->d_mtab_cap = c->mblob.size();
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_mtab, c->mblob.data(), c->mblob.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->mtable_dirty = false;
+  return A5X_OK;
+}
+
+A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode,
+                          int mn, int mx) {
+  A5xModeLaunch M;
+  memset(&M, 0, sizeof M);
+  M.mtab = c->d_mtab; M.mtab_bytes = c->mtab_bytes; M.words = d_words; M.woff = d_woff; M.nw = nw;
+  M.mode = mode; M.mn = mn; M.mx = mx; M.SEG = c->mseg;
+  M.count = c->count.p; M.nseg = c->m_nseg.p; M.flags = c->flags.p;
+  M.seg_off = c->m_seg_off.p; M.item_w = c->m_item_w.p; M.nitems = c->m_items;
+  M.seg_bytes = c->m_seg_bytes.p; M.seg_boff = c->m_seg_boff.p;
+  M.cand_begin = 0; M.cand_end = ~0ull;
+  M.err = c->d_scalars + 2;
+  return M;
+}
+
+// Keyspace of the -r / -s / -s -r engines: per-word counts (DP), items of mseg
+// candidates, a length pass over every item (output bytes are not closed-form under
+// sequential strings.ReplaceAll), and the scans.  Synchronises twice.
+int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn,
+                      int mx, uint64_t* d_cand_off, uint64_t* d_byte_off, hipStream_t st, Batch* B, bool timed) {
+  int rc;
+  if ((rc = upload_mtable(c))) return rc;
+  if (nw > 0xffffffffull) return fail(c, A5X_E_ARG, "batch of %llu words (max 2^32-1)", (unsigned long long)nw);
+  // -r with min < 0: generateCombinations(n, k<0) recurses until the goroutine stack
+  // overflows (main.go:263-281), which kills the reference process on the first word.
+  if (mode == A5X_MODE_REVERSE && mn < 0 && mx >= -1 && nw > 0)
+    return fail(c, A5X_E_BOUNDS,
+                "fatal error: stack overflow (generateCombinations with k < 0, main.go:273; --table-min %d)", mn);
+  if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
+      (rc = grow(c, c->m_nseg, nw + 1)) || (rc = grow(c, c->m_seg_off, nw + 1)) ||
+      (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)))
+    return rc;
+  if (!d_cand_off) {
+    if ((rc = grow(c, c->cand_off, nw + 1))) return rc;
+    d_cand_off = c->cand_off.p;
+  }
+  if (!d_byte_off) {
+    if ((rc = grow(c, c->byte_off, nw + 1))) return rc;
+    d_byte_off = c->byte_off.p;
+  }
+  if (timed) HIPCHK(c, hipEventRecord(c->ev[0], st));
+  HIPCHK(c, hipMemsetAsync(c->d_scalars, 0, 128, st));
+  B->cand_off = d_cand_off;
+  B->byte_off = d_byte_off;
+  B->nbig = B->nslow = 0;
+  if (nw == 0) {
+    HIPCHK(c, hipMemsetAsync(d_cand_off, 0, 8, st));
+    HIPCHK(c, hipMemsetAsync(d_byte_off, 0, 8, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    B->total_cands = B->total_bytes = 0;
+    c->m_items = 0;
+    return A5X_OK;
+  }
+  A5xModeLaunch M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx);
+  HIPCHK(c, a5x_launch_mode_count(M, st));
+  HIPCHK(c, a5x_launch_scan(c->count.p, c->m_nseg.p, nw, d_cand_off, c->m_seg_off.p, c->scan_tmp.p,
+                            c->d_scalars + 2, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_totals, d_cand_off + nw, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_totals + 1, c->m_seg_off.p + nw, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  auto name_word = [&]() {
+    std::vector<uint32_t> fl(nw);
+    std::vector<uint64_t> wo(nw + 1);
+    if (hipMemcpy(fl.data(), c->flags.p, nw * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+        hipMemcpy(wo.data(), d_woff, (nw + 1) * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      for (uint64_t i = 0; i < nw; i++)
+        if (fl[i] & (A5X_WF_ERR_BIG | A5X_WF_ERR_OVF)) {
+          std::string w((size_t)(wo[i + 1] - wo[i]), '\0');
+          (void)hipMemcpy(&w[0], d_words + wo[i], w.size(), hipMemcpyDeviceToHost);
+          char tail[160];
+          snprintf(tail, sizeof tail, " [word %llu len %zu: %.40s]", (unsigned long long)i, w.size(), w.c_str());
+          c->err += tail;
+          break;
+        }
+    }
+  };
+  if ((rc = decode_dev_err(c, c->h_scalars[2]))) {
+    name_word();
+    return rc;
+  }
+  B->total_cands = c->h_totals[0];
+  const uint64_t items = c->h_totals[1];
+  c->m_items = items;
+  if ((rc = grow(c, c->m_item_w, items + 1)) || (rc = grow(c, c->m_seg_bytes, items + 1)) ||
+      (rc = grow(c, c->m_seg_boff, items + 1)) || (rc = grow(c, c->m_tmp, items + 1)) ||
+      (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(items + 1) + 16)))
+    return rc;
+  M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx);
+  M.cand_off = d_cand_off;
+  M.item_begin = 0;
+  M.item_end = items;
+  if (items) {
+    HIPCHK(c, a5x_launch_plan(c->m_seg_off.p, nw, 1, c->m_item_w.p, st));
+    HIPCHK(c, a5x_launch_mode_items(M, 0, st));
+  }
+  if (items)
+    HIPCHK(c, a5x_launch_scan(c->m_seg_bytes.p, c->m_seg_bytes.p, items, c->m_seg_boff.p, c->m_tmp.p,
+                              c->scan_tmp.p, c->d_scalars + 2, st));
+  else
+    HIPCHK(c, hipMemsetAsync(c->m_seg_boff.p, 0, 8, st));
+  HIPCHK(c, a5x_launch_mode_wordbytes(c->m_seg_off.p, c->m_seg_boff.p, nw, d_byte_off, c->bytes.p, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_totals + 1, d_byte_off + nw, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+  B->total_bytes = c->h_totals[1];
+  return A5X_OK;
+}
+
+int expand_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn, int mx,
+                uint64_t cand_begin, uint64_t cand_end, uint8_t* d_out, uint64_t out_cap, uint64_t* d_cand_off,
+                uint64_t* d_byte_off, a5x_stats* stats, hipStream_t st) {
+  int rc;
+  Batch B;
+  if ((rc = run_keyspace_mode(c, d_words, d_woff, nw, mode, mn, mx, d_cand_off, d_byte_off, st, &B, true)))
+    return rc;
+  const uint64_t cb = std::min(cand_begin, B.total_cands);
+  const uint64_t ce = std::min(cand_end, B.total_cands);
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->words = nw;
+  }
+  if (ce <= cb) return A5X_OK;
+  A5xModeLaunch M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx);
+  M.cand_off = B.cand_off;
+  uint64_t b0 = 0, b1 = B.total_bytes, i0 = 0, i1 = c->m_items;
+  if (cb > 0 || ce < B.total_cands) {
+    if ((rc = grow(c, c->locate, 8))) return rc;
+    uint64_t hq[2] = {cb, ce};
+    HIPCHK(c, hipMemcpyAsync(c->locate.p, hq, 16, hipMemcpyHostToDevice, st));
+    HIPCHK(c, a5x_launch_mode_locate(M, c->locate.p, 2, c->locate.p + 2, st));
+    uint64_t loc[6];
+    HIPCHK(c, hipMemcpyAsync(loc, c->locate.p + 2, 48, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+    i0 = loc[0]; b0 = loc[2];
+    i1 = loc[3] + (loc[4] ? 1 : 0); b1 = loc[5];
+  }
+  if (stats) {
+    stats->candidates = ce - cb;
+    stats->bytes = b1 - b0;
+  }
+  if (b1 - b0 > out_cap || (!d_out && b1 > b0))
+    return fail(c, A5X_E_CAPACITY, "output needs %llu bytes, buffer has %llu", (unsigned long long)(b1 - b0),
+                (unsigned long long)out_cap);
+  M.item_begin = i0;
+  M.item_end = i1;
+  M.cand_begin = cb;
+  M.cand_end = ce;
+  M.out = d_out;
+  M.out_base = b0;
+  M.out_cap = out_cap;
+  HIPCHK(c, hipEventRecord(c->ev[1], st));
+  HIPCHK(c, a5x_launch_mode_items(M, 1, st));
+  HIPCHK(c, hipEventRecord(c->ev[2], st));
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+  if (stats) {
+    float a = 0, b = 0, t = 0;
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    HIPCHK(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[2]));
+    stats->ms_keyspace = a;
+    stats->ms_expand = b;
+    stats->ms_total = t;
+    stats->expand_launches = 1;
+  }
+  return A5X_OK;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -464,6 +738,7 @@ int a5x_create(int device, a5x_ctx** out) {
     return A5X_E_HIP;
   }
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
+  if (const char* e = getenv("A5X_MSEG")) c->mseg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_SEG")) c->seg = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_ABLATE")) c->ablate = (uint32_t)atoi(e);
   if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
@@ -479,6 +754,9 @@ void a5x_destroy(a5x_ctx* c) {
   release(c->count); release(c->bytes); release(c->cand_off); release(c->byte_off); release(c->scan_tmp);
   release(c->locate); release(c->flags); release(c->defer); release(c->chunk_w0); release(c->slow_list); release(c->big_list);
   release(c->segs);
+  release(c->m_nseg); release(c->m_seg_off); release(c->m_seg_bytes); release(c->m_seg_boff); release(c->m_tmp);
+  release(c->m_item_w);
+  if (c->d_mtab) (void)hipFree(c->d_mtab);
   release(c->s_words); release(c->s_out); release(c->s_woff);
   if (c->d_table) (void)hipFree(c->d_table);
   if (c->d_scalars) (void)hipFree(c->d_scalars);
@@ -524,6 +802,7 @@ int a5x_parse_table(a5x_ctx* c, const uint8_t* data, size_t len) {
   if (rc) return rc;
   c->table = std::move(t);
   c->table_dirty = true;
+  c->mtable_dirty = true;
   return A5X_OK;
 }
 
@@ -545,6 +824,7 @@ int a5x_set_table(a5x_ctx* c, const uint8_t* kb, const uint64_t* koff, uint32_t 
   }
   c->table = std::move(t);
   c->table_dirty = true;
+  c->mtable_dirty = true;
   return A5X_OK;
 }
 
@@ -552,6 +832,7 @@ int a5x_clear_table(a5x_ctx* c) {
   if (!c) return A5X_E_ARG;
   c->table.clear();
   c->table_dirty = true;
+  c->mtable_dirty = true;
   return A5X_OK;
 }
 
@@ -612,7 +893,11 @@ int a5x_keyspace_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   Batch B;
-  if ((rc = run_keyspace(c, d_words, d_woff, nw, mn, mx, d_cand_off, d_byte_off, st, &B, false))) return rc;
+  if (mode != A5X_MODE_DEFAULT)
+    rc = run_keyspace_mode(c, d_words, d_woff, nw, mode, mn, mx, d_cand_off, d_byte_off, st, &B, false);
+  else
+    rc = run_keyspace(c, d_words, d_woff, nw, mn, mx, d_cand_off, d_byte_off, st, &B, false);
+  if (rc) return rc;
   if (tc) *tc = B.total_cands;
   if (tb) *tb = B.total_bytes;
   return A5X_OK;
@@ -627,6 +912,9 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   if ((rc = check_mode(c, mode))) return rc;
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (mode != A5X_MODE_DEFAULT)
+    return expand_mode(c, d_words, d_woff, nw, mode, mn, mx, cand_begin, cand_end, d_out, out_cap, d_cand_off,
+                       d_byte_off, stats, st);
   Batch B;
   if ((rc = run_keyspace(c, d_words, d_woff, nw, mn, mx, d_cand_off, d_byte_off, st, &B, true))) return rc;
   const uint64_t cb = std::min(cand_begin, B.total_cands);
@@ -736,8 +1024,11 @@ int a5x_keyspace(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_
   if (wbytes) HIPCHK(c, hipMemcpyAsync(c->s_words.p, words, wbytes, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->s_woff.p, woff, (nw + 1) * 8, hipMemcpyHostToDevice, c->stream));
   Batch B;
-  if ((rc = run_keyspace(c, c->s_words.p, c->s_woff.p, nw, mn, mx, nullptr, nullptr, c->stream, &B, false)))
-    return rc;
+  if (mode != A5X_MODE_DEFAULT)
+    rc = run_keyspace_mode(c, c->s_words.p, c->s_woff.p, nw, mode, mn, mx, nullptr, nullptr, c->stream, &B, false);
+  else
+    rc = run_keyspace(c, c->s_words.p, c->s_woff.p, nw, mn, mx, nullptr, nullptr, c->stream, &B, false);
+  if (rc) return rc;
   if (out_count && nw) HIPCHK(c, hipMemcpyAsync(out_count, c->count.p, nw * 8, hipMemcpyDeviceToHost, c->stream));
   if (out_bytes && nw) HIPCHK(c, hipMemcpyAsync(out_bytes, c->bytes.p, nw * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -79,3 +79,37 @@ hipError_t a5x_launch_locate(const A5xExpLaunch& L, const uint64_t* cands, uint3
                              hipStream_t st);
 hipError_t a5x_launch_digest(const uint8_t* out, const uint64_t* byte_off, uint64_t out_base, uint64_t nw,
                              uint64_t* dig, hipStream_t st);
+
+// ---- -r / -s / -s -r engines (a5x_modes.hip) --------------------------------
+struct A5xModeLaunch {
+  const uint8_t* mtab;  // A5xMHdr blob (a5x_format.h)
+  uint32_t mtab_bytes;
+  const uint8_t* words;
+  const uint64_t* woff;
+  uint64_t nw;
+  int mode, mn, mx;
+  uint64_t SEG;          // candidates per item
+  uint64_t* count;       // k_mode_count outputs: per-word count, items, flags
+  uint64_t* nseg;
+  uint32_t* flags;
+  const uint64_t* cand_off;  // exclusive scans (n+1)
+  const uint64_t* seg_off;
+  const uint32_t* item_w;    // item -> word
+  uint64_t nitems;
+  uint64_t item_begin, item_end;
+  uint64_t* seg_bytes;       // length pass output (per item)
+  const uint64_t* seg_boff;  // exclusive scan of seg_bytes (nitems+1)
+  uint64_t cand_begin, cand_end;
+  uint8_t* out;
+  uint64_t out_base, out_cap;
+  uint32_t* err;
+};
+size_t a5x_mode_lds(uint32_t mtab_bytes);
+hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st);
+// op 0: per-item output bytes (seg_bytes); op 1: expand items [item_begin, item_end)
+hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st);
+// out[3q..3q+2] = {item, index in item, byte offset} of global candidate cands[q]
+hipError_t a5x_launch_mode_locate(const A5xModeLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out,
+                                  hipStream_t st);
+hipError_t a5x_launch_mode_wordbytes(const uint64_t* seg_off, const uint64_t* seg_boff, uint64_t nw,
+                                     uint64_t* byte_off, uint64_t* bytes, hipStream_t st);

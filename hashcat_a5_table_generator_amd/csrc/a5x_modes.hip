@@ -1,0 +1,528 @@
+// a5x_modes.hip -- gfx950 kernels for the -r, -s and -s -r engines.
+//
+//   -r     processWordReverse              /root/reference/main.go:208-261 (+263-305)
+//   -s     processWordSubstituteAll        /root/reference/main.go:308-365
+//   -s -r  processWordSubstituteAllReverse /root/reference/main.go:369-440
+//
+// The three engines enumerate subsets of a per-word list with a size window:
+//   -r     non-overlapping subsets of the match positions (start, keyLength) of
+//          the ORIGINAL word (main.go:215-226, 283-305), sizes [max(min,0),
+//          min(max,#positions)], each position replaced by subs[0] and applied in
+//          descending index order with the reference's running offset
+//          (main.go:249-257, bug-compatible; a negative start is the Go slice
+//          panic, reported as A5X_E_BOUNDS);
+//   -s     the sorted unique patterns present in the word (main.go:310-327), each
+//          either kept or replaced by one of its values, sizes [max(min,0), max];
+//          the leaf applies strings.ReplaceAll per chosen pattern (main.go:339-341);
+//   -s -r  the same patterns with subs[0] only (main.go:387-392), every subset of
+//          size [max(min,0), max] (the recursion of main.go:396-437 visits each once).
+// Go iterates the leaf's map in random order (main.go:339, 410); the device applies
+// the patterns in sorted order, one of the orders the reference can take (for
+// confluent words the only result).
+//
+// Counting is a DP over the list with the subset size as the column (lanes over
+// columns):  -r   D[j][c] = D[j+1][c] + D[next(j)][c-1]   (next = first position
+//                                                            starting past j's key)
+//            -s   D[i][c] = D[i+1][c] + f_i * D[i+1][c-1]  (f_i = values of pattern i;
+//                                                            1 for -s -r)
+// and candidate t of a word is unranked by walking the same table.  Output bytes
+// are not closed-form under sequential ReplaceAll, so a length pass builds every
+// candidate once and the expansion pass builds it again and writes it.
+//
+// Work items: (word, SEG-candidate segment); one wave per item; every lane builds
+// one candidate per round in its own LDS buffer (stride 132 B: the 64 lanes' byte
+// columns fall in distinct banks), a wave scan of the lengths places them, and the
+// lane stores its bytes.  These engines are not the headline path.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "a5x.h"
+#include "a5x_format.h"
+#include "a5x_launch.h"
+
+namespace {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+#define M_WAVE_SYNC()                                        \
+  do {                                                       \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+    __builtin_amdgcn_wave_barrier();                         \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+  } while (0)
+
+// device error bits (shared with a5x_kernels.hip's A5X_DERR_*)
+constexpr u32 M_ERR_OVF = 1u << 1;
+constexpr u32 M_ERR_STATE = 1u << 3;
+constexpr u32 M_ERR_GUARD = 1u << 5;
+constexpr u32 M_ERR_LIMIT = 1u << 6;  // word beyond the mode-engine limits
+constexpr u32 M_ERR_PANIC = 1u << 7;  // -r slice-bounds panic (main.go:255)
+constexpr u32 M_ERR_CLEN = 1u << 8;   // a candidate longer than A5X_M_CBUF-1
+
+constexpr u32 LSTRIDE = A5X_M_CBUF + 4;
+constexpr u32 CMAXLEN = A5X_M_CBUF - 1;
+
+struct MLds {
+  u64 dp[A5X_M_DPMAX];
+  u32 bitmap[A5X_MTAB_KEYS_MAX / 32];
+  uint8_t word[A5X_M_LMAX + 16];
+  uint16_t pat[64];          // key index per sorted pattern (-s) / per position (-r)
+  uint8_t pst[64], pnx[64];  // -r: start byte, first later compatible position
+  uint8_t buf[2][64 * LSTRIDE];
+};
+
+struct MT {
+  const A5xMHdr* h;
+  const uint16_t* bucket;
+  const A5xMKey* keys;
+  const A5xMVal* vals;
+  const uint8_t* blob;
+};
+
+struct MInfo {
+  u32 L, n, cmin, cmax, cols;
+  u64 count;
+  u32 bad;  // M_ERR_* of the word (0: fine)
+};
+
+__device__ __forceinline__ u32 m_lane() { return __lane_id(); }
+
+__device__ __forceinline__ u32 m_incl_scan(u32 x) {
+  const u32 lane = m_lane();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 y = (u32)__shfl_up((int)x, d, 64);
+    if ((int)lane >= d) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ u32 m_wave_or(u32 x) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) x |= (u32)__shfl_xor((int)x, d, 64);
+  return x;
+}
+
+__device__ __forceinline__ u64 m_uniform64(u64 x) {
+  const u32 lo = (u32)__builtin_amdgcn_readfirstlane((int)(u32)x);
+  const u32 hi = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(x >> 32));
+  return ((u64)hi << 32) | lo;
+}
+
+__device__ __forceinline__ MT m_table(uint8_t* lds, const uint8_t* g, u32 bytes) {
+  // stage the mode table (16-B granules, the blob is 16-B padded by the host)
+  const uint4* src = (const uint4*)g;
+  uint4* dst = (uint4*)lds;
+  for (u32 i = threadIdx.x; i < bytes / 16; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  MT T;
+  T.h = (const A5xMHdr*)lds;
+  T.bucket = (const uint16_t*)(lds + T.h->off_bucket);
+  T.keys = (const A5xMKey*)(lds + T.h->off_keys);
+  T.vals = (const A5xMVal*)(lds + T.h->off_vals);
+  T.blob = lds + T.h->off_blob;
+  return T;
+}
+
+// does key k match the word at q (the word is in LDS, length L)?
+__device__ __forceinline__ bool m_match(const MT& T, const uint8_t* wd, u32 L, u32 q, u32 k) {
+  const A5xMKey K = T.keys[k];
+  if (K.klen == 0 || q + K.klen > L) return false;
+  const uint8_t* p = T.blob + K.key_off;
+  for (u32 i = 0; i < K.klen; i++)
+    if (wd[q + i] != p[i]) return false;
+  return true;
+}
+
+// utf8.DecodeRuneInString width (invalid -> 1), as strings.Replace steps runes
+// for an empty old (Go 1.23 unicode/utf8)
+__device__ __forceinline__ u32 m_rune_len(const uint8_t* s, u32 n) {
+  const u32 b0 = s[0];
+  if (b0 < 0x80u) return 1;
+  u32 size, lo = 0x80u, hi = 0xBFu;
+  if (b0 >= 0xC2u && b0 <= 0xDFu) size = 2;
+  else if (b0 >= 0xE0u && b0 <= 0xEFu) {
+    size = 3;
+    if (b0 == 0xE0u) lo = 0xA0u;
+    else if (b0 == 0xEDu) hi = 0x9Fu;
+  } else if (b0 >= 0xF0u && b0 <= 0xF4u) {
+    size = 4;
+    if (b0 == 0xF0u) lo = 0x90u;
+    else if (b0 == 0xF4u) hi = 0x8Fu;
+  } else {
+    return 1;
+  }
+  if (n < size) return 1;
+  if (s[1] < lo || s[1] > hi) return 1;
+  for (u32 k = 2; k < size; k++)
+    if (s[k] < 0x80u || s[k] > 0xBFu) return 1;
+  return size;
+}
+
+// strings.ReplaceAll(src[:n], p, v) into dst; returns the length (err |= CLEN when
+// the result does not fit the lane buffer)
+__device__ u32 m_replace_all(const uint8_t* src, u32 n, const uint8_t* p, u32 pl, const uint8_t* v, u32 vl,
+                             uint8_t* dst, u32& err) {
+  u32 o = 0;
+  if (pl == 0) {  // "" matches before every rune and at the end
+    if (vl > CMAXLEN) { err |= M_ERR_CLEN; return 0; }
+    for (u32 k = 0; k < vl; k++) dst[o++] = v[k];
+    u32 i = 0;
+    while (i < n) {
+      const u32 sz = m_rune_len(src + i, n - i);
+      if (o + sz + vl > CMAXLEN) { err |= M_ERR_CLEN; return 0; }
+      for (u32 k = 0; k < sz; k++) dst[o++] = src[i + k];
+      for (u32 k = 0; k < vl; k++) dst[o++] = v[k];
+      i += sz;
+    }
+    return o;
+  }
+  const uint8_t p0 = p[0];
+  u32 i = 0;
+  while (i < n) {
+    bool m = src[i] == p0 && i + pl <= n;
+    for (u32 k = 1; m && k < pl; k++) m = src[i + k] == p[k];
+    if (m) {
+      if (o + vl > CMAXLEN) { err |= M_ERR_CLEN; return 0; }
+      for (u32 k = 0; k < vl; k++) dst[o++] = v[k];
+      i += pl;
+    } else {
+      if (o + 1 > CMAXLEN) { err |= M_ERR_CLEN; return 0; }
+      dst[o++] = src[i++];
+    }
+  }
+  return o;
+}
+
+// Per-word setup (wave-uniform result): word -> LDS, the pattern / position list,
+// the DP table and the count.
+__device__ MInfo m_setup(MLds& S, const MT& T, const A5xModeLaunch& a, u64 w) {
+  const u32 lane = m_lane();
+  MInfo I;
+  I.L = I.n = I.cmin = I.cmax = I.cols = 0;
+  I.count = 0;
+  I.bad = 0;
+  const u64 w0 = a.woff[w], w1 = a.woff[w + 1];
+  if (w1 - w0 > A5X_M_LMAX) { I.bad = M_ERR_LIMIT; return I; }
+  const u32 L = (u32)(w1 - w0);
+  I.L = L;
+  M_WAVE_SYNC();  // previous item's readers of S are done
+  for (u32 i = lane; i < L; i += 64) S.word[i] = a.words[w0 + i];
+  M_WAVE_SYNC();
+  u32 n = 0;
+  if (a.mode == A5X_MODE_REVERSE) {
+    // positions in (start, keyLength) order (main.go:215-226): starts q = lane, lane+64
+    for (u32 half = 0; half < 2; half++) {
+      const u32 q = half * 64 + lane;
+      u32 k0 = 0, k1 = 0, m = 0;
+      if (q < L) {
+        const u32 b = S.word[q];
+        k0 = T.bucket[b];
+        k1 = T.bucket[b + 1];
+        for (u32 k = k0; k < k1; k++) m += m_match(T, S.word, L, q, k) ? 1u : 0u;
+      }
+      const u32 incl = m_incl_scan(m);
+      const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+      u32 o = n + incl - m;
+      if (n + tot <= A5X_M_NMAX && m)
+        for (u32 k = k0; k < k1; k++)
+          if (m_match(T, S.word, L, q, k)) { S.pat[o] = (uint16_t)k; S.pst[o] = (uint8_t)q; o++; }
+      n += tot;
+    }
+    if (n > A5X_M_NMAX) { I.bad = M_ERR_LIMIT; return I; }
+    M_WAVE_SYNC();
+    if (lane < n) {
+      const u32 end = S.pst[lane] + T.keys[S.pat[lane]].klen;
+      u32 nx = n;
+      for (u32 k = lane + 1; k < n; k++)
+        if (S.pst[k] >= end) { nx = k; break; }
+      S.pnx[lane] = (uint8_t)nx;
+    }
+  } else {
+    // unique patterns present (main.go:312-319), sorted = increasing key index
+    const u32 nk = T.h->nkeys, nwd = (nk + 31) / 32;
+    for (u32 i = lane; i < nwd; i += 64) S.bitmap[i] = 0;
+    M_WAVE_SYNC();
+    for (u32 q = lane; q < L; q += 64) {
+      const u32 b = S.word[q];
+      for (u32 k = T.bucket[b]; k < T.bucket[b + 1]; k++)
+        if (m_match(T, S.word, L, q, k)) atomicOr(&S.bitmap[k >> 5], 1u << (k & 31));
+    }
+    if (T.h->has_empty && L > 0 && lane == 0) atomicOr(&S.bitmap[0], 1u);
+    M_WAVE_SYNC();
+    const u32 d0 = 2 * lane < nwd ? S.bitmap[2 * lane] : 0u;
+    const u32 d1 = 2 * lane + 1 < nwd ? S.bitmap[2 * lane + 1] : 0u;
+    const u32 m = (u32)__builtin_popcount(d0) + (u32)__builtin_popcount(d1);
+    const u32 incl = m_incl_scan(m);
+    n = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    if (n > A5X_M_NMAX) { I.bad = M_ERR_LIMIT; return I; }
+    u32 o = incl - m;
+    for (u32 x = d0; x; x &= x - 1) S.pat[o++] = (uint16_t)(64 * lane + (u32)__builtin_ctz(x));
+    for (u32 x = d1; x; x &= x - 1) S.pat[o++] = (uint16_t)(64 * lane + 32 + (u32)__builtin_ctz(x));
+  }
+  I.n = n;
+  if (a.mx < 0) return I;
+  const u32 cmax = min((u32)a.mx, n);
+  const u32 cmin = a.mn > 0 ? (u32)a.mn : 0u;
+  if (cmin > cmax) return I;
+  const u32 cols = cmax + 1;
+  if ((n + 1) * cols > A5X_M_DPMAX) { I.bad = M_ERR_LIMIT; return I; }
+  I.cmin = cmin; I.cmax = cmax; I.cols = cols;
+  M_WAVE_SYNC();
+  u64* D = S.dp;
+  const u32 c = lane;
+  if (c < cols) D[n * cols + c] = c == 0 ? 1ull : 0ull;
+  u32 ovf = 0;
+  for (int r = (int)n - 1; r >= 0; r--) {
+    M_WAVE_SYNC();
+    if (c < cols) {
+      u64 x = D[(r + 1) * cols + c];
+      if (c > 0) {
+        u64 y;
+        if (a.mode == A5X_MODE_REVERSE) {
+          y = D[S.pnx[r] * cols + c - 1];
+        } else {
+          u64 f = T.keys[S.pat[r]].nvals;
+          if (a.mode == A5X_MODE_SUBALL_REVERSE) f = f ? 1u : 0u;
+          if (__builtin_mul_overflow(f, D[(r + 1) * cols + c - 1], &y)) { ovf = 1; y = ~0ull; }
+        }
+        if (__builtin_add_overflow(x, y, &x)) { ovf = 1; x = ~0ull; }
+      }
+      D[r * cols + c] = x;
+    }
+  }
+  M_WAVE_SYNC();
+  u64 cnt = 0;
+  for (u32 k = cmin; k <= cmax; k++)
+    if (__builtin_add_overflow(cnt, D[k], &cnt)) ovf = 1;
+  if (m_wave_or(ovf)) { I.bad = M_ERR_OVF; return I; }
+  I.count = m_uniform64(cnt);
+  return I;
+}
+
+// Build candidate t (0 <= t < count) of the word set up in S into this lane's
+// buffer; returns its length and the buffer holding it.
+__device__ u32 m_build(MLds& S, const MT& T, const MInfo& I, int mode, u64 t, const uint8_t** outp, u32& err) {
+  const u32 lane = m_lane();
+  uint8_t* b0 = S.buf[0] + lane * LSTRIDE;
+  uint8_t* b1 = S.buf[1] + lane * LSTRIDE;
+  const u64* D = S.dp;
+  const u32 cols = I.cols, n = I.n;
+  u32 c = I.cmin;
+  while (c < I.cmax && t >= D[c]) { t -= D[c]; c++; }
+  if (mode == A5X_MODE_REVERSE) {
+    // unrank the non-overlapping subset (bit j = position j chosen)
+    u64 sel = 0;
+    u32 r = 0;
+    while (c > 0) {
+      if (r >= n) { err |= M_ERR_STATE; break; }
+      const u64 a0 = D[(r + 1) * cols + c];
+      if (t < a0) { r++; continue; }
+      t -= a0;
+      sel |= 1ull << r;
+      r = S.pnx[r];
+      c--;
+    }
+    u32 len = I.L;
+    for (u32 i = 0; i < len; i++) b0[i] = S.word[i];
+    // combo indices descending, running offset (main.go:249-257)
+    int off = 0;
+    while (sel) {
+      const u32 j = 63u - (u32)__builtin_clzll(sel);
+      sel &= ~(1ull << j);
+      const A5xMKey K = T.keys[S.pat[j]];
+      if (K.nvals == 0) { err |= M_ERR_PANIC; break; }  // pos.subs[0] on an empty list
+      const A5xMVal V = T.vals[K.val_base];
+      const int st = (int)S.pst[j] + off;
+      if (st < 0) { err |= M_ERR_PANIC; break; }       // result[:actualStart], actualStart < 0
+      const int dl = (int)V.len - (int)K.klen;
+      const int nl = (int)len + dl;
+      if (nl > (int)CMAXLEN) { err |= M_ERR_CLEN; break; }
+      const u32 tail = (u32)st + K.klen;  // <= len
+      if (dl > 0) {
+        for (u32 i = len; i-- > tail;) b0[i + dl] = b0[i];
+      } else if (dl < 0) {
+        for (u32 i = tail; i < len; i++) b0[i + dl] = b0[i];
+      }
+      const uint8_t* v = T.blob + V.off;
+      for (u32 i = 0; i < V.len; i++) b0[st + i] = v[i];
+      len = (u32)nl;
+      off += dl;
+    }
+    *outp = b0;
+    return len;
+  }
+  // -s / -s -r: chosen patterns in sorted order, ReplaceAll each (main.go:339-341)
+  const uint8_t* src = S.word;
+  uint8_t* dst = b0;
+  u32 len = I.L;
+  for (u32 r = 0; r < n && c > 0; r++) {
+    const u64 a0 = D[(r + 1) * cols + c];
+    if (t < a0) continue;
+    t -= a0;
+    const A5xMKey K = T.keys[S.pat[r]];
+    u32 v = 0;
+    if (mode == A5X_MODE_SUBALL && K.nvals > 1) {
+      const u64 b = D[(r + 1) * cols + c - 1];
+      v = (u32)(t / b);
+      t -= (u64)v * b;
+    }
+    const A5xMVal V = T.vals[K.val_base + v];
+    len = m_replace_all(src, len, T.blob + K.key_off, K.klen, T.blob + V.off, V.len, dst, err);
+    src = dst;
+    dst = dst == b0 ? b1 : b0;
+    c--;
+  }
+  *outp = src;
+  return len;
+}
+
+__device__ __forceinline__ void m_err(u32* e, u32 bits) {
+  if (bits && m_lane() == 0) atomicOr(e, bits);
+}
+
+extern __shared__ __attribute__((aligned(16))) uint8_t m_dyn[];
+
+// one wave per word: count, segments, per-word error flags
+__global__ void __launch_bounds__(64) k_mode_count(A5xModeLaunch a) {
+  MLds& S = *(MLds*)m_dyn;
+  const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
+  for (u64 w = blockIdx.x; w < a.nw; w += gridDim.x) {
+    const MInfo I = m_setup(S, T, a, w);
+    if (m_lane() == 0) {
+      const u64 cnt = I.bad ? 0 : I.count;
+      a.count[w] = cnt;
+      a.nseg[w] = (cnt + a.SEG - 1) / a.SEG;
+      a.flags[w] = I.bad == M_ERR_OVF ? A5X_WF_ERR_OVF : (I.bad ? A5X_WF_ERR_BIG : 0u);
+    }
+    m_err(a.err, I.bad);
+  }
+}
+
+// Run the candidates [t0, t0 + nc) of the set-up word: op 0 = sum of (len+1),
+// op 1 = write them at out[base + prefix - out_base] when their global index
+// (g0 + t) is inside [cand_begin, cand_end).
+__device__ u64 m_run(MLds& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 t0, u32 nc, int op,
+                     u64 g0, u64 base, u32& err) {
+  const u32 lane = m_lane();
+  u64 run = 0;
+  for (u32 k0 = 0; k0 < nc; k0 += 64) {
+    const u32 k = k0 + lane;
+    const bool v = k < nc;
+    const uint8_t* p = nullptr;
+    u32 len = 0;
+    if (v) len = m_build(S, T, I, a.mode, t0 + k, &p, err) + 1;
+    const u32 incl = m_incl_scan(len);
+    const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    if (op == 1 && v) {
+      const u64 g = g0 + t0 + k;
+      if (g >= a.cand_begin && g < a.cand_end) {
+        const u64 pos = base + run + (incl - len) - a.out_base;
+        if (pos + len > a.out_cap) {
+          err |= M_ERR_GUARD;
+        } else {
+          uint8_t* o = a.out + pos;
+          for (u32 i = 0; i + 1 < len; i++) o[i] = p[i];
+          o[len - 1] = '\n';
+        }
+      }
+    }
+    run += tot;
+  }
+  return run;
+}
+
+// one wave per item (word, SEG-candidate segment): op 0 = seg_bytes, op 1 = expand
+__global__ void __launch_bounds__(64) k_mode_items(A5xModeLaunch a, int op) {
+  MLds& S = *(MLds*)m_dyn;
+  const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
+  for (u64 i = a.item_begin + blockIdx.x; i < a.item_end; i += gridDim.x) {
+    const u64 w = a.item_w[i];
+    const u64 cw0 = a.cand_off[w], cnt = a.cand_off[w + 1] - cw0;
+    const u64 t0 = (i - a.seg_off[w]) * a.SEG;
+    if (t0 >= cnt) { m_err(a.err, M_ERR_STATE); continue; }
+    const u32 nc = (u32)min(a.SEG, cnt - t0);
+    const MInfo I = m_setup(S, T, a, w);
+    if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); continue; }
+    u32 err = 0;
+    const u64 base = op == 1 ? a.seg_boff[i] : 0;
+    const u64 run = m_run(S, T, I, a, t0, nc, op, cw0, base, err);
+    if (op == 0 && m_lane() == 0) a.seg_bytes[i] = run;
+    m_err(a.err, m_wave_or(err));
+  }
+}
+
+// one wave per query g: {item containing g, index inside the item, byte offset of g}
+__global__ void __launch_bounds__(64) k_mode_locate(A5xModeLaunch a, const u64* cands, u32 nq, u64* out) {
+  MLds& S = *(MLds*)m_dyn;
+  const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
+  for (u32 q = blockIdx.x; q < nq; q += gridDim.x) {
+    const u64 g = cands[q];
+    const u64 total = a.cand_off[a.nw];
+    if (g >= total) {
+      if (m_lane() == 0) { out[3 * q] = a.nitems; out[3 * q + 1] = 0; out[3 * q + 2] = a.seg_boff[a.nitems]; }
+      continue;
+    }
+    u64 lo = 0, hi = a.nw;  // largest w with cand_off[w] <= g
+    while (hi - lo > 1) {
+      const u64 mid = (lo + hi) / 2;
+      if (a.cand_off[mid] <= g) lo = mid; else hi = mid;
+    }
+    const u64 w = lo, local = g - a.cand_off[w];
+    const u64 item = a.seg_off[w] + local / a.SEG;
+    const u64 t0 = (local / a.SEG) * a.SEG;
+    const u32 r = (u32)(local - t0);
+    u64 pre = 0;
+    if (r) {
+      const MInfo I = m_setup(S, T, a, w);
+      if (I.bad || I.count != a.cand_off[w + 1] - a.cand_off[w]) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); continue; }
+      u32 err = 0;
+      pre = m_run(S, T, I, a, t0, r, 0, 0, 0, err);
+      m_err(a.err, m_wave_or(err));
+    }
+    if (m_lane() == 0) { out[3 * q] = item; out[3 * q + 1] = r; out[3 * q + 2] = a.seg_boff[item] + pre; }
+  }
+}
+
+// per-word byte offsets / bytes from the per-item byte offsets
+__global__ void __launch_bounds__(256) k_mode_wordbytes(const u64* seg_off, const u64* seg_boff, u64 nw,
+                                                        u64* byte_off, u64* bytes) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w <= nw; w += stride) {
+    const u64 b = seg_boff[seg_off[w]];
+    byte_off[w] = b;
+    if (w < nw && bytes) bytes[w] = seg_boff[seg_off[w + 1]] - b;
+  }
+}
+
+inline u32 m_grid(u64 n, u32 cap) { return (u32)(n < 1 ? 1 : (n < cap ? n : cap)); }
+
+}  // namespace
+
+size_t a5x_mode_lds(uint32_t mtab_bytes) { return sizeof(MLds) + ((mtab_bytes + 15u) & ~15u); }
+
+hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st) {
+  hipLaunchKernelGGL(k_mode_count, dim3(m_grid(L.nw, 1u << 18)), dim3(64), a5x_mode_lds(L.mtab_bytes), st, L);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st) {
+  if (L.item_end <= L.item_begin) return hipSuccess;
+  hipLaunchKernelGGL(k_mode_items, dim3(m_grid(L.item_end - L.item_begin, 1u << 18)), dim3(64),
+                     a5x_mode_lds(L.mtab_bytes), st, L, op);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_mode_locate(const A5xModeLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(k_mode_locate, dim3(m_grid(n, 64)), dim3(64), a5x_mode_lds(L.mtab_bytes), st, L, cands, n, out);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_mode_wordbytes(const uint64_t* seg_off, const uint64_t* seg_boff, uint64_t nw,
+                                     uint64_t* byte_off, uint64_t* bytes, hipStream_t st) {
+  hipLaunchKernelGGL(k_mode_wordbytes, dim3(m_grid((nw + 256) / 256, 65536)), dim3(256), 0, st, seg_off, seg_boff,
+                     nw, byte_off, bytes);
+  return hipGetLastError();
+}

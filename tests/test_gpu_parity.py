@@ -195,9 +195,9 @@ def test_overflow_is_reported(gpu_ctx):
     assert "OVERFLOW" in str(e.value)
 
 
-def test_unsupported_mode_fails_loudly(gpu_ctx):
+def test_bad_mode_fails_loudly(gpu_ctx):
     from hashcat_a5_table_generator_amd import A5xError, pack_words
     gpu_ctx.set_table({b"a": [b"b"]})
     data, offs = pack_words([b"abc"])
     with pytest.raises(A5xError):
-        gpu_ctx.expand(data, offs, 2, 0, 15)
+        gpu_ctx.expand(data, offs, 7, 0, 15)
