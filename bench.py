@@ -38,6 +38,10 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+MODE_NAMES = {0: "processWord (default)", 1: "processWordReverse (-r)", 2: "processWordSubstituteAll (-s)",
+              3: "processWordSubstituteAllReverse (-s -r)"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -47,6 +51,8 @@ def parse():
     ap.add_argument("--words", type=int, default=10_000_000, help="words per GPU")
     ap.add_argument("--min", type=int, default=0)
     ap.add_argument("--max", type=int, default=15)
+    ap.add_argument("--mode", type=int, default=0, choices=(0, 1, 2, 3),
+                    help="0 processWord (headline), 1 -r, 2 -s, 3 -s -r (main.go:80-92)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-words", type=int, default=50_000)
     ap.add_argument("--verify", action="store_true", help="digest-check the last step against the C oracle")
@@ -110,7 +116,7 @@ def cpu_baseline(tables, args):
         nwords = args.cpu_sample_words if th == 1 else max(1000, args.cpu_sample_words // 5)
         _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
         t0 = time.perf_counter()
-        c, b = t.run_pipeline(data, offs, 0, args.min, args.max, th, fd)
+        c, b = t.run_pipeline(data, offs, args.mode, args.min, args.max, th, fd)
         dt = time.perf_counter() - t0
         r = {"value": c / dt, "unit": "candidates/s", "cores": th, "kind": "port",
              "sample": f"{nwords} words of workload {args.workload} (seed 0xC0FFEE): {c} candidates, "
@@ -135,13 +141,13 @@ def main():
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)
     do = DeviceBuffer.from_array(ctx, offs)
-    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, 0, args.min, args.max)
+    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max)
     log(f"rank {D.rank}: {ctx.device_name}: {n} words -> {tc} candidates, {tb / 1e9:.2f} GB")
     out = DeviceBuffer(ctx, max(tb, 16))
     boff = DeviceBuffer(ctx, (n + 1) * 8)
 
     def step():
-        return ctx.expand_device(dw.ptr, do.ptr, n, out.ptr, tb, 0, args.min, args.max, d_byte_off=boff.ptr)
+        return ctx.expand_device(dw.ptr, do.ptr, n, out.ptr, tb, args.mode, args.min, args.max, d_byte_off=boff.ptr)
 
     for _ in range(args.warmup):
         step()
@@ -165,7 +171,7 @@ def main():
         ctx.digest_device(out.ptr, boff.ptr, 0, n, dig.ptr)
         got = dig.to_array(np.uint64).reshape(n, 4)
         want = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables]
-                         ).digest_batch(data, offs, 0, args.min, args.max)
+                         ).digest_batch(data, offs, args.mode, args.min, args.max)
         bad = int((got != want).any(axis=1).sum())
         log(f"verify: {bad} mismatching words of {n}")
         if bad:
@@ -173,7 +179,7 @@ def main():
 
     if D.rank == 0:
         achieved = tb / (ms_exp * 1e-3) / 1e9  # GB/s, algorithmic bytes per launch / launch time
-        prof = latest_profile_traffic(args.workload)
+        prof = latest_profile_traffic(args.workload) if args.mode == 0 else None
         traffic = None
         if prof:
             traffic = prof["bytes_per_launch"]
@@ -199,7 +205,7 @@ def main():
                 "bytes_per_gpu_step": tb,
                 "table_min": args.min,
                 "table_max": args.max,
-                "mode": "processWord (default)",
+                "mode": MODE_NAMES[args.mode],
                 "parallelism": f"weak: {D.world} x independent word shards, no data-path collective",
             },
             "roofline": {
@@ -209,7 +215,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_expand_fast+k_expand_slow+k_expand_b (launched when present)",
+                "kernel": ("k_expand_fast+k_expand_slow+k_expand_b (launched when present)" if args.mode == 0
+                           else "k_mode_items (expansion pass)"),
                 "ms_per_launch": ms_exp,
                 "ms_per_launch_max_rank": ms_exp_max,
                 "ms_keyspace_scan_plan": ms_ks,

@@ -28,6 +28,7 @@ EXPORTS = (
     "a5x_split_words", "a5x_keyspace", "a5x_expand", "a5x_expand_device", "a5x_keyspace_device",
     "a5x_digest_device", "a5x_partition", "a5x_dev_alloc", "a5x_dev_free", "a5x_memcpy_h2d",
     "a5x_memcpy_d2h", "a5x_synchronize", "a5x_debug_stamps", "a5x_debug_plan_word",
+    "a5x_set_targets", "a5x_expand_digest", "a5x_expand_digest_device", "a5x_digest_lines_device",
 )
 
 
@@ -46,6 +47,11 @@ class Stats(ctypes.Structure):
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+class Hit(ctypes.Structure):
+    """a5x_hit: word index, candidate index inside the word, digest."""
+    _fields_ = [("word", ctypes.c_uint64), ("cand", ctypes.c_uint64), ("digest", ctypes.c_uint8 * 16)]
 
 
 SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t)
@@ -96,6 +102,11 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     L.a5x_synchronize.argtypes = [vp]
     L.a5x_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i]
     L.a5x_debug_plan_word.argtypes = [vp, vp, sz, i, i, vp, sz, vp]
+    L.a5x_set_targets.argtypes = [vp, i, vp, u64]
+    L.a5x_expand_digest.argtypes = [vp, vp, vp, u64, i, i, i, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(Stats)]
+    L.a5x_expand_digest_device.argtypes = [vp, vp, vp, u64, i, i, i, u64, vp, u64, ctypes.POINTER(u64),
+                                           ctypes.POINTER(Stats), vp]
+    L.a5x_digest_lines_device.argtypes = [vp, i, vp, u64, vp, u64, ctypes.POINTER(u64), vp]
     _lib = L
     return L
 

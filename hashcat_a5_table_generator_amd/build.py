@@ -19,7 +19,7 @@ LIB = os.path.join(OUT, "liba5x.so")
 CLI = os.path.join(OUT, "a5x_generator")
 ARCH = os.environ.get("A5X_OFFLOAD_ARCH", "gfx950")
 
-LIB_SRCS = ["a5x_kernels.hip", "a5x_modes.hip", "a5x_host.cpp"]
+LIB_SRCS = ["a5x_kernels.hip", "a5x_modes.hip", "a5x_digest.hip", "a5x_host.cpp"]
 HEADERS = ["a5x_format.h", "a5x_gosem.h", "a5x_launch.h", "a5x_plan.h"]
 
 

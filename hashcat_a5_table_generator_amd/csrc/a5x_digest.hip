@@ -1,0 +1,383 @@
+// a5x_digest.hip -- fused digest + lookup over an expanded candidate stream.
+//
+// No counterpart in the reference: main.go only prints candidates (main.go:66) and
+// hashcat hashes them (README.MD:69).  Here the "cand\n" stream that the expansion
+// kernels leave in HBM is hashed on the device, so candidates never round-trip to the
+// host:
+//   MD5   RFC 1321 over the candidate bytes (== Go crypto/md5);
+//   NTLM  MD4 (RFC 1320) over UTF-16LE of the candidate decoded as Go does for
+//         []rune(string): invalid UTF-8 byte -> U+FFFD, runes > U+FFFF -> surrogate
+//         pairs (unicode/utf16.Encode).
+// Each digest is probed against a device-resident target set: a 2^k-bit prefilter
+// indexed by digest word 0, then an open-addressing table of 16-B digests.
+//
+// Work unit: one wave per 2 KiB block of the stream.  The wave stages the block (+256 B
+// of the next one) in LDS, finds line starts with a SWAR newline test (exact per byte),
+// compacts them into an ordered start list, and every lane hashes one candidate at a
+// time; the candidate owned by a block is the one STARTING in it.  A hit records
+// (block, ordinal in block, digest); a per-block start count + scan turns that into
+// the global candidate index afterwards (hits are rare).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "a5x.h"
+#include "a5x_launch.h"
+
+namespace {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+constexpr u32 DBLK = 2048;                 // stream bytes per wave
+constexpr u32 DMARGIN = 256;               // next-block bytes staged for straddling lines
+constexpr u32 DBUF = DBLK + DMARGIN + 80;  // + slack for the 8-B over-reads of the loader
+constexpr u32 USTRIDE = 132;               // NTLM UTF-16 buffer per lane (64 units + pad)
+constexpr u32 UMAX = 128;                  // UTF-16LE bytes per candidate (64 units)
+constexpr u32 D_ERR_LONG = 1u << 9;        // an NTLM candidate beyond 64 UTF-16 units
+constexpr u32 D_ERR_HITCAP = 1u << 10;     // more hits than the caller's buffer
+
+__device__ __forceinline__ u32 d_lane() { return __lane_id(); }
+
+__device__ __forceinline__ u32 d_incl_scan(u32 x) {
+  const u32 lane = d_lane();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 y = (u32)__shfl_up((int)x, d, 64);
+    if ((int)lane >= d) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ u32 rotl(u32 x, u32 s) { return __builtin_amdgcn_alignbit(x, x, 32u - s); }
+
+// ---------------------------------------------------------------------------
+// MD5 (RFC 1321) and MD4 (RFC 1320) compression functions
+// ---------------------------------------------------------------------------
+#define MD5_STEP(f, a, b, c, d, x, t, s) \
+  a += f(b, c, d) + (x) + (t);           \
+  a = rotl(a, s) + b;
+#define MD5_F(x, y, z) (((x) & (y)) | (~(x) & (z)))
+#define MD5_G(x, y, z) (((x) & (z)) | ((y) & ~(z)))
+#define MD5_H(x, y, z) ((x) ^ (y) ^ (z))
+#define MD5_I(x, y, z) ((y) ^ ((x) | ~(z)))
+
+__device__ __forceinline__ void md5_block(u32* st, const u32* M) {
+  u32 a = st[0], b = st[1], c = st[2], d = st[3];
+  MD5_STEP(MD5_F, a, b, c, d, M[0], 0xd76aa478u, 7) MD5_STEP(MD5_F, d, a, b, c, M[1], 0xe8c7b756u, 12)
+  MD5_STEP(MD5_F, c, d, a, b, M[2], 0x242070dbu, 17) MD5_STEP(MD5_F, b, c, d, a, M[3], 0xc1bdceeeu, 22)
+  MD5_STEP(MD5_F, a, b, c, d, M[4], 0xf57c0fafu, 7) MD5_STEP(MD5_F, d, a, b, c, M[5], 0x4787c62au, 12)
+  MD5_STEP(MD5_F, c, d, a, b, M[6], 0xa8304613u, 17) MD5_STEP(MD5_F, b, c, d, a, M[7], 0xfd469501u, 22)
+  MD5_STEP(MD5_F, a, b, c, d, M[8], 0x698098d8u, 7) MD5_STEP(MD5_F, d, a, b, c, M[9], 0x8b44f7afu, 12)
+  MD5_STEP(MD5_F, c, d, a, b, M[10], 0xffff5bb1u, 17) MD5_STEP(MD5_F, b, c, d, a, M[11], 0x895cd7beu, 22)
+  MD5_STEP(MD5_F, a, b, c, d, M[12], 0x6b901122u, 7) MD5_STEP(MD5_F, d, a, b, c, M[13], 0xfd987193u, 12)
+  MD5_STEP(MD5_F, c, d, a, b, M[14], 0xa679438eu, 17) MD5_STEP(MD5_F, b, c, d, a, M[15], 0x49b40821u, 22)
+  MD5_STEP(MD5_G, a, b, c, d, M[1], 0xf61e2562u, 5) MD5_STEP(MD5_G, d, a, b, c, M[6], 0xc040b340u, 9)
+  MD5_STEP(MD5_G, c, d, a, b, M[11], 0x265e5a51u, 14) MD5_STEP(MD5_G, b, c, d, a, M[0], 0xe9b6c7aau, 20)
+  MD5_STEP(MD5_G, a, b, c, d, M[5], 0xd62f105du, 5) MD5_STEP(MD5_G, d, a, b, c, M[10], 0x02441453u, 9)
+  MD5_STEP(MD5_G, c, d, a, b, M[15], 0xd8a1e681u, 14) MD5_STEP(MD5_G, b, c, d, a, M[4], 0xe7d3fbc8u, 20)
+  MD5_STEP(MD5_G, a, b, c, d, M[9], 0x21e1cde6u, 5) MD5_STEP(MD5_G, d, a, b, c, M[14], 0xc33707d6u, 9)
+  MD5_STEP(MD5_G, c, d, a, b, M[3], 0xf4d50d87u, 14) MD5_STEP(MD5_G, b, c, d, a, M[8], 0x455a14edu, 20)
+  MD5_STEP(MD5_G, a, b, c, d, M[13], 0xa9e3e905u, 5) MD5_STEP(MD5_G, d, a, b, c, M[2], 0xfcefa3f8u, 9)
+  MD5_STEP(MD5_G, c, d, a, b, M[7], 0x676f02d9u, 14) MD5_STEP(MD5_G, b, c, d, a, M[12], 0x8d2a4c8au, 20)
+  MD5_STEP(MD5_H, a, b, c, d, M[5], 0xfffa3942u, 4) MD5_STEP(MD5_H, d, a, b, c, M[8], 0x8771f681u, 11)
+  MD5_STEP(MD5_H, c, d, a, b, M[11], 0x6d9d6122u, 16) MD5_STEP(MD5_H, b, c, d, a, M[14], 0xfde5380cu, 23)
+  MD5_STEP(MD5_H, a, b, c, d, M[1], 0xa4beea44u, 4) MD5_STEP(MD5_H, d, a, b, c, M[4], 0x4bdecfa9u, 11)
+  MD5_STEP(MD5_H, c, d, a, b, M[7], 0xf6bb4b60u, 16) MD5_STEP(MD5_H, b, c, d, a, M[10], 0xbebfbc70u, 23)
+  MD5_STEP(MD5_H, a, b, c, d, M[13], 0x289b7ec6u, 4) MD5_STEP(MD5_H, d, a, b, c, M[0], 0xeaa127fau, 11)
+  MD5_STEP(MD5_H, c, d, a, b, M[3], 0xd4ef3085u, 16) MD5_STEP(MD5_H, b, c, d, a, M[6], 0x04881d05u, 23)
+  MD5_STEP(MD5_H, a, b, c, d, M[9], 0xd9d4d039u, 4) MD5_STEP(MD5_H, d, a, b, c, M[12], 0xe6db99e5u, 11)
+  MD5_STEP(MD5_H, c, d, a, b, M[15], 0x1fa27cf8u, 16) MD5_STEP(MD5_H, b, c, d, a, M[2], 0xc4ac5665u, 23)
+  MD5_STEP(MD5_I, a, b, c, d, M[0], 0xf4292244u, 6) MD5_STEP(MD5_I, d, a, b, c, M[7], 0x432aff97u, 10)
+  MD5_STEP(MD5_I, c, d, a, b, M[14], 0xab9423a7u, 15) MD5_STEP(MD5_I, b, c, d, a, M[5], 0xfc93a039u, 21)
+  MD5_STEP(MD5_I, a, b, c, d, M[12], 0x655b59c3u, 6) MD5_STEP(MD5_I, d, a, b, c, M[3], 0x8f0ccc92u, 10)
+  MD5_STEP(MD5_I, c, d, a, b, M[10], 0xffeff47du, 15) MD5_STEP(MD5_I, b, c, d, a, M[1], 0x85845dd1u, 21)
+  MD5_STEP(MD5_I, a, b, c, d, M[8], 0x6fa87e4fu, 6) MD5_STEP(MD5_I, d, a, b, c, M[15], 0xfe2ce6e0u, 10)
+  MD5_STEP(MD5_I, c, d, a, b, M[6], 0xa3014314u, 15) MD5_STEP(MD5_I, b, c, d, a, M[13], 0x4e0811a1u, 21)
+  MD5_STEP(MD5_I, a, b, c, d, M[4], 0xf7537e82u, 6) MD5_STEP(MD5_I, d, a, b, c, M[11], 0xbd3af235u, 10)
+  MD5_STEP(MD5_I, c, d, a, b, M[2], 0x2ad7d2bbu, 15) MD5_STEP(MD5_I, b, c, d, a, M[9], 0xeb86d391u, 21)
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+}
+
+#define MD4_F(x, y, z) (((x) & (y)) | (~(x) & (z)))
+#define MD4_G(x, y, z) (((x) & (y)) | ((x) & (z)) | ((y) & (z)))
+#define MD4_H(x, y, z) ((x) ^ (y) ^ (z))
+#define MD4_R1(a, b, c, d, k, s) a = rotl(a + MD4_F(b, c, d) + M[k], s);
+#define MD4_R2(a, b, c, d, k, s) a = rotl(a + MD4_G(b, c, d) + M[k] + 0x5a827999u, s);
+#define MD4_R3(a, b, c, d, k, s) a = rotl(a + MD4_H(b, c, d) + M[k] + 0x6ed9eba1u, s);
+
+__device__ __forceinline__ void md4_block(u32* st, const u32* M) {
+  u32 a = st[0], b = st[1], c = st[2], d = st[3];
+  MD4_R1(a, b, c, d, 0, 3) MD4_R1(d, a, b, c, 1, 7) MD4_R1(c, d, a, b, 2, 11) MD4_R1(b, c, d, a, 3, 19)
+  MD4_R1(a, b, c, d, 4, 3) MD4_R1(d, a, b, c, 5, 7) MD4_R1(c, d, a, b, 6, 11) MD4_R1(b, c, d, a, 7, 19)
+  MD4_R1(a, b, c, d, 8, 3) MD4_R1(d, a, b, c, 9, 7) MD4_R1(c, d, a, b, 10, 11) MD4_R1(b, c, d, a, 11, 19)
+  MD4_R1(a, b, c, d, 12, 3) MD4_R1(d, a, b, c, 13, 7) MD4_R1(c, d, a, b, 14, 11) MD4_R1(b, c, d, a, 15, 19)
+  MD4_R2(a, b, c, d, 0, 3) MD4_R2(d, a, b, c, 4, 5) MD4_R2(c, d, a, b, 8, 9) MD4_R2(b, c, d, a, 12, 13)
+  MD4_R2(a, b, c, d, 1, 3) MD4_R2(d, a, b, c, 5, 5) MD4_R2(c, d, a, b, 9, 9) MD4_R2(b, c, d, a, 13, 13)
+  MD4_R2(a, b, c, d, 2, 3) MD4_R2(d, a, b, c, 6, 5) MD4_R2(c, d, a, b, 10, 9) MD4_R2(b, c, d, a, 14, 13)
+  MD4_R2(a, b, c, d, 3, 3) MD4_R2(d, a, b, c, 7, 5) MD4_R2(c, d, a, b, 11, 9) MD4_R2(b, c, d, a, 15, 13)
+  MD4_R3(a, b, c, d, 0, 3) MD4_R3(d, a, b, c, 8, 9) MD4_R3(c, d, a, b, 4, 11) MD4_R3(b, c, d, a, 12, 15)
+  MD4_R3(a, b, c, d, 2, 3) MD4_R3(d, a, b, c, 10, 9) MD4_R3(c, d, a, b, 6, 11) MD4_R3(b, c, d, a, 14, 15)
+  MD4_R3(a, b, c, d, 1, 3) MD4_R3(d, a, b, c, 9, 9) MD4_R3(c, d, a, b, 5, 11) MD4_R3(b, c, d, a, 13, 15)
+  MD4_R3(a, b, c, d, 3, 3) MD4_R3(d, a, b, c, 11, 9) MD4_R3(c, d, a, b, 7, 11) MD4_R3(b, c, d, a, 15, 15)
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+}
+
+// 4 message bytes at byte offset off of an LDS buffer (two aligned reads + funnel shift)
+__device__ __forceinline__ u32 lds4(const uint8_t* base, u32 off) {
+  const u32* p = (const u32*)(base + (off & ~3u));
+  return __builtin_amdgcn_alignbyte(p[1], p[0], off & 3u);
+}
+
+__device__ __forceinline__ u32 glob4(const uint8_t* base, u64 off, u64 lim) {
+  u32 v = 0;
+  for (u32 k = 0; k < 4; k++)
+    if (off + k < lim) v |= (u32)base[off + k] << (8 * k);
+  return v;
+}
+
+// Merkle-Damgard over message bytes [0, len) of src (LDS, or global when lds == false):
+// RFC 1321/1320 padding (0x80, zeros, 64-bit little-endian bit length).
+template <bool MD5>
+__device__ __forceinline__ void md_digest(const uint8_t* lbase, u32 loff, const uint8_t* gbase, u64 goff, u64 glim,
+                                          bool lds, u32 len, u32* st) {
+  st[0] = 0x67452301u; st[1] = 0xefcdab89u; st[2] = 0x98badcfeu; st[3] = 0x10325476u;
+  const u32 nb = (len + 8u) / 64u + 1u;
+  for (u32 blk = 0; blk < nb; blk++) {
+    u32 M[16];
+#pragma unroll
+    for (u32 j = 0; j < 16; j++) {
+      const u32 b = blk * 64u + 4u * j;
+      const int k = (int)len - (int)b;
+      u32 raw = 0;
+      if (k > 0) raw = lds ? lds4(lbase, loff + b) : glob4(gbase, goff + b, glim);
+      const u32 keep = k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
+      const u32 pad = (k >= 0 && k < 4) ? (0x80u << (8 * k)) : 0u;
+      M[j] = (raw & keep) | pad;
+    }
+    if (blk == nb - 1) {
+      M[14] = len << 3;
+      M[15] = len >> 29;
+    }
+    if (MD5) md5_block(st, M); else md4_block(st, M);
+  }
+}
+
+// Go []rune(string) + utf16.Encode of candidate bytes into UTF-16LE bytes at dst;
+// returns the byte length, or UMAX + 2 when it does not fit.
+__device__ u32 utf16le(const uint8_t* lbase, u32 loff, const uint8_t* gbase, u64 goff, bool lds, u32 len,
+                       uint8_t* dst) {
+  auto at = [&](u32 i) -> u32 { return lds ? (u32)lbase[loff + i] : (u32)gbase[goff + i]; };
+  u32 o = 0, i = 0;
+  while (i < len) {
+    const u32 b0 = at(i);
+    u32 r = 0xFFFDu, sz = 1;
+    if (b0 < 0x80u) {
+      r = b0;
+    } else {
+      u32 size = 0, lo = 0x80u, hi = 0xBFu;
+      if (b0 >= 0xC2u && b0 <= 0xDFu) size = 2;
+      else if (b0 >= 0xE0u && b0 <= 0xEFu) { size = 3; if (b0 == 0xE0u) lo = 0xA0u; else if (b0 == 0xEDu) hi = 0x9Fu; }
+      else if (b0 >= 0xF0u && b0 <= 0xF4u) { size = 4; if (b0 == 0xF0u) lo = 0x90u; else if (b0 == 0xF4u) hi = 0x8Fu; }
+      if (size && i + size <= len) {
+        const u32 b1 = at(i + 1);
+        bool ok = b1 >= lo && b1 <= hi;
+        for (u32 k = 2; ok && k < size; k++) { const u32 bk = at(i + k); ok = bk >= 0x80u && bk <= 0xBFu; }
+        if (ok) {
+          sz = size;
+          if (size == 2) r = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
+          else if (size == 3) r = ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (at(i + 2) & 0x3Fu);
+          else r = ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((at(i + 2) & 0x3Fu) << 6) | (at(i + 3) & 0x3Fu);
+        }
+      }
+    }
+    i += sz;
+    if (r >= 0x10000u) {
+      if (o + 4 > UMAX) return UMAX + 2;
+      const u32 v = r - 0x10000u, h = 0xD800u + (v >> 10), l = 0xDC00u + (v & 0x3FFu);
+      dst[o] = (uint8_t)h; dst[o + 1] = (uint8_t)(h >> 8); dst[o + 2] = (uint8_t)l; dst[o + 3] = (uint8_t)(l >> 8);
+      o += 4;
+    } else {
+      if (o + 2 > UMAX) return UMAX + 2;
+      dst[o] = (uint8_t)r; dst[o + 1] = (uint8_t)(r >> 8);
+      o += 2;
+    }
+  }
+  return o;
+}
+
+__device__ __forceinline__ bool probe(const A5xDigLaunch& a, const u32* d) {
+  if ((d[0] | d[1] | d[2] | d[3]) == 0u) return a.has_zero_target != 0;
+  const u32 bi = d[0] & ((1u << a.bm_log2) - 1u);
+  if (!((a.bitmap[bi >> 5] >> (bi & 31u)) & 1u)) return false;
+  const u64 h = ((u64)d[1] | ((u64)d[2] << 32)) * 0x9E3779B97F4A7C15ull;
+  u64 slot = (h >> 20) & a.tmask;
+  for (u64 n = 0; n <= a.tmask; n++) {
+    const uint4 e = a.table[slot];
+    if (e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3]) return true;
+    if ((e.x | e.y | e.z | e.w) == 0u) return false;
+    slot = (slot + 1) & a.tmask;
+  }
+  return false;
+}
+
+struct DWave {
+  uint8_t data[DBUF];
+  uint16_t starts[DBLK + 2];
+};
+
+// op 0: probe targets, record hits; op 1: count line starts per block; op 2: write
+// every candidate's digest at dig_out[16 * (blk_pre[blk] + i)]
+template <bool MD5>
+__global__ void __launch_bounds__(256) k_digest_stream(A5xDigLaunch a, int op) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t d_dyn[];
+  const u32 wv = threadIdx.x / 64, lane = d_lane();
+  const u32 nwv = blockDim.x / 64;
+  const u32 per = (u32)sizeof(DWave) + (MD5 ? 0u : 64u * USTRIDE);
+  DWave& W = *(DWave*)(d_dyn + wv * ((per + 15u) & ~15u));
+  uint8_t* ubuf = (uint8_t*)&W + sizeof(DWave) + lane * USTRIDE;
+  const u64 nblk = (a.nbytes + DBLK - 1) / DBLK;
+  u32 err = 0;
+  for (u64 blk = (u64)blockIdx.x * nwv + wv; blk < nblk; blk += (u64)gridDim.x * nwv) {
+    const u64 bs = blk * DBLK;
+    const u32 bl = (u32)min<u64>(DBLK, a.nbytes - bs);                  // block bytes
+    const u32 sl = (u32)min<u64>(DBLK + DMARGIN, a.nbytes - bs);        // staged bytes
+    __builtin_amdgcn_wave_barrier();
+    // stage [bs, bs + sl) (16-B loads; the stream base is 16-B aligned, see the launcher)
+    const uint4* g16 = (const uint4*)(a.out + bs);
+    uint4* l16 = (uint4*)W.data;
+    for (u32 i = lane; i < sl / 16; i += 64) l16[i] = g16[i];
+    for (u32 i = (sl & ~15u) + lane; i < sl; i += 64) W.data[i] = a.out[bs + i];
+    for (u32 i = sl + lane; i < DBUF; i += 64) W.data[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // newline bits of this lane's 32-byte slice
+    u32 nl = 0;
+    const u32 q0 = lane * 32u;
+#pragma unroll
+    for (u32 j = 0; j < 8; j++) {
+      const u32 x = ((const u32*)W.data)[lane * 8 + j] ^ 0x0a0a0a0au;
+      const u32 t = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);  // 0x80 where the byte is '\n'
+      const u32 f = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+      nl |= f << (4 * j);
+    }
+    if (q0 + 32u > bl) nl &= q0 >= bl ? 0u : ((1u << (bl - q0)) - 1u);
+    // line starts: byte 0 of the stream, and every byte after a '\n'
+    u32 carry = (u32)__shfl_up((int)(nl >> 31), 1, 64);
+    if (lane == 0) carry = bs == 0 ? 1u : (a.out[bs - 1] == '\n' ? 1u : 0u);
+    u32 sm = (nl << 1) | carry;
+    if (q0 + 32u > bl) sm &= q0 >= bl ? 0u : ((1u << (bl - q0)) - 1u);
+    const u32 m = (u32)__builtin_popcount(sm);
+    const u32 incl = d_incl_scan(m);
+    const u32 nst = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    u32 o = incl - m;
+    for (u32 x = sm; x; x &= x - 1) W.starts[o++] = (uint16_t)(q0 + (u32)__builtin_ctz(x));
+    if (op == 1) {
+      if (lane == 0) a.blk_cnt[blk] = nst;
+      continue;
+    }
+    // end of the last line starting here: first '\n' at or after it
+    u64 tail_end = 0;
+    if (nst) {
+      const u32 s_last = W.starts[nst - 1];
+      const u32 lim = min(sl, DBLK + DMARGIN);
+      // lanes look at 64 consecutive bytes at a time
+      u64 found = ~0ull;
+      for (u32 base = s_last; base < lim && found == ~0ull; base += 64) {
+        const u32 q = base + lane;
+        const bool hit = q < lim && W.data[q] == '\n';
+        const u64 bal = __ballot(hit);
+        if (bal) found = base + (u32)__builtin_ctzll(bal);
+      }
+      if (found == ~0ull) {  // the line runs past the staged bytes: scan HBM
+        u64 g = bs + lim;
+        for (;; g += 64) {
+          const u64 q = g + lane;
+          const bool hit = q < a.nbytes && a.out[q] == '\n';
+          const u64 bal = __ballot(hit);
+          if (bal) { found = g - bs + (u32)__builtin_ctzll(bal); break; }
+          if (g + 64 >= a.nbytes) { found = a.nbytes - bs; break; }  // unterminated (not produced here)
+        }
+      }
+      tail_end = found;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (u32 i = lane; i < nst; i += 64) {
+      const u32 s = W.starts[i];
+      const u64 e = i + 1 < nst ? (u64)W.starts[i + 1] - 1 : tail_end;  // '\n' position
+      const u32 len = (u32)(e - s);
+      const bool in_lds = e + 72 <= DBUF && s + len + 72 <= DBUF;
+      u32 d[4];
+      if (MD5) {
+        md_digest<true>(W.data, s, a.out, bs + s, a.nbytes, in_lds, len, d);
+      } else {
+        const u32 ul = utf16le(W.data, s, a.out, bs + s, in_lds, len, ubuf);
+        if (ul > UMAX) { err |= D_ERR_LONG; continue; }
+        md_digest<false>(ubuf, 0, nullptr, 0, 0, true, ul, d);
+      }
+      if (op == 2) {
+        uint4* o4 = (uint4*)(a.dig_out + 16 * (a.blk_pre[blk] + i));
+        *o4 = make_uint4(d[0], d[1], d[2], d[3]);
+      } else if (probe(a, d)) {
+        const u32 h = atomicAdd(a.nhits, 1u);
+        if (h < a.hit_cap) {
+          A5xHitRaw r;
+          r.blk = blk; r.idx = i; r.d[0] = d[0]; r.d[1] = d[1]; r.d[2] = d[2]; r.d[3] = d[3];
+          a.hits[h] = r;
+        } else {
+          err |= D_ERR_HITCAP;
+        }
+      }
+    }
+  }
+  if (err) atomicOr(a.err, err);
+}
+
+// hits: (block, ordinal) -> global candidate index -> (word, candidate in word)
+__global__ void __launch_bounds__(64) k_hits_resolve(A5xHitRaw* hits, u32 n, const u64* blk_pre, u64 cand_base,
+                                                      const u64* cand_off, u64 nw) {
+  for (u32 h = blockIdx.x * 64 + threadIdx.x; h < n; h += gridDim.x * 64) {
+    A5xHitRaw r = hits[h];
+    const u64 g = cand_base + blk_pre[r.blk] + r.idx;
+    u64 lo = 0, hi = nw;  // largest w with cand_off[w] <= g
+    while (hi - lo > 1) {
+      const u64 mid = (lo + hi) / 2;
+      if (cand_off[mid] <= g) lo = mid; else hi = mid;
+    }
+    r.blk = lo;
+    r.idx = g - cand_off[lo];
+    hits[h] = r;
+  }
+}
+
+}  // namespace
+
+size_t a5x_digest_lds(int algo) {
+  const u32 per = ((u32)sizeof(DWave) + (algo == A5X_ALGO_MD5 ? 0u : 64u * USTRIDE) + 15u) & ~15u;
+  return 4u * per;
+}
+
+hipError_t a5x_launch_digest_stream(const A5xDigLaunch& L, int op, uint32_t grid, hipStream_t st) {
+  if (L.nbytes == 0) return hipSuccess;
+  if (((uintptr_t)L.out & 15u) != 0) return hipErrorInvalidValue;
+  const u64 nblk = (L.nbytes + DBLK - 1) / DBLK;
+  const u64 want = (nblk + 3) / 4;
+  const u32 g = (u32)(want < grid ? want : grid);
+  if (L.algo == A5X_ALGO_MD5)
+    hipLaunchKernelGGL(k_digest_stream<true>, dim3(g), dim3(256), a5x_digest_lds(L.algo), st, L, op);
+  else
+    hipLaunchKernelGGL(k_digest_stream<false>, dim3(g), dim3(256), a5x_digest_lds(L.algo), st, L, op);
+  return hipGetLastError();
+}
+
+uint64_t a5x_digest_blocks(uint64_t nbytes) { return (nbytes + DBLK - 1) / DBLK; }
+
+hipError_t a5x_launch_hits_resolve(A5xHitRaw* hits, uint32_t n, const uint64_t* blk_pre, uint64_t cand_base,
+                                   const uint64_t* cand_off, uint64_t nw, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_hits_resolve, dim3((n + 63) / 64 < 4096 ? (n + 63) / 64 : 4096), dim3(64), 0, st, hits, n,
+                     blk_pre, cand_base, cand_off, nw);
+  return hipGetLastError();
+}

@@ -90,6 +90,17 @@ struct a5x_ctx {
   DevBuf<uint32_t> m_item_w;
   uint64_t m_items = 0;
   uint64_t mseg = 1024;  // candidates per mode-engine item
+  // fused digest + lookup (a5x_digest.hip)
+  int t_algo = -1;
+  uint64_t n_targets = 0;
+  uint32_t t_bm_log2 = 0, t_has_zero = 0;
+  uint64_t t_tmask = 0;
+  DevBuf<uint32_t> t_bitmap;
+  DevBuf<uint4> t_table;
+  DevBuf<uint8_t> dg_scratch;
+  DevBuf<uint64_t> dg_blk_cnt, dg_blk_pre, dg_cand_off, dg_byte_off;
+  DevBuf<A5xHitRaw> dg_hits;
+  hipEvent_t dev_ev[2] = {nullptr, nullptr};
 
   DevBuf<uint64_t> count, bytes, cand_off, byte_off, scan_tmp, locate;
   DevBuf<uint32_t> flags, defer, chunk_w0, slow_list, big_list, roff, cplx;
@@ -696,6 +707,46 @@ int expand_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint
   return A5X_OK;
 }
 
+// ---------------------------------------------------------------------------
+// fused digest + lookup (a5x_digest.hip)
+// ---------------------------------------------------------------------------
+inline uint64_t tgt_slot(const uint32_t* d, uint64_t tmask) {
+  const uint64_t h = ((uint64_t)d[1] | ((uint64_t)d[2] << 32)) * 0x9E3779B97F4A7C15ull;  // == probe()
+  return (h >> 20) & tmask;
+}
+
+A5xDigLaunch dig_launch(a5x_ctx* c) {
+  A5xDigLaunch D;
+  memset(&D, 0, sizeof D);
+  D.algo = c->t_algo < 0 ? A5X_ALGO_MD5 : c->t_algo;
+  D.bitmap = c->t_bitmap.p; D.bm_log2 = c->t_bm_log2;
+  D.table = c->t_table.p; D.tmask = c->t_tmask; D.has_zero_target = c->t_has_zero;
+  D.err = c->d_scalars + 2;
+  return D;
+}
+
+uint32_t dig_grid(a5x_ctx* c) { return (uint32_t)std::max(1, c->cus) * 8u; }
+
+// per-2KiB-block line starts and their exclusive scan (blk_pre, nblk+1 entries)
+int dig_block_prefix(a5x_ctx* c, A5xDigLaunch& D, hipStream_t st, uint64_t* total_lines) {
+  int rc;
+  const uint64_t nblk = a5x_digest_blocks(D.nbytes);
+  if ((rc = grow(c, c->dg_blk_cnt, nblk + 1)) || (rc = grow(c, c->dg_blk_pre, nblk + 1)) ||
+      (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nblk + 1) + 16)))
+    return rc;
+  D.blk_cnt = c->dg_blk_cnt.p;
+  HIPCHK(c, a5x_launch_digest_stream(D, 1, dig_grid(c), st));
+  HIPCHK(c, a5x_launch_scan(c->dg_blk_cnt.p, c->dg_blk_cnt.p, nblk, c->dg_blk_pre.p, c->dg_blk_pre.p, c->scan_tmp.p,
+                            c->d_scalars + 2, st));
+  D.blk_pre = c->dg_blk_pre.p;
+  if (total_lines) {
+    HIPCHK(c, hipMemcpyAsync(c->h_totals + 2, c->dg_blk_pre.p + nblk, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    *total_lines = c->h_totals[2];
+  }
+  return A5X_OK;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -733,6 +784,7 @@ int a5x_create(int device, a5x_ctx** out) {
             hipHostMalloc((void**)&c->h_scalars, 256, 0) == hipSuccess &&
             hipHostMalloc((void**)&c->h_totals, 64, 0) == hipSuccess && a5x_set_kernel_attrs() == hipSuccess;
   for (int i = 0; i < 4 && ok; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  for (int i = 0; i < 2 && ok; i++) ok = hipEventCreate(&c->dev_ev[i]) == hipSuccess;
   if (!ok) {
     a5x_destroy(c);
     return A5X_E_HIP;
@@ -756,6 +808,10 @@ void a5x_destroy(a5x_ctx* c) {
   release(c->segs);
   release(c->m_nseg); release(c->m_seg_off); release(c->m_seg_bytes); release(c->m_seg_boff); release(c->m_tmp);
   release(c->m_item_w);
+  release(c->t_bitmap); release(c->t_table); release(c->dg_scratch); release(c->dg_blk_cnt); release(c->dg_blk_pre);
+  release(c->dg_cand_off); release(c->dg_byte_off); release(c->dg_hits);
+  for (auto& e : c->dev_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->d_mtab) (void)hipFree(c->d_mtab);
   release(c->s_words); release(c->s_out); release(c->s_woff);
   if (c->d_table) (void)hipFree(c->d_table);
@@ -1192,6 +1248,173 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
                                   (unsigned long long)pos, (unsigned long long)C.bytes);
   info[3] = pos;
   return A5X_OK;
+}
+
+int a5x_set_targets(a5x_ctx* c, int algo, const uint8_t* dig, uint64_t n) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (n && !dig)) return A5X_E_ARG;
+  if (algo != A5X_ALGO_MD5 && algo != A5X_ALGO_NTLM) return fail(c, A5X_E_ARG, "bad digest algorithm %d", algo);
+  HIPCHK(c, hipSetDevice(c->device));
+  // prefilter: >= 64 bits per target (false-positive rate <= 1/64), table: load <= 1/2
+  uint32_t bm_log2 = 16;
+  while (bm_log2 < 32 && (1ull << bm_log2) < n * 64) bm_log2++;
+  uint64_t tsz = 16;
+  while (tsz < 2 * n) tsz <<= 1;
+  std::vector<uint32_t> bm((1ull << bm_log2) / 32, 0);
+  std::vector<uint4> tab(tsz);
+  memset(tab.data(), 0, tsz * sizeof(uint4));
+  uint32_t has_zero = 0;
+  const uint64_t tmask = tsz - 1;
+  for (uint64_t i = 0; i < n; i++) {
+    uint32_t d[4];
+    memcpy(d, dig + 16 * i, 16);
+    if ((d[0] | d[1] | d[2] | d[3]) == 0) { has_zero = 1; continue; }
+    const uint32_t bi = d[0] & (uint32_t)((1ull << bm_log2) - 1);
+    bm[bi >> 5] |= 1u << (bi & 31);
+    for (uint64_t slot = tgt_slot(d, tmask);; slot = (slot + 1) & tmask) {
+      uint4& e = tab[slot];
+      if (e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3]) break;  // duplicate
+      if ((e.x | e.y | e.z | e.w) == 0) { e = make_uint4(d[0], d[1], d[2], d[3]); break; }
+    }
+  }
+  int rc;
+  if ((rc = grow(c, c->t_bitmap, bm.size())) || (rc = grow(c, c->t_table, tsz))) return rc;
+  HIPCHK(c, hipMemcpy(c->t_bitmap.p, bm.data(), bm.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->t_table.p, tab.data(), tsz * sizeof(uint4), hipMemcpyHostToDevice));
+  c->t_algo = algo;
+  c->n_targets = n;
+  c->t_bm_log2 = bm_log2;
+  c->t_tmask = tmask;
+  c->t_has_zero = has_zero;
+  return A5X_OK;
+}
+
+int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode,
+                             int mn, int mx, uint64_t scratch_bytes, a5x_hit* hits, uint64_t hit_cap,
+                             uint64_t* n_hits, a5x_stats* stats, void* stream) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!d_words || !d_woff)) || (hit_cap && !hits)) return A5X_E_ARG;
+  if (c->t_algo < 0) return fail(c, A5X_E_ARG, "no target set (a5x_set_targets)");
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if ((rc = grow(c, c->dg_cand_off, nw + 1)) || (rc = grow(c, c->dg_byte_off, nw + 1))) return rc;
+  uint64_t tc = 0, tb = 0;
+  if ((rc = a5x_keyspace_device(c, d_words, d_woff, nw, mode, mn, mx, nullptr, nullptr, &tc, &tb, st))) return rc;
+  uint64_t cap = scratch_bytes ? scratch_bytes : ((uint64_t)2 << 30);
+  cap = std::max<uint64_t>(4096, std::min<uint64_t>(cap, tb + 64));
+  if ((rc = grow(c, c->dg_scratch, cap + 64))) return rc;
+  const uint64_t dev_hits = std::max<uint64_t>(1, std::min<uint64_t>(hit_cap ? hit_cap : 1, 1u << 20));
+  if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+  a5x_stats total;
+  memset(&total, 0, sizeof total);
+  total.words = nw;
+  uint64_t found = 0;
+  double ms_dig = 0;
+  const uint64_t avg = tc ? (tb + tc - 1) / tc : 16;
+  uint64_t g = 0, step = std::max<uint64_t>(1, cap / (avg + avg / 4 + 1));
+  while (g < tc) {
+    const uint64_t ge = std::min(tc, g + step);
+    a5x_stats s;
+    rc = a5x_expand_device(c, d_words, d_woff, nw, mode, mn, mx, g, ge, c->dg_scratch.p, cap, c->dg_cand_off.p,
+                           c->dg_byte_off.p, &s, st);
+    if (rc == A5X_E_CAPACITY) {
+      if (ge - g == 1) return rc;
+      step = std::max<uint64_t>(1, (ge - g) / 2);
+      continue;
+    }
+    if (rc) return rc;
+    A5xDigLaunch D = dig_launch(c);
+    D.out = c->dg_scratch.p;
+    D.nbytes = s.bytes;
+    D.hits = c->dg_hits.p;
+    D.hit_cap = (uint32_t)dev_hits;
+    D.nhits = c->d_scalars + 8;
+    HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, st));
+    HIPCHK(c, hipEventRecord(c->dev_ev[0], st));
+    HIPCHK(c, a5x_launch_digest_stream(D, 0, dig_grid(c), st));
+    HIPCHK(c, hipEventRecord(c->dev_ev[1], st));
+    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->dev_ev[0], c->dev_ev[1]));
+    ms_dig += ms;
+    const uint32_t e = c->h_scalars[2] & ~(1u << 10);
+    if (e & (1u << 9))
+      return fail(c, A5X_E_UNSUPPORTED, "an NTLM candidate is longer than 64 UTF-16 code units (device limit)");
+    if ((rc = decode_dev_err(c, e))) return rc;
+    const uint64_t nh = c->h_scalars[8];
+    if (nh) {
+      const uint64_t got = std::min<uint64_t>(nh, dev_hits);
+      if ((rc = dig_block_prefix(c, D, st, nullptr))) return rc;
+      HIPCHK(c, a5x_launch_hits_resolve(c->dg_hits.p, (uint32_t)got, c->dg_blk_pre.p, g, c->dg_cand_off.p, nw, st));
+      const uint64_t room = found < hit_cap ? hit_cap - found : 0;
+      const uint64_t take = std::min(room, got);
+      if (take) HIPCHK(c, hipMemcpyAsync(hits + found, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, st));
+      HIPCHK(c, hipStreamSynchronize(st));
+      found += nh;
+    }
+    total.candidates += s.candidates;
+    total.bytes += s.bytes;
+    total.ms_keyspace += s.ms_keyspace;
+    total.ms_expand += s.ms_expand;
+    total.ms_total += s.ms_total + ms;
+    total.expand_launches += s.expand_launches;
+    g = ge;
+    if (s.bytes < cap / 2) step *= 2;
+  }
+  if (n_hits) *n_hits = found;
+  if (stats) *stats = total;
+  if (found > hit_cap)
+    return fail(c, A5X_E_CAPACITY, "%llu hits, buffer has %llu", (unsigned long long)found,
+                (unsigned long long)hit_cap);
+  return A5X_OK;
+}
+
+int a5x_expand_digest(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
+                      a5x_hit* hits, uint64_t hit_cap, uint64_t* n_hits, a5x_stats* stats) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!words || !woff))) return A5X_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t wbytes = nw ? woff[nw] : 0;
+  int rc;
+  if ((rc = grow(c, c->s_words, wbytes + 16)) || (rc = grow(c, c->s_woff, nw + 1))) return rc;
+  if (wbytes) HIPCHK(c, hipMemcpyAsync(c->s_words.p, words, wbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->s_woff.p, woff, (nw + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  return a5x_expand_digest_device(c, c->s_words.p, c->s_woff.p, nw, mode, mn, mx, 0, hits, hit_cap, n_hits, stats,
+                                  c->stream);
+}
+
+int a5x_digest_lines_device(a5x_ctx* c, int algo, const uint8_t* d_lines, uint64_t nbytes, uint8_t* d_dig,
+                            uint64_t cap, uint64_t* n_lines, void* stream) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nbytes && !d_lines)) return A5X_E_ARG;
+  if (algo != A5X_ALGO_MD5 && algo != A5X_ALGO_NTLM) return fail(c, A5X_E_ARG, "bad digest algorithm %d", algo);
+  if (((uintptr_t)d_lines & 15u) != 0) return fail(c, A5X_E_ARG, "d_lines must be 16-byte aligned");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (n_lines) *n_lines = 0;
+  if (!nbytes) return A5X_OK;
+  HIPCHK(c, hipMemsetAsync(c->d_scalars, 0, 64, st));
+  A5xDigLaunch D = dig_launch(c);
+  D.algo = algo;
+  D.out = d_lines;
+  D.nbytes = nbytes;
+  uint64_t lines = 0;
+  int rc;
+  if ((rc = dig_block_prefix(c, D, st, &lines))) return rc;
+  if (n_lines) *n_lines = lines;
+  if (lines > cap || !d_dig)
+    return fail(c, A5X_E_CAPACITY, "%llu lines, digest buffer has room for %llu", (unsigned long long)lines,
+                (unsigned long long)cap);
+  D.dig_out = d_dig;
+  HIPCHK(c, a5x_launch_digest_stream(D, 2, dig_grid(c), st));
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if (c->h_scalars[2] & (1u << 9))
+    return fail(c, A5X_E_UNSUPPORTED, "an NTLM candidate is longer than 64 UTF-16 code units (device limit)");
+  return decode_dev_err(c, c->h_scalars[2]);
 }
 
 int a5x_partition(const uint64_t* prefix, uint64_t n, uint32_t parts, uint64_t* split) {

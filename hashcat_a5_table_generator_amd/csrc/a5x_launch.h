@@ -113,3 +113,32 @@ hipError_t a5x_launch_mode_locate(const A5xModeLaunch& L, const uint64_t* cands,
                                   hipStream_t st);
 hipError_t a5x_launch_mode_wordbytes(const uint64_t* seg_off, const uint64_t* seg_boff, uint64_t nw,
                                      uint64_t* byte_off, uint64_t* bytes, hipStream_t st);
+
+// ---- fused digest + lookup (a5x_digest.hip) ----------------------------------
+struct A5xHitRaw {  // (block, ordinal) until k_hits_resolve, then (word, candidate in word)
+  uint64_t blk;
+  uint64_t idx;
+  uint32_t d[4];
+};
+struct A5xDigLaunch {
+  const uint8_t* out;  // "cand\n" stream, 16-B aligned, starts at a candidate
+  uint64_t nbytes;
+  int algo;            // A5X_ALGO_MD5 / A5X_ALGO_NTLM
+  const uint32_t* bitmap;
+  uint32_t bm_log2;
+  const uint4* table;  // open addressing, all-zero = empty
+  uint64_t tmask;
+  uint32_t has_zero_target;
+  A5xHitRaw* hits;
+  uint32_t* nhits;
+  uint32_t hit_cap;
+  uint64_t* blk_cnt;        // op 1 output (per 2 KiB block line starts)
+  const uint64_t* blk_pre;  // op 2 / resolve input (exclusive scan of blk_cnt)
+  uint8_t* dig_out;         // op 2 output: 16 B per candidate
+  uint32_t* err;
+};
+size_t a5x_digest_lds(int algo);
+uint64_t a5x_digest_blocks(uint64_t nbytes);
+hipError_t a5x_launch_digest_stream(const A5xDigLaunch& L, int op, uint32_t grid, hipStream_t st);
+hipError_t a5x_launch_hits_resolve(A5xHitRaw* hits, uint32_t n, const uint64_t* blk_pre, uint64_t cand_base,
+                                   const uint64_t* cand_off, uint64_t nw, hipStream_t st);

@@ -34,6 +34,8 @@ MODE_DEFAULT = 0
 MODE_REVERSE = 1
 MODE_SUBALL = 2
 MODE_SUBALL_REVERSE = 3
+ALGO_MD5 = 0   # RFC 1321 (Go crypto/md5)
+ALGO_NTLM = 1  # MD4 over UTF-16LE ([]rune + utf16.Encode)
 
 SubMap = Dict[bytes, List[bytes]]
 
@@ -205,6 +207,48 @@ class Context:
                                             d_out or None, out_cap, d_cand_off or None, d_byte_off or None,
                                             ctypes.byref(st), stream or None))
         return st.as_dict()
+
+    # ---- fused digest + lookup ----------------------------------
+    def set_targets(self, algo: int, digests) -> None:
+        """Device target set from 16-byte digests (bytes of length 16*n or an (n,16) uint8 array)."""
+        buf = np.ascontiguousarray(np.frombuffer(bytes(digests), dtype=np.uint8) if isinstance(digests, (bytes, bytearray))
+                                   else np.asarray(digests, dtype=np.uint8)).reshape(-1)
+        if buf.size % 16:
+            raise ValueError("digests must be 16 bytes each")
+        self._chk(self._L.a5x_set_targets(self.h, algo, buf.ctypes.data if buf.size else None, buf.size // 16))
+
+    @staticmethod
+    def _hits(arr, n) -> List[Tuple[int, int, bytes]]:
+        return [(int(h.word), int(h.cand), bytes(h.digest)) for h in arr[:n]]
+
+    def expand_digest(self, words: np.ndarray, offs: np.ndarray, mode: int = MODE_DEFAULT, mn: int = 0,
+                      mx: int = 15, hit_cap: int = 1 << 16) -> Tuple[List[Tuple[int, int, bytes]], dict]:
+        """Expand + hash + probe on the device; returns ([(word, cand_in_word, digest)], stats)."""
+        arr = (_lib.Hit * max(1, hit_cap))()
+        nh = ctypes.c_uint64()
+        st = Stats()
+        self._chk(self._L.a5x_expand_digest(self.h, words.ctypes.data, offs.ctypes.data, len(offs) - 1, mode, mn, mx,
+                                            arr, hit_cap, ctypes.byref(nh), ctypes.byref(st)))
+        return self._hits(arr, min(nh.value, hit_cap)), st.as_dict()
+
+    def expand_digest_device(self, d_words: int, d_offs: int, n_words: int, mode: int = MODE_DEFAULT, mn: int = 0,
+                             mx: int = 15, scratch_bytes: int = 0, hit_cap: int = 1 << 16,
+                             stream: int = 0) -> Tuple[List[Tuple[int, int, bytes]], dict]:
+        arr = (_lib.Hit * max(1, hit_cap))()
+        nh = ctypes.c_uint64()
+        st = Stats()
+        self._chk(self._L.a5x_expand_digest_device(self.h, d_words, d_offs, n_words, mode, mn, mx, scratch_bytes,
+                                                   arr, hit_cap, ctypes.byref(nh), ctypes.byref(st),
+                                                   stream or None))
+        return self._hits(arr, min(nh.value, hit_cap)), st.as_dict()
+
+    def digest_lines_device(self, algo: int, d_lines: int, nbytes: int, d_digests: int, cap: int,
+                            stream: int = 0) -> int:
+        """16-byte digest of every line of a device "cand\n" stream; returns the line count."""
+        n = ctypes.c_uint64()
+        self._chk(self._L.a5x_digest_lines_device(self.h, algo, d_lines, nbytes, d_digests or None, cap,
+                                                  ctypes.byref(n), stream or None))
+        return n.value
 
     def keyspace_device(self, d_words: int, d_offs: int, n_words: int, mode: int = MODE_DEFAULT, mn: int = 0,
                         mx: int = 15, d_cand_off: int = 0, d_byte_off: int = 0, stream: int = 0) -> Tuple[int, int]:

@@ -61,6 +61,20 @@ enum {
   A5X_MODE_SUBALL_REVERSE = 3
 };
 
+/* digest algorithms of the fused digest + lookup stage */
+enum {
+  A5X_ALGO_MD5 = 0,  /* RFC 1321 over the candidate bytes (== Go crypto/md5) */
+  A5X_ALGO_NTLM = 1  /* MD4 (RFC 1320) over UTF-16LE of the candidate ([]rune + utf16.Encode) */
+};
+
+/* One target hit: word index in the batch, candidate index inside that word (in the
+ * library's per-word candidate order, the one a5x_expand emits), digest bytes. */
+typedef struct a5x_hit {
+  uint64_t word;
+  uint64_t cand;
+  uint8_t digest[16];
+} a5x_hit;
+
 typedef struct a5x_ctx a5x_ctx;
 
 /* Sink for expanded bytes: a run of complete "cand\n" lines.  Return 0 to go on. */
@@ -141,6 +155,32 @@ A5X_API int a5x_keyspace_device(a5x_ctx* ctx, const uint8_t* d_words, const uint
  * d_digest[4*w..] = {count, bytes, sum h, sum h^2}, h = fmix64(fnv1a64(cand)). */
 A5X_API int a5x_digest_device(a5x_ctx* ctx, const uint8_t* d_out, const uint64_t* d_word_byte_off, uint64_t out_base,
                               uint64_t n_words, uint64_t* d_digest, void* stream);
+
+/* ---- fused digest + lookup (no reference counterpart: hashcat
+ * hashes the candidates main.go:66 prints, README.MD:69) ----------------------- */
+/* Replace the device-resident target set: n 16-byte digests of algorithm algo
+ * (duplicates allowed).  Built on the host (prefilter bitmap + open-addressing table)
+ * and uploaded once. */
+A5X_API int a5x_set_targets(a5x_ctx* ctx, int algo, const uint8_t* digests, uint64_t n);
+/* Expand the batch (device-resident words) in ranges that fit a device scratch of
+ * scratch_bytes (0 = library default), hash every candidate on the device and probe the
+ * target set.  Hits go to hits (host memory, hit_cap entries, any order); *n_hits gets
+ * the total (which may exceed hit_cap: A5X_E_CAPACITY after filling hit_cap).
+ * stats->candidates/bytes cover the whole batch; ms_expand is expansion time,
+ * ms_total - ms_keyspace - ms_expand the digest time. */
+A5X_API int a5x_expand_digest_device(a5x_ctx* ctx, const uint8_t* d_words, const uint64_t* d_word_off,
+                                     uint64_t n_words, int mode, int min, int max, uint64_t scratch_bytes,
+                                     a5x_hit* hits, uint64_t hit_cap, uint64_t* n_hits, a5x_stats* stats,
+                                     void* stream);
+/* Host-buffer version (stages the words into HBM first). */
+A5X_API int a5x_expand_digest(a5x_ctx* ctx, const uint8_t* words, const uint64_t* word_off, uint64_t n_words,
+                              int mode, int min, int max, a5x_hit* hits, uint64_t hit_cap, uint64_t* n_hits,
+                              a5x_stats* stats);
+/* Digest of every line of a device "cand\n" stream (d_lines 16-B aligned, nbytes
+ * ending in '\n') into d_digests (16 B per line, in line order); *n_lines = lines.
+ * Verification hook for the digest kernels (tests compare with hashlib / RFC MD4). */
+A5X_API int a5x_digest_lines_device(a5x_ctx* ctx, int algo, const uint8_t* d_lines, uint64_t nbytes,
+                                    uint8_t* d_digests, uint64_t digests_cap, uint64_t* n_lines, void* stream);
 
 /* ---- multi-GPU partition --------------------------------------- */
 /* Balanced split of [0, total) for `parts` ranks from an inclusive/exclusive

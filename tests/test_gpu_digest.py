@@ -1,0 +1,109 @@
+"""GPU parity of the fused digest + lookup stage (a5x_digest.hip) through the C ABI.
+
+Digests are checked bit-exact against hashlib MD5 (== Go crypto/md5) and the RFC 1320
+MD4 restatement of oracle/digest_oracle.py (NTLM) on every candidate of expanded
+batches; lookups against planted targets must return exactly the planted
+(word, candidate) pairs and nothing else.
+"""
+import numpy as np
+import pytest
+
+from conftest import table_path
+
+pytestmark = pytest.mark.gpu
+
+
+def _rw(rng, alpha, n):
+    return np.asarray(rng.choice(alpha, size=int(n)), dtype=np.uint8).tobytes()
+
+
+def _words(seed, n, greek=False):
+    rng = np.random.default_rng(seed)
+    alpha = list("αβγδεζηθικλμνξοπρστυφχψω".encode()) if greek else list(b"abcdefghijklmnopqrstuvwxyzs")
+    out = [_rw(rng, alpha, rng.integers(1, 13)) for _ in range(n)]
+    return out + [b"", b"a", b"strasse", b"\xff\xfe", "😀ab".encode()]
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("tabs", [["czech", "german"], ["greek-hebrew"], ["qwerty-cyrillic"]])
+def test_digest_every_candidate(gpu_ctx, algo, tabs):
+    """a5x_digest_lines_device over an expanded batch == oracle digest of every line."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer, pack_words
+    from oracle import digest_oracle as dg
+    gpu_ctx.clear_table()
+    gpu_ctx.load_tables([table_path(t) for t in tabs])
+    words = _words(algo * 7 + len(tabs), 1500, greek=tabs == ["greek-hebrew"])
+    # MD5 block edges (55/56/63/64/119/120 bytes) with one substitutable letter each
+    words += [b"1" * (n - 1) + b"a" for n in (54, 55, 56, 63, 64, 119, 120, 200)]
+    data, offs = pack_words(words)
+    dw = DeviceBuffer.from_array(gpu_ctx, data)
+    do = DeviceBuffer.from_array(gpu_ctx, offs)
+    tc, tb = gpu_ctx.keyspace_device(dw.ptr, do.ptr, len(words))
+    out = DeviceBuffer(gpu_ctx, tb + 64)
+    gpu_ctx.expand_device(dw.ptr, do.ptr, len(words), out.ptr, tb)
+    stream = bytes(out.to_array(count=tb))
+    lines = stream.split(b"\n")[:-1]
+    if algo == 1:  # NTLM device limit: 64 UTF-16 units
+        keep = [ln for ln in lines if len(dg.utf16le_go(ln)) <= 128]
+        if len(keep) != len(lines):
+            stream = b"".join(x + b"\n" for x in keep)
+            lines = keep
+            out = DeviceBuffer.from_array(gpu_ctx, np.frombuffer(stream, dtype=np.uint8))
+    dig = DeviceBuffer(gpu_ctx, 16 * len(lines) + 16)
+    n = gpu_ctx.digest_lines_device(algo, out.ptr, len(stream), dig.ptr, len(lines))
+    assert n == len(lines)
+    got = dig.to_array(count=16 * n).reshape(n, 16)
+    f = dg.ALGOS[algo]
+    bad = [i for i, ln in enumerate(lines) if bytes(got[i]) != f(ln)]
+    assert not bad, [(lines[i], bytes(got[i]).hex(), f(lines[i]).hex()) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_lookup_planted_targets(gpu_ctx, algo, mode):
+    """Planted digests are found at their (word, candidate) and random digests never hit."""
+    from hashcat_a5_table_generator_amd import pack_words
+    from oracle import digest_oracle as dg
+    gpu_ctx.clear_table()
+    gpu_ctx.load_tables([table_path("czech"), table_path("german")])
+    words = _words(100 + algo, 800)
+    per_word = gpu_ctx.expand_words(words, mode, 0, 15)
+    rng = np.random.default_rng(9)
+    f = dg.ALGOS[algo]
+    planted = {}
+    for w in rng.choice(len(words), size=40, replace=False):
+        if per_word[w]:
+            c = int(rng.integers(0, len(per_word[w])))
+            planted[f(per_word[w][c])] = (int(w), c)
+    targets = list(planted) + [bytes(rng.integers(0, 256, size=16, dtype=np.uint8)) for _ in range(5000)]
+    gpu_ctx.set_targets(algo, b"".join(targets))
+    data, offs = pack_words(words)
+    hits, st = gpu_ctx.expand_digest(data, offs, mode, 0, 15)
+    assert st["candidates"] == sum(len(x) for x in per_word)
+    got = {}
+    for w, c, d in hits:
+        assert f(per_word[w][c]) == d  # the reported candidate really has that digest
+        got.setdefault(d, set()).add((w, c))
+    for d, (w, c) in planted.items():
+        assert (w, c) in got.get(d, set()), (per_word[w][c], d.hex())
+    assert set(got) == set(planted)
+
+
+def test_lookup_small_scratch_ranges(gpu_ctx):
+    """The range loop (scratch smaller than the batch output) finds the same hits."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer, pack_words
+    from oracle import digest_oracle as dg
+    gpu_ctx.clear_table()
+    gpu_ctx.load_tables([table_path("czech"), table_path("german")])
+    words = _words(5, 3000)
+    per_word = gpu_ctx.expand_words(words, 0, 0, 15)
+    pl = [(w, len(per_word[w]) - 1) for w in range(0, len(words), 97) if per_word[w]]
+    gpu_ctx.set_targets(0, b"".join(dg.md5(per_word[w][c]) for w, c in pl))
+    data, offs = pack_words(words)
+    dw = DeviceBuffer.from_array(gpu_ctx, data)
+    do = DeviceBuffer.from_array(gpu_ctx, offs)
+    hits, st = gpu_ctx.expand_digest_device(dw.ptr, do.ptr, len(words), 0, 0, 15, scratch_bytes=50_000)
+    assert st["expand_launches"] > 3
+    tg = {dg.md5(per_word[w][c]) for w, c in pl}
+    want = sorted((w, c) for w, cs in enumerate(per_word) for c, x in enumerate(cs) if dg.md5(x) in tg)
+    assert sorted((w, c) for w, c, _ in hits) == want  # every candidate with a target digest, once
