@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-words", type=int, default=50_000)
     ap.add_argument("--verify", action="store_true", help="digest-check the last step against the C oracle")
+    ap.add_argument("--digest", default="none", choices=("none", "md5", "ntlm"),
+                    help="fused expansion + digest + lookup (SURVEY 8(a) a8, configs[4]); use with --workload c5")
+    ap.add_argument("--targets", type=int, default=1_000_000, help="target digests for --digest (planted + random)")
+    ap.add_argument("--scratch-gb", type=float, default=8.0, help="device scratch for the --digest range loop")
     return ap.parse_args()
 
 
@@ -130,9 +134,108 @@ def cpu_baseline(tables, args):
     return best
 
 
+def digest_cpu_baseline(tables, args):
+    """Reference algorithm restated in C (oracle/a5_oracle.c) + per-candidate digest on one host core."""
+    from oracle import c_oracle as co
+    from oracle import digest_oracle as dg
+    from hashcat_a5_table_generator_amd import synth
+    t = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", x + ".table") for x in tables])
+    nwords = max(50, args.cpu_sample_words // (50 if args.digest == "md5" else 2000))
+    _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
+    f = dg.ALGOS[0 if args.digest == "md5" else 1]
+    t0 = time.perf_counter()
+    out, _ = t.expand_batch(data, offs, args.mode, args.min, args.max)
+    n = 0
+    for line in bytes(out).split(b"\n")[:-1]:
+        f(line)
+        n += 1
+    dt = time.perf_counter() - t0
+    log(f"cpu digest baseline: {n / dt / 1e6:.3f} Mcand/s ({dt:.2f} s)")
+    return {"value": n / dt, "unit": "candidates/s", "cores": 1, "kind": "port",
+            "sample": f"{nwords} words of workload {args.workload} (seed 0xC0FFEE): {n} candidates; C restatement "
+                      f"of main.go expansion + {'hashlib MD5' if args.digest == 'md5' else 'RFC 1320 MD4 in Python (NTLM)'}"
+                      f" per candidate, 1 thread"}
+
+
+def run_digest(args, D):
+    """Fused expansion + MD5/NTLM + target lookup over a resident batch (configs[4] shape)."""
+    from hashcat_a5_table_generator_amd import ALGO_MD5, ALGO_NTLM, Context, DeviceBuffer, pack_words, synth
+    algo = ALGO_MD5 if args.digest == "md5" else ALGO_NTLM
+    tables, (data, offs) = synth.config_words(args.workload, args.words, seed=0x5A5 + 7919 * D.rank)
+    n = len(offs) - 1
+    ctx = Context(D.local)
+    ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
+    dw = DeviceBuffer.from_array(ctx, data)
+    do = DeviceBuffer.from_array(ctx, offs)
+    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max)
+    # planted targets: one candidate of each of 1000 sampled words, digested by the device
+    rng = np.random.default_rng(0xD16E57 + D.rank)
+    sample = sorted(set(int(x) for x in rng.integers(0, n, size=1000)))
+    sw = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in sample]
+    cands = ctx.expand_words(sw, args.mode, args.min, args.max)
+    planted = [(w, int(rng.integers(0, len(c)))) for w, c in zip(sample, cands) if c]
+    lines = b"".join(cands[sample.index(w)][k] + b"\n" for w, k in planted)
+    lb = DeviceBuffer.from_array(ctx, np.frombuffer(lines, dtype=np.uint8))
+    db = DeviceBuffer(ctx, 16 * len(planted) + 16)
+    ctx.digest_lines_device(algo, lb.ptr, len(lines), db.ptr, len(planted))
+    pd = db.to_array(count=16 * len(planted)).reshape(-1, 16)
+    rand = rng.integers(0, 256, size=(max(0, args.targets - len(planted)), 16), dtype=np.uint8)
+    ctx.set_targets(algo, np.concatenate([pd, rand]))
+    scratch = int(args.scratch_gb * (1 << 30))
+    log(f"rank {D.rank}: {n} words -> {tc} candidates, {tb / 1e9:.2f} GB; {args.targets} targets "
+        f"({len(planted)} planted)")
+
+    def step():
+        return ctx.expand_digest_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max, scratch_bytes=scratch,
+                                        hit_cap=1 << 20)
+
+    for _ in range(args.warmup):
+        step()
+    D.barrier()
+    t0 = time.perf_counter()
+    res = [step() for _ in range(args.steps)]
+    D.barrier()
+    dt = time.perf_counter() - t0
+    hits, st = res[-1]
+    got = {(w, c) for w, c, _ in hits}
+    missing = [p for p in planted if p not in got]
+    if missing:
+        raise SystemExit(f"digest lookup lost {len(missing)} planted hits, e.g. {missing[:3]}")
+    dt_max = D.reduce(dt, "max")
+    cands_all = D.reduce(float(tc) * args.steps, "sum")
+    hits_all = D.reduce(float(len(hits)), "sum")
+    ms_dig = float(np.mean([s["ms_total"] - s["ms_keyspace"] - s["ms_expand"] for _, s in res]))
+    ms_exp = float(np.mean([s["ms_expand"] for _, s in res]))
+    if D.rank == 0:
+        desc = synth.CONFIGS[args.workload][3]
+        res_line = {
+            "metric": "candidates/sec (whole node) at 1/2/4/8 MI355X + % HBM write roofline",
+            "value": cands_all / dt_max, "unit": "candidates/s", "n_gpus": D.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8/u32", "data": "synthetic",
+            "config": {"workload": f"{args.workload}: {desc} + fused {args.digest.upper()} lookup (configs[4])",
+                       "tables": tables, "words_per_gpu": n, "candidates_per_gpu_step": tc, "bytes_per_gpu_step": tb,
+                       "targets": args.targets, "planted": len(planted), "hits_all_ranks": hits_all,
+                       "mode": MODE_NAMES[args.mode], "table_min": args.min, "table_max": args.max,
+                       "scratch_bytes": scratch,
+                       "parallelism": f"weak: {D.world} x independent word shards; hit counts all-reduced"},
+            "roofline": {"bound": "valu", "kernel": f"k_digest_stream<{args.digest}>",
+                         "ms_digest_per_step": ms_dig, "ms_expand_per_step": ms_exp,
+                         "digest_cand_per_s": tc / (ms_dig * 1e-3),
+                         "note": "VALU-bound; instruction counts per candidate: profiles/pmc_*digest*.json"},
+            "cpu_baseline": None if args.no_cpu_baseline else digest_cpu_baseline(tables, args),
+        }
+        print(json.dumps(res_line), flush=True)
+    D.barrier()
+    ctx.close()
+    D.close()
+
+
 def main():
     args = parse()
     D = Dist(args.gpus)
+    if args.digest != "none":
+        return run_digest(args, D)
     from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
 
     tables, (data, offs) = synth.config_words(args.workload, args.words, seed=0x5A5 + 7919 * D.rank)

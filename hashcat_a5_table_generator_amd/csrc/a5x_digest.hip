@@ -28,9 +28,10 @@ namespace {
 typedef uint64_t u64;
 typedef uint32_t u32;
 
-constexpr u32 DBLK = 2048;                 // stream bytes per wave
+// stream bytes per wave: 4 KiB for MD5 (lanes stay busy over ~3 rounds of candidates),
+// 2 KiB for NTLM (its per-lane UTF-16 buffers also live in LDS)
+template <bool MD5> struct DCfg { static constexpr u32 BLK = MD5 ? 4096u : 2048u; };
 constexpr u32 DMARGIN = 256;               // next-block bytes staged for straddling lines
-constexpr u32 DBUF = DBLK + DMARGIN + 80;  // + slack for the 8-B over-reads of the loader
 constexpr u32 USTRIDE = 132;               // NTLM UTF-16 buffer per lane (64 units + pad)
 constexpr u32 UMAX = 128;                  // UTF-16LE bytes per candidate (64 units)
 constexpr u32 D_ERR_LONG = 1u << 9;        // an NTLM candidate beyond 64 UTF-16 units
@@ -220,9 +221,11 @@ __device__ __forceinline__ bool probe(const A5xDigLaunch& a, const u32* d) {
   return false;
 }
 
+template <u32 BLK>
 struct DWave {
-  uint8_t data[DBUF];
-  uint16_t starts[DBLK + 2];
+  static constexpr u32 BUF = BLK + DMARGIN + 80;  // + slack for the 8-B over-reads of the loader
+  uint8_t data[BUF];
+  uint16_t starts[BLK + 2];
 };
 
 // op 0: probe targets, record hits; op 1: count line starts per block; op 2: write
@@ -232,9 +235,13 @@ __global__ void __launch_bounds__(256) k_digest_stream(A5xDigLaunch a, int op) {
   extern __shared__ __attribute__((aligned(16))) uint8_t d_dyn[];
   const u32 wv = threadIdx.x / 64, lane = d_lane();
   const u32 nwv = blockDim.x / 64;
-  const u32 per = (u32)sizeof(DWave) + (MD5 ? 0u : 64u * USTRIDE);
-  DWave& W = *(DWave*)(d_dyn + wv * ((per + 15u) & ~15u));
-  uint8_t* ubuf = (uint8_t*)&W + sizeof(DWave) + lane * USTRIDE;
+  constexpr u32 DBLK = DCfg<MD5>::BLK;
+  typedef DWave<DBLK> WT;
+  constexpr u32 DBUF = WT::BUF;
+  constexpr u32 NM = DBLK / 2048u;  // 32-bit newline masks per lane (32 B each)
+  const u32 per = (u32)sizeof(WT) + (MD5 ? 0u : 64u * USTRIDE);
+  WT& W = *(WT*)(d_dyn + wv * ((per + 15u) & ~15u));
+  uint8_t* ubuf = (uint8_t*)&W + sizeof(WT) + lane * USTRIDE;
   const u64 nblk = (a.nbytes + DBLK - 1) / DBLK;
   u32 err = 0;
   for (u64 blk = (u64)blockIdx.x * nwv + wv; blk < nblk; blk += (u64)gridDim.x * nwv) {
@@ -251,31 +258,40 @@ __global__ void __launch_bounds__(256) k_digest_stream(A5xDigLaunch a, int op) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // newline bits of this lane's 32-byte slice
-    u32 nl = 0;
-    const u32 q0 = lane * 32u;
+    // newline bits of this lane's slice (NM x 32 bytes)
+    const u32 q0 = lane * 32u * NM;
+    u32 nl[NM], sm[NM];
 #pragma unroll
-    for (u32 j = 0; j < 8; j++) {
-      const u32 x = ((const u32*)W.data)[lane * 8 + j] ^ 0x0a0a0a0au;
+    for (u32 h = 0; h < NM; h++) nl[h] = 0;
+#pragma unroll
+    for (u32 j = 0; j < 8 * NM; j++) {
+      const u32 x = ((const u32*)W.data)[lane * 8 * NM + j] ^ 0x0a0a0a0au;
       const u32 t = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);  // 0x80 where the byte is '\n'
       const u32 f = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
-      nl |= f << (4 * j);
+      nl[j >> 3] |= f << (4 * (j & 7));
     }
-    if (q0 + 32u > bl) nl &= q0 >= bl ? 0u : ((1u << (bl - q0)) - 1u);
+    auto keep = [&](u32 base) -> u32 {
+      return base >= bl ? 0u : (base + 32u <= bl ? 0xffffffffu : ((1u << (bl - base)) - 1u));
+    };
+#pragma unroll
+    for (u32 h = 0; h < NM; h++) nl[h] &= keep(q0 + 32u * h);
     // line starts: byte 0 of the stream, and every byte after a '\n'
-    u32 carry = (u32)__shfl_up((int)(nl >> 31), 1, 64);
+    u32 carry = (u32)__shfl_up((int)(nl[NM - 1] >> 31), 1, 64);
     if (lane == 0) carry = bs == 0 ? 1u : (a.out[bs - 1] == '\n' ? 1u : 0u);
-    u32 sm = (nl << 1) | carry;
-    if (q0 + 32u > bl) sm &= q0 >= bl ? 0u : ((1u << (bl - q0)) - 1u);
-    const u32 m = (u32)__builtin_popcount(sm);
+    u32 m = 0;
+#pragma unroll
+    for (u32 h = 0; h < NM; h++) {
+      sm[h] = ((nl[h] << 1) | (h ? (nl[h - 1] >> 31) : carry)) & keep(q0 + 32u * h);
+      m += (u32)__builtin_popcount(sm[h]);
+    }
     const u32 incl = d_incl_scan(m);
     const u32 nst = (u32)__builtin_amdgcn_readlane((int)incl, 63);
     u32 o = incl - m;
-    for (u32 x = sm; x; x &= x - 1) W.starts[o++] = (uint16_t)(q0 + (u32)__builtin_ctz(x));
-    if (op == 1) {
-      if (lane == 0) a.blk_cnt[blk] = nst;
-      continue;
-    }
+#pragma unroll
+    for (u32 h = 0; h < NM; h++)
+      for (u32 x = sm[h]; x; x &= x - 1) W.starts[o++] = (uint16_t)(q0 + 32u * h + (u32)__builtin_ctz(x));
+    if (lane == 0 && a.blk_cnt) a.blk_cnt[blk] = nst;  // ordinals of hits (k_hits_resolve)
+    if (op == 1) continue;
     // end of the last line starting here: first '\n' at or after it
     u64 tail_end = 0;
     if (nst) {
@@ -355,14 +371,15 @@ __global__ void __launch_bounds__(64) k_hits_resolve(A5xHitRaw* hits, u32 n, con
 }  // namespace
 
 size_t a5x_digest_lds(int algo) {
-  const u32 per = ((u32)sizeof(DWave) + (algo == A5X_ALGO_MD5 ? 0u : 64u * USTRIDE) + 15u) & ~15u;
-  return 4u * per;
+  const u32 per = algo == A5X_ALGO_MD5 ? (u32)sizeof(DWave<DCfg<true>::BLK>)
+                                       : (u32)sizeof(DWave<DCfg<false>::BLK>) + 64u * USTRIDE;
+  return 4u * ((per + 15u) & ~15u);
 }
 
 hipError_t a5x_launch_digest_stream(const A5xDigLaunch& L, int op, uint32_t grid, hipStream_t st) {
   if (L.nbytes == 0) return hipSuccess;
   if (((uintptr_t)L.out & 15u) != 0) return hipErrorInvalidValue;
-  const u64 nblk = (L.nbytes + DBLK - 1) / DBLK;
+  const u64 nblk = a5x_digest_blocks(L.nbytes, L.algo);
   const u64 want = (nblk + 3) / 4;
   const u32 g = (u32)(want < grid ? want : grid);
   if (L.algo == A5X_ALGO_MD5)
@@ -372,7 +389,10 @@ hipError_t a5x_launch_digest_stream(const A5xDigLaunch& L, int op, uint32_t grid
   return hipGetLastError();
 }
 
-uint64_t a5x_digest_blocks(uint64_t nbytes) { return (nbytes + DBLK - 1) / DBLK; }
+uint64_t a5x_digest_blocks(uint64_t nbytes, int algo) {
+  const u64 b = algo == A5X_ALGO_MD5 ? DCfg<true>::BLK : DCfg<false>::BLK;
+  return (nbytes + b - 1) / b;
+}
 
 hipError_t a5x_launch_hits_resolve(A5xHitRaw* hits, uint32_t n, const uint64_t* blk_pre, uint64_t cand_base,
                                    const uint64_t* cand_off, uint64_t nw, hipStream_t st) {

@@ -730,7 +730,7 @@ uint32_t dig_grid(a5x_ctx* c) { return (uint32_t)std::max(1, c->cus) * 8u; }
 // per-2KiB-block line starts and their exclusive scan (blk_pre, nblk+1 entries)
 int dig_block_prefix(a5x_ctx* c, A5xDigLaunch& D, hipStream_t st, uint64_t* total_lines) {
   int rc;
-  const uint64_t nblk = a5x_digest_blocks(D.nbytes);
+  const uint64_t nblk = a5x_digest_blocks(D.nbytes, D.algo);
   if ((rc = grow(c, c->dg_blk_cnt, nblk + 1)) || (rc = grow(c, c->dg_blk_pre, nblk + 1)) ||
       (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nblk + 1) + 16)))
     return rc;
@@ -1328,6 +1328,11 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
     A5xDigLaunch D = dig_launch(c);
     D.out = c->dg_scratch.p;
     D.nbytes = s.bytes;
+    const uint64_t nblk = a5x_digest_blocks(s.bytes, D.algo);
+    if ((rc = grow(c, c->dg_blk_cnt, nblk + 1)) || (rc = grow(c, c->dg_blk_pre, nblk + 1)) ||
+        (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nblk + 1) + 16)))
+      return rc;
+    D.blk_cnt = c->dg_blk_cnt.p;
     D.hits = c->dg_hits.p;
     D.hit_cap = (uint32_t)dev_hits;
     D.nhits = c->d_scalars + 8;
@@ -1347,7 +1352,8 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
     const uint64_t nh = c->h_scalars[8];
     if (nh) {
       const uint64_t got = std::min<uint64_t>(nh, dev_hits);
-      if ((rc = dig_block_prefix(c, D, st, nullptr))) return rc;
+      HIPCHK(c, a5x_launch_scan(c->dg_blk_cnt.p, c->dg_blk_cnt.p, nblk, c->dg_blk_pre.p, c->dg_blk_pre.p,
+                                c->scan_tmp.p, c->d_scalars + 2, st));
       HIPCHK(c, a5x_launch_hits_resolve(c->dg_hits.p, (uint32_t)got, c->dg_blk_pre.p, g, c->dg_cand_off.p, nw, st));
       const uint64_t room = found < hit_cap ? hit_cap - found : 0;
       const uint64_t take = std::min(room, got);

@@ -138,7 +138,7 @@ struct A5xDigLaunch {
   uint32_t* err;
 };
 size_t a5x_digest_lds(int algo);
-uint64_t a5x_digest_blocks(uint64_t nbytes);
+uint64_t a5x_digest_blocks(uint64_t nbytes, int algo);  // 4 KiB (MD5) / 2 KiB (NTLM) blocks
 hipError_t a5x_launch_digest_stream(const A5xDigLaunch& L, int op, uint32_t grid, hipStream_t st);
 hipError_t a5x_launch_hits_resolve(A5xHitRaw* hits, uint32_t n, const uint64_t* blk_pre, uint64_t cand_base,
                                    const uint64_t* cand_off, uint64_t nw, hipStream_t st);
