@@ -37,14 +37,29 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_diag(verbose: bool = False) -> str:
-    """Diagnostic variant with per-phase s_memtime stamps (-DA5X_STAMPS) in _build_diag/."""
-    out = os.path.join(PKG, "_build_diag")
+def build_diag(verbose: bool = False, stamps: bool = True) -> str:
+    """Diagnostic variant in _build_diag/: per-phase s_memtime stamps (-DA5X_STAMPS) and the
+    A5X_ABLATE timing switches (-DA5X_DIAG); never loaded by the product or the tests."""
+    out = os.path.join(PKG, "_build_diag" if stamps else "_build_abl")
     os.makedirs(out, exist_ok=True)
     lib = os.path.join(out, "liba5x.so")
     srcs = [os.path.join(CSRC, s) for s in LIB_SRCS]
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
-           "-DA5X_STAMPS", "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", lib]
+           *(["-DA5X_STAMPS"] if stamps else []), "-DA5X_DIAG", "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", lib]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return lib
+
+
+def build_variant(name: str, defines, verbose: bool = False) -> str:
+    """A5X tuning experiments: liba5x with extra -D defines in _build_<name>/ (never the product)."""
+    out = os.path.join(PKG, "_build_" + name)
+    os.makedirs(out, exist_ok=True)
+    lib = os.path.join(out, "liba5x.so")
+    srcs = [os.path.join(CSRC, s) for s in LIB_SRCS]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+           *["-D" + d for d in defines], "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", lib]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -208,7 +208,7 @@ __device__ u32 utf16le(const uint8_t* lbase, u32 loff, const uint8_t* gbase, u64
 
 __device__ __forceinline__ bool probe(const A5xDigLaunch& a, const u32* d) {
   if ((d[0] | d[1] | d[2] | d[3]) == 0u) return a.has_zero_target != 0;
-  const u32 bi = d[0] & ((1u << a.bm_log2) - 1u);
+  const u32 bi = d[0] & a.bm_mask;
   if (!((a.bitmap[bi >> 5] >> (bi & 31u)) & 1u)) return false;
   const u64 h = ((u64)d[1] | ((u64)d[2] << 32)) * 0x9E3779B97F4A7C15ull;
   u64 slot = (h >> 20) & a.tmask;
@@ -324,7 +324,9 @@ __global__ void __launch_bounds__(256) k_digest_stream(A5xDigLaunch a, int op) {
       const u32 s = W.starts[i];
       const u64 e = i + 1 < nst ? (u64)W.starts[i + 1] - 1 : tail_end;  // '\n' position
       const u32 len = (u32)(e - s);
-      const bool in_lds = e + 72 <= DBUF && s + len + 72 <= DBUF;
+      // every byte of the line staged (bytes past sl are zero-filled) and the 8-B
+      // over-read of the last message word inside the buffer
+      const bool in_lds = e <= sl && e + 8 <= DBUF;
       u32 d[4];
       if (MD5) {
         md_digest<true>(W.data, s, a.out, bs + s, a.nbytes, in_lds, len, d);

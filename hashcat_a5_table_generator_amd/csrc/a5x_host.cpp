@@ -110,17 +110,21 @@ struct a5x_ctx {
   uint32_t* h_scalars = nullptr;  // pinned
   uint64_t* h_totals = nullptr;   // pinned [0] cands [1] bytes [2..3] locate
 
-  // host-API staging
-  DevBuf<uint8_t> s_words, s_out;
+  // host-API staging: words, and the double-buffered output stream of a5x_expand
+  // (two HBM range buffers, two pinned host buffers, a copy stream; main.go:58-68)
+  DevBuf<uint8_t> s_words, s_out[2];
   DevBuf<uint64_t> s_woff;
-  uint8_t* h_out = nullptr;
+  uint8_t* h_out[2] = {nullptr, nullptr};
   size_t h_out_cap = 0;
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_exp[2] = {nullptr, nullptr}, ev_cpy[2] = {nullptr, nullptr};
+  DevBuf<uint64_t> loc_q, loc_r;  // range-boundary queries / results (job_locate)
 
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   uint64_t seg = 1024;        // candidates per per-word-path segment (a radix round there costs ~64x a FAST one)
   uint64_t chunk = 8192;      // candidates per expand wave (sweep on C3: 8192 < 16384 < 32768 ms)
   uint32_t waves_per_block = 4;
-  uint32_t ablate = 0;        // A5X_ABLATE (timing experiments only)
+  uint32_t ablate = 0;        // A5X_ABLATE: read only by the diagnostic build (-DA5X_DIAG)
 };
 
 namespace {
@@ -557,9 +561,11 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   int rc;
   if ((rc = upload_mtable(c))) return rc;
   if (nw > 0xffffffffull) return fail(c, A5X_E_ARG, "batch of %llu words (max 2^32-1)", (unsigned long long)nw);
-  // -r with min < 0: generateCombinations(n, k<0) recurses until the goroutine stack
-  // overflows (main.go:263-281), which kills the reference process on the first word.
-  if (mode == A5X_MODE_REVERSE && mn < 0 && mx >= -1 && nw > 0)
+  // -r with min < 0: the subCount loop (main.go:238) reaches k = min < 0 whenever it runs
+  // at all (min(max, n) >= min, i.e. max >= min), and generateCombinations(n, k < 0)
+  // recurses until the goroutine stack overflows (main.go:263-281), which kills the
+  // reference process on the first word.
+  if (mode == A5X_MODE_REVERSE && mn < 0 && mx >= mn && nw > 0)
     return fail(c, A5X_E_BOUNDS,
                 "fatal error: stack overflow (generateCombinations with k < 0, main.go:273; --table-min %d)", mn);
   if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
@@ -644,66 +650,198 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   return A5X_OK;
 }
 
-int expand_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn, int mx,
-                uint64_t cand_begin, uint64_t cand_end, uint8_t* d_out, uint64_t out_cap, uint64_t* d_cand_off,
-                uint64_t* d_byte_off, a5x_stats* stats, hipStream_t st) {
-  int rc;
+// ---------------------------------------------------------------------------
+// Batch jobs: the keyspace runs once per batch (job_prepare), then any number of
+// candidate ranges are located and expanded against it (job_locate, job_launch).
+// ---------------------------------------------------------------------------
+struct Job {
+  const uint8_t* w = nullptr;
+  const uint64_t* wo = nullptr;
+  uint64_t nw = 0;
+  int mode = 0, mn = 0, mx = 0;
+  hipStream_t st = nullptr;
   Batch B;
-  if ((rc = run_keyspace_mode(c, d_words, d_woff, nw, mode, mn, mx, d_cand_off, d_byte_off, st, &B, true)))
-    return rc;
-  const uint64_t cb = std::min(cand_begin, B.total_cands);
-  const uint64_t ce = std::min(cand_end, B.total_cands);
-  if (stats) {
-    memset(stats, 0, sizeof *stats);
-    stats->words = nw;
+};
+
+// [cb, ce) global candidates <-> output bytes [b0, b1); -r/-s engines: items [i0, i1)
+struct Range {
+  uint64_t cb, ce, b0, b1, i0, i1;
+};
+
+int job_prepare(a5x_ctx* c, Job& J, uint64_t* d_cand_off, uint64_t* d_byte_off, bool timed) {
+  int rc;
+  if (J.mode != A5X_MODE_DEFAULT)
+    return run_keyspace_mode(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, d_cand_off, d_byte_off, J.st, &J.B, timed);
+  if ((rc = run_keyspace(c, J.w, J.wo, J.nw, J.mn, J.mx, d_cand_off, d_byte_off, J.st, &J.B, timed))) return rc;
+  if (J.B.total_cands) {  // chunk -> first word map, consumed by every range's k_expand_fast
+    const uint64_t nchunks = (J.B.total_cands + c->chunk - 1) / c->chunk;
+    if ((rc = grow(c, c->chunk_w0, nchunks + 1))) return rc;
+    HIPCHK(c, a5x_launch_plan(J.B.cand_off, J.nw, c->chunk, c->chunk_w0.p, J.st));
   }
-  if (ce <= cb) return A5X_OK;
-  A5xModeLaunch M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx);
-  M.cand_off = B.cand_off;
-  uint64_t b0 = 0, b1 = B.total_bytes, i0 = 0, i1 = c->m_items;
-  if (cb > 0 || ce < B.total_cands) {
-    if ((rc = grow(c, c->locate, 8))) return rc;
-    uint64_t hq[2] = {cb, ce};
-    HIPCHK(c, hipMemcpyAsync(c->locate.p, hq, 16, hipMemcpyHostToDevice, st));
-    HIPCHK(c, a5x_launch_mode_locate(M, c->locate.p, 2, c->locate.p + 2, st));
-    uint64_t loc[6];
-    HIPCHK(c, hipMemcpyAsync(loc, c->locate.p + 2, 48, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
-    i0 = loc[0]; b0 = loc[2];
-    i1 = loc[3] + (loc[4] ? 1 : 0); b1 = loc[5];
+  return A5X_OK;
+}
+
+int job_check(a5x_ctx* c, const Job& J) {
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, J.st));
+  HIPCHK(c, hipStreamSynchronize(J.st));
+  return decode_dev_err(c, c->h_scalars[2]);
+}
+
+// Output byte (and -r/-s item) positions of global candidate indices q[0..n) (sorted or
+// not); synchronises.  res[3 i] = byte offset, [3 i + 1] = item, [3 i + 2] = index in item.
+int job_locate(a5x_ctx* c, const Job& J, const std::vector<uint64_t>& q, std::vector<uint64_t>& res) {
+  int rc;
+  const uint32_t n = (uint32_t)q.size();
+  res.assign(3 * (size_t)n, 0);
+  if (!n) return A5X_OK;
+  if ((rc = grow(c, c->loc_q, n)) || (rc = grow(c, c->loc_r, 3 * (size_t)n))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->loc_q.p, q.data(), 8 * (size_t)n, hipMemcpyHostToDevice, J.st));
+  if (J.mode != A5X_MODE_DEFAULT) {
+    A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx);
+    M.cand_off = J.B.cand_off;
+    HIPCHK(c, a5x_launch_mode_locate(M, c->loc_q.p, n, c->loc_r.p, J.st));
+    std::vector<uint64_t> t(3 * (size_t)n);
+    HIPCHK(c, hipMemcpyAsync(t.data(), c->loc_r.p, 24 * (size_t)n, hipMemcpyDeviceToHost, J.st));
+    if ((rc = job_check(c, J))) return rc;
+    for (uint32_t i = 0; i < n; i++) {
+      res[3 * i] = t[3 * i + 2];
+      res[3 * i + 1] = t[3 * i];
+      res[3 * i + 2] = t[3 * i + 1];
+    }
+    return A5X_OK;
   }
-  if (stats) {
-    stats->candidates = ce - cb;
-    stats->bytes = b1 - b0;
+  A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
+  HIPCHK(c, a5x_launch_locate(E, c->loc_q.p, n, c->loc_r.p, J.st));
+  std::vector<uint64_t> t(n);
+  HIPCHK(c, hipMemcpyAsync(t.data(), c->loc_r.p, 8 * (size_t)n, hipMemcpyDeviceToHost, J.st));
+  if ((rc = job_check(c, J))) return rc;
+  for (uint32_t i = 0; i < n; i++) res[3 * i] = t[i];
+  return A5X_OK;
+}
+
+Range range_of(const Job& J, uint64_t cb, uint64_t ce, const uint64_t* lb, const uint64_t* le) {
+  Range R;
+  R.cb = cb; R.ce = ce;
+  R.b0 = lb[0]; R.b1 = le[0];
+  R.i0 = lb[1];
+  R.i1 = le[1] + (le[2] ? 1 : 0);
+  (void)J;
+  return R;
+}
+
+// Cut [0, total) into ranges of at most cap output bytes: candidate boundaries spaced for
+// ~3/4 cap each, located in one call; ranges that still exceed cap are halved.
+int plan_ranges(a5x_ctx* c, const Job& J, uint64_t cap, std::vector<Range>& out) {
+  out.clear();
+  const uint64_t T = J.B.total_cands, TB = J.B.total_bytes;
+  if (!T) return A5X_OK;
+  if (TB <= cap) {
+    Range R{0, T, 0, TB, 0, J.mode != A5X_MODE_DEFAULT ? c->m_items : 0};
+    out.push_back(R);
+    return A5X_OK;
   }
-  if (b1 - b0 > out_cap || (!d_out && b1 > b0))
-    return fail(c, A5X_E_CAPACITY, "output needs %llu bytes, buffer has %llu", (unsigned long long)(b1 - b0),
+  const uint64_t K = std::max<uint64_t>(2, (TB + cap * 3 / 4 - 1) / std::max<uint64_t>(1, cap * 3 / 4));
+  std::vector<uint64_t> q(K + 1), res;
+  for (uint64_t k = 0; k <= K; k++) q[k] = (uint64_t)((unsigned __int128)T * k / K);
+  int rc;
+  if ((rc = job_locate(c, J, q, res))) return rc;
+  std::vector<Range> work;
+  for (uint64_t k = 0; k < K; k++)
+    if (q[k + 1] > q[k]) work.push_back(range_of(J, q[k], q[k + 1], &res[3 * k], &res[3 * (k + 1)]));
+  // halve oversize ranges until every range fits
+  for (int pass = 0; pass < 64; pass++) {
+    std::vector<uint64_t> mid;
+    for (auto& R : work)
+      if (R.b1 - R.b0 > cap) {
+        if (R.ce - R.cb == 1)
+          return fail(c, A5X_E_CAPACITY, "one candidate needs %llu bytes, the range buffer has %llu",
+                      (unsigned long long)(R.b1 - R.b0), (unsigned long long)cap);
+        mid.push_back(R.cb + (R.ce - R.cb) / 2);
+      }
+    if (mid.empty()) break;
+    std::vector<uint64_t> mres;
+    if ((rc = job_locate(c, J, mid, mres))) return rc;
+    std::vector<Range> next;
+    size_t m = 0;
+    for (auto& R : work) {
+      if (R.b1 - R.b0 > cap) {
+        const uint64_t lb[3] = {R.b0, R.i0, 0};
+        const uint64_t* lm = &mres[3 * m];
+        const uint64_t le[3] = {R.b1, R.i1, 0};
+        next.push_back(range_of(J, R.cb, mid[m], lb, lm));
+        Range H = range_of(J, mid[m], R.ce, lm, le);
+        H.i0 = lm[1];  // the half starts inside item lm[1]
+        next.push_back(H);
+        m++;
+      } else {
+        next.push_back(R);
+      }
+    }
+    work.swap(next);
+  }
+  out.swap(work);
+  return A5X_OK;
+}
+
+// Launch the expansion of one located range into d_out (asynchronous on J.st).
+int job_launch(a5x_ctx* c, const Job& J, const Range& R, uint8_t* d_out, uint64_t out_cap) {
+  int rc;
+  if (R.ce <= R.cb) return A5X_OK;
+  if (R.b1 - R.b0 > out_cap || (!d_out && R.b1 > R.b0))
+    return fail(c, A5X_E_CAPACITY, "output needs %llu bytes, buffer has %llu", (unsigned long long)(R.b1 - R.b0),
                 (unsigned long long)out_cap);
-  M.item_begin = i0;
-  M.item_end = i1;
-  M.cand_begin = cb;
-  M.cand_end = ce;
-  M.out = d_out;
-  M.out_base = b0;
-  M.out_cap = out_cap;
-  HIPCHK(c, hipEventRecord(c->ev[1], st));
-  HIPCHK(c, a5x_launch_mode_items(M, 1, st));
-  HIPCHK(c, hipEventRecord(c->ev[2], st));
-  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipStreamSynchronize(st));
-  if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
-  if (stats) {
-    float a = 0, b = 0, t = 0;
-    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-    HIPCHK(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
-    HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[2]));
-    stats->ms_keyspace = a;
-    stats->ms_expand = b;
-    stats->ms_total = t;
-    stats->expand_launches = 1;
+  if (J.mode != A5X_MODE_DEFAULT) {
+    A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx);
+    M.cand_off = J.B.cand_off;
+    M.item_begin = R.i0;
+    M.item_end = R.i1;
+    M.cand_begin = R.cb;
+    M.cand_end = R.ce;
+    M.out = d_out;
+    M.out_base = R.b0;
+    M.out_cap = out_cap;
+    HIPCHK(c, a5x_launch_mode_items(M, 1, J.st));
+    return A5X_OK;
   }
+  const Batch& B = J.B;
+  A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, B);
+  E.cand_begin = R.cb;
+  E.cand_end = R.ce;
+  E.out = d_out;
+  E.out_base = R.b0;
+  E.out_cap = out_cap;
+  // slow / BIG words: (word, SEG-candidate segment) items, slow from segs[0], BIG
+  // from segs[sbound]; a word adds at most ceil(range / SEG) + 1 segments
+  const uint64_t rng_segs = (R.ce - R.cb) / c->seg + 1;
+  const uint64_t sbound = B.nslow ? B.nslow + rng_segs : 0;
+  const uint64_t bbound = B.nbig ? B.nbig + rng_segs : 0;
+  if (sbound + bbound > 0xffffffffull)
+    return fail(c, A5X_E_CAPACITY, "call range needs more than 2^32 slow-path segments (lower A5X_CHUNK range)");
+  if (B.nslow || B.nbig) {
+    if ((rc = grow(c, c->segs, sbound + bbound + 1))) return rc;
+    HIPCHK(c, hipMemsetAsync(c->d_scalars + 5, 0, 8, J.st));
+  }
+  if (B.nslow)
+    HIPCHK(c, a5x_launch_segments(c->slow_list.p, c->d_scalars + 3, B.nslow, B.cand_off, R.cb, R.ce, c->seg,
+                                  c->segs.p, c->d_scalars + 5, J.st));
+  if (B.nbig)
+    HIPCHK(c, a5x_launch_segments(c->big_list.p, c->d_scalars + 1, B.nbig, B.cand_off, R.cb, R.ce, c->seg,
+                                  c->segs.p + sbound, c->d_scalars + 6, J.st));
+  HIPCHK(c, a5x_launch_expand(E, 0, J.st));
+  if (B.nslow) {
+    E.segs = c->segs.p; E.nsegs = c->d_scalars + 5; E.nsegs_bound = sbound;
+    HIPCHK(c, a5x_launch_expand(E, 1, J.st));
+  }
+  if (B.nbig) {
+    E.segs = c->segs.p + sbound; E.nsegs = c->d_scalars + 6; E.nsegs_bound = bbound;
+    HIPCHK(c, a5x_launch_expand(E, 2, J.st));
+  }
+  return A5X_OK;
+}
+
+int job_open(a5x_ctx* c, Job& J, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn,
+             int mx, hipStream_t st) {
+  J.w = d_words; J.wo = d_woff; J.nw = nw; J.mode = mode; J.mn = mn; J.mx = mx; J.st = st;
   return A5X_OK;
 }
 
@@ -719,7 +857,8 @@ A5xDigLaunch dig_launch(a5x_ctx* c) {
   A5xDigLaunch D;
   memset(&D, 0, sizeof D);
   D.algo = c->t_algo < 0 ? A5X_ALGO_MD5 : c->t_algo;
-  D.bitmap = c->t_bitmap.p; D.bm_log2 = c->t_bm_log2;
+  D.bitmap = c->t_bitmap.p;
+  D.bm_mask = c->t_bm_log2 >= 32 ? 0xffffffffu : (uint32_t)((1ull << c->t_bm_log2) - 1);
   D.table = c->t_table.p; D.tmask = c->t_tmask; D.has_zero_target = c->t_has_zero;
   D.err = c->d_scalars + 2;
   return D;
@@ -792,7 +931,9 @@ int a5x_create(int device, a5x_ctx** out) {
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_MSEG")) c->mseg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_SEG")) c->seg = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
-  if (const char* e = getenv("A5X_ABLATE")) c->ablate = (uint32_t)atoi(e);
+#ifdef A5X_DIAG
+  if (const char* e = getenv("A5X_ABLATE")) c->ablate = (uint32_t)atoi(e);  // timing experiments only
+#endif
   if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   *out = c;
   return A5X_OK;
@@ -813,12 +954,19 @@ void a5x_destroy(a5x_ctx* c) {
   for (auto& e : c->dev_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->d_mtab) (void)hipFree(c->d_mtab);
-  release(c->s_words); release(c->s_out); release(c->s_woff);
+  release(c->s_words); release(c->s_out[0]); release(c->s_out[1]); release(c->s_woff);
+  release(c->loc_q); release(c->loc_r);
+  for (auto& e : c->ev_exp)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_cpy)
+    if (e) (void)hipEventDestroy(e);
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->d_table) (void)hipFree(c->d_table);
   if (c->d_scalars) (void)hipFree(c->d_scalars);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
   if (c->h_totals) (void)hipHostFree(c->h_totals);
-  if (c->h_out) (void)hipHostFree(c->h_out);
+  for (auto& h : c->h_out)
+    if (h) (void)hipHostFree(h);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -967,12 +1115,10 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   int rc;
   if ((rc = check_mode(c, mode))) return rc;
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  if (mode != A5X_MODE_DEFAULT)
-    return expand_mode(c, d_words, d_woff, nw, mode, mn, mx, cand_begin, cand_end, d_out, out_cap, d_cand_off,
-                       d_byte_off, stats, st);
-  Batch B;
-  if ((rc = run_keyspace(c, d_words, d_woff, nw, mn, mx, d_cand_off, d_byte_off, st, &B, true))) return rc;
+  Job J;
+  job_open(c, J, d_words, d_woff, nw, mode, mn, mx, stream ? (hipStream_t)stream : c->stream);
+  if ((rc = job_prepare(c, J, d_cand_off, d_byte_off, true))) return rc;
+  const Batch& B = J.B;
   const uint64_t cb = std::min(cand_begin, B.total_cands);
   const uint64_t ce = std::min(cand_end, B.total_cands);
   if (stats) {
@@ -980,68 +1126,20 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     stats->words = nw;
   }
   if (ce <= cb) return A5X_OK;
-  A5xExpLaunch E = exp_launch(c, d_words, d_woff, nw, mn, mx, B);
-  E.cand_begin = cb;
-  E.cand_end = ce;
-  // byte range of [cb, ce)
-  uint64_t b0 = 0, b1 = B.total_bytes;
+  Range R{cb, ce, 0, B.total_bytes, 0, mode != A5X_MODE_DEFAULT ? c->m_items : 0};
   if (cb > 0 || ce < B.total_cands) {
-    if ((rc = grow(c, c->locate, 4))) return rc;
-    uint64_t hc[2] = {cb, ce};
-    HIPCHK(c, hipMemcpyAsync(c->locate.p, hc, 16, hipMemcpyHostToDevice, st));
-    HIPCHK(c, a5x_launch_locate(E, c->locate.p, 2, c->locate.p + 2, st));
-    HIPCHK(c, hipMemcpyAsync(c->h_totals + 2, c->locate.p + 2, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
-    b0 = c->h_totals[2];
-    b1 = c->h_totals[3];
+    std::vector<uint64_t> res;
+    if ((rc = job_locate(c, J, {cb, ce}, res))) return rc;
+    R = range_of(J, cb, ce, &res[0], &res[3]);
   }
   if (stats) {
     stats->candidates = ce - cb;
-    stats->bytes = b1 - b0;
+    stats->bytes = R.b1 - R.b0;
   }
-  if (b1 - b0 > out_cap || (!d_out && b1 > b0))
-    return fail(c, A5X_E_CAPACITY, "output needs %llu bytes, buffer has %llu", (unsigned long long)(b1 - b0),
-                (unsigned long long)out_cap);
-  E.out = d_out;
-  E.out_base = b0;
-  E.out_cap = out_cap;
-  const uint64_t nchunks = (B.total_cands + c->chunk - 1) / c->chunk;
-  if ((rc = grow(c, c->chunk_w0, nchunks + 1))) return rc;
-  E.chunk_w0 = c->chunk_w0.p;
-  // slow / BIG words: (word, CH-candidate segment) items, slow from segs[0], BIG
-  // from segs[sbound]; a word adds at most ceil(range / CH) + 1 segments
-  const uint64_t rng_segs = (ce - cb) / c->seg + 1;
-  const uint64_t sbound = B.nslow ? B.nslow + rng_segs : 0;
-  const uint64_t bbound = B.nbig ? B.nbig + rng_segs : 0;
-  if (sbound + bbound > 0xffffffffull)
-    return fail(c, A5X_E_CAPACITY, "call range needs more than 2^32 slow-path segments (lower A5X_CHUNK range)");
-  if (B.nslow || B.nbig) {
-    if ((rc = grow(c, c->segs, sbound + bbound + 1))) return rc;
-    HIPCHK(c, hipMemsetAsync(c->d_scalars + 5, 0, 8, st));
-  }
-  if (B.nslow)
-    HIPCHK(c, a5x_launch_segments(c->slow_list.p, c->d_scalars + 3, B.nslow, B.cand_off, cb, ce, c->seg,
-                                  c->segs.p, c->d_scalars + 5, st));
-  if (B.nbig)
-    HIPCHK(c, a5x_launch_segments(c->big_list.p, c->d_scalars + 1, B.nbig, B.cand_off, cb, ce, c->seg,
-                                  c->segs.p + sbound, c->d_scalars + 6, st));
-  HIPCHK(c, a5x_launch_plan(B.cand_off, nw, c->chunk, c->chunk_w0.p, st));
-  HIPCHK(c, hipEventRecord(c->ev[1], st));
-  HIPCHK(c, a5x_launch_expand(E, 0, st));
-  if (B.nslow) {
-    E.segs = c->segs.p; E.nsegs = c->d_scalars + 5; E.nsegs_bound = sbound;
-    HIPCHK(c, a5x_launch_expand(E, 1, st));
-  }
-  if (B.nbig) {
-    E.segs = c->segs.p + sbound; E.nsegs = c->d_scalars + 6; E.nsegs_bound = bbound;
-    HIPCHK(c, a5x_launch_expand(E, 2, st));
-  }
-  HIPCHK(c, hipEventRecord(c->ev[2], st));
-  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipStreamSynchronize(st));
-  if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[1], J.st));
+  if ((rc = job_launch(c, J, R, d_out, out_cap))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[2], J.st));
+  if ((rc = job_check(c, J))) return rc;
   if (stats) {
     float a = 0, b = 0, t = 0;
     HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
@@ -1051,7 +1149,7 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     stats->ms_expand = b;
     stats->ms_total = t;
     stats->words_pass_b = B.nbig;
-    stats->expand_launches = 1 + (B.nslow ? 1 : 0) + (B.nbig ? 1 : 0);
+    stats->expand_launches = mode != A5X_MODE_DEFAULT ? 1 : 1 + (B.nslow ? 1 : 0) + (B.nbig ? 1 : 0);
     stats->words_slow = B.nslow;
   }
   return A5X_OK;
@@ -1091,6 +1189,9 @@ int a5x_keyspace(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_
   return A5X_OK;
 }
 
+// The stdout path (main.go:58-68): ranges of <= cap bytes expanded into two HBM buffers
+// in turn; each range's D2H runs on a copy stream into a pinned buffer while the next
+// range expands, and the sink consumes range k while range k + 1 is being copied.
 int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
                a5x_sink_fn sink, void* user, a5x_stats* stats) {
   if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
@@ -1102,47 +1203,69 @@ int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t 
   if ((rc = grow(c, c->s_words, wbytes + 16)) || (rc = grow(c, c->s_woff, nw + 1))) return rc;
   if (wbytes) HIPCHK(c, hipMemcpyAsync(c->s_words.p, words, wbytes, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->s_woff.p, woff, (nw + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  uint64_t tc = 0, tb = 0;
-  if ((rc = a5x_keyspace_device(c, c->s_words.p, c->s_woff.p, nw, mode, mn, mx, nullptr, nullptr, &tc, &tb,
-                                c->stream)))
-    return rc;
-  // stream the output through a bounded device buffer, in candidate ranges
-  size_t cap = (size_t)1 << 28;
+  Job J;
+  job_open(c, J, c->s_words.p, c->s_woff.p, nw, mode, mn, mx, c->stream);
+  if ((rc = job_prepare(c, J, nullptr, nullptr, true))) return rc;
+  size_t cap = (size_t)1 << 27;
   if (const char* e = getenv("A5X_HOST_CHUNK_BYTES")) cap = std::max<size_t>(4096, strtoull(e, nullptr, 10));
-  if ((rc = grow(c, c->s_out, cap))) return rc;
-  if (c->h_out_cap < cap) {
-    if (c->h_out) (void)hipHostFree(c->h_out);
-    c->h_out = nullptr;
-    HIPCHK(c, hipHostMalloc((void**)&c->h_out, cap, 0));
-    c->h_out_cap = cap;
-  }
-  a5x_stats total;
-  memset(&total, 0, sizeof total);
-  total.words = nw;
-  uint64_t g = 0, step = std::max<uint64_t>(1, cap / 32);
-  while (g < tc) {
-    const uint64_t ge = std::min(tc, g + step);
-    a5x_stats s;
-    rc = a5x_expand_device(c, c->s_words.p, c->s_woff.p, nw, mode, mn, mx, g, ge, c->s_out.p, cap, nullptr,
-                           nullptr, &s, c->stream);
-    if (rc == A5X_E_CAPACITY) {
-      if (ge - g == 1) return rc;  // one candidate larger than the buffer
-      step = std::max<uint64_t>(1, (ge - g) / 2);
-      continue;
+  std::vector<Range> ranges;
+  if ((rc = plan_ranges(c, J, cap, ranges))) return rc;
+  if (!ranges.empty()) {
+    if ((rc = grow(c, c->s_out[0], cap)) || (rc = grow(c, c->s_out[1], cap))) return rc;
+    if (c->h_out_cap < cap) {
+      for (auto& h : c->h_out)
+        if (h) (void)hipHostFree(h), h = nullptr;
+      c->h_out_cap = 0;
+      HIPCHK(c, hipHostMalloc((void**)&c->h_out[0], cap, 0));
+      HIPCHK(c, hipHostMalloc((void**)&c->h_out[1], cap, 0));
+      c->h_out_cap = cap;
     }
-    if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->h_out, c->s_out.p, s.bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (s.bytes && sink(user, c->h_out, s.bytes)) return fail(c, A5X_E_SINK, "sink returned non-zero");
-    total.candidates += s.candidates;
-    total.bytes += s.bytes;
-    total.ms_keyspace += s.ms_keyspace;
-    total.ms_expand += s.ms_expand;
-    total.ms_total += s.ms_total;
-    g = ge;
-    if (s.bytes < cap / 4) step *= 2;  // adapt the range to the buffer
+    if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+      if (!c->ev_exp[i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_exp[i], hipEventDisableTiming));
+      if (!c->ev_cpy[i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_cpy[i], hipEventDisableTiming));
+    }
   }
-  if (stats) *stats = total;
+  // error word of each range, copied behind its launch (valid once its copy event fired)
+  uint32_t* herr = c->h_scalars + 32;
+  auto drain = [&](size_t k) -> int {  // range k has been copied: check it, hand it to the sink
+    HIPCHK(c, hipEventSynchronize(c->ev_cpy[k & 1]));
+    if (herr[k & 1]) return decode_dev_err(c, herr[k & 1]);
+    const uint64_t nb = ranges[k].b1 - ranges[k].b0;
+    if (nb && sink(user, c->h_out[k & 1], nb)) return fail(c, A5X_E_SINK, "sink returned non-zero");
+    return A5X_OK;
+  };
+  HIPCHK(c, hipEventRecord(c->ev[1], J.st));
+  for (size_t k = 0; k < ranges.size(); k++) {
+    const int b = (int)(k & 1);
+    if (k >= 2) HIPCHK(c, hipStreamWaitEvent(J.st, c->ev_cpy[b], 0));  // range k-2's copy left buffer b
+    if ((rc = job_launch(c, J, ranges[k], c->s_out[b].p, cap))) return rc;
+    HIPCHK(c, hipMemcpyAsync(herr + b, c->d_scalars + 2, 4, hipMemcpyDeviceToHost, J.st));
+    HIPCHK(c, hipEventRecord(c->ev_exp[b], J.st));
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_exp[b], 0));
+    HIPCHK(c, hipMemcpyAsync(c->h_out[b], c->s_out[b].p, ranges[k].b1 - ranges[k].b0, hipMemcpyDeviceToHost,
+                             c->cstream));
+    HIPCHK(c, hipEventRecord(c->ev_cpy[b], c->cstream));
+    if (k >= 1 && (rc = drain(k - 1))) return rc;
+  }
+  if (!ranges.empty() && (rc = drain(ranges.size() - 1))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[2], J.st));
+  if ((rc = job_check(c, J))) return rc;
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->words = nw;
+    stats->candidates = J.B.total_cands;
+    stats->bytes = J.B.total_bytes;
+    float a = 0, t = 0;
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[2]));
+    stats->ms_keyspace = a;
+    stats->ms_total = t;  // includes the D2H copies and the sink
+    stats->ms_expand = t - a;
+    stats->expand_launches = (uint32_t)ranges.size();
+    stats->words_slow = J.B.nslow;
+    stats->words_pass_b = J.B.nbig;
+  }
   return A5X_OK;
 }
 
@@ -1298,78 +1421,87 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
   int rc;
   if ((rc = check_mode(c, mode))) return rc;
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  Job J;
+  job_open(c, J, d_words, d_woff, nw, mode, mn, mx, stream ? (hipStream_t)stream : c->stream);
   if ((rc = grow(c, c->dg_cand_off, nw + 1)) || (rc = grow(c, c->dg_byte_off, nw + 1))) return rc;
-  uint64_t tc = 0, tb = 0;
-  if ((rc = a5x_keyspace_device(c, d_words, d_woff, nw, mode, mn, mx, nullptr, nullptr, &tc, &tb, st))) return rc;
+  if ((rc = job_prepare(c, J, c->dg_cand_off.p, c->dg_byte_off.p, true))) return rc;
+  const uint64_t tc = J.B.total_cands, tb = J.B.total_bytes;
   uint64_t cap = scratch_bytes ? scratch_bytes : ((uint64_t)2 << 30);
   cap = std::max<uint64_t>(4096, std::min<uint64_t>(cap, tb + 64));
+  std::vector<Range> ranges;
+  if ((rc = plan_ranges(c, J, cap, ranges))) return rc;
   if ((rc = grow(c, c->dg_scratch, cap + 64))) return rc;
-  const uint64_t dev_hits = std::max<uint64_t>(1, std::min<uint64_t>(hit_cap ? hit_cap : 1, 1u << 20));
+  uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
   if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
   a5x_stats total;
   memset(&total, 0, sizeof total);
   total.words = nw;
-  uint64_t found = 0;
-  double ms_dig = 0;
-  const uint64_t avg = tc ? (tb + tc - 1) / tc : 16;
-  uint64_t g = 0, step = std::max<uint64_t>(1, cap / (avg + avg / 4 + 1));
-  while (g < tc) {
-    const uint64_t ge = std::min(tc, g + step);
-    a5x_stats s;
-    rc = a5x_expand_device(c, d_words, d_woff, nw, mode, mn, mx, g, ge, c->dg_scratch.p, cap, c->dg_cand_off.p,
-                           c->dg_byte_off.p, &s, st);
-    if (rc == A5X_E_CAPACITY) {
-      if (ge - g == 1) return rc;
-      step = std::max<uint64_t>(1, (ge - g) / 2);
-      continue;
-    }
-    if (rc) return rc;
+  total.candidates = tc;
+  total.bytes = tb;
+  uint64_t found = 0, copied = 0;
+  float ms_exp = 0, ms_dig = 0;
+  for (const Range& R : ranges) {
+    HIPCHK(c, hipEventRecord(c->ev[1], J.st));
+    if ((rc = job_launch(c, J, R, c->dg_scratch.p, cap))) return rc;
+    HIPCHK(c, hipEventRecord(c->ev[2], J.st));
     A5xDigLaunch D = dig_launch(c);
     D.out = c->dg_scratch.p;
-    D.nbytes = s.bytes;
-    const uint64_t nblk = a5x_digest_blocks(s.bytes, D.algo);
+    D.nbytes = R.b1 - R.b0;
+    const uint64_t nblk = a5x_digest_blocks(D.nbytes, D.algo);
     if ((rc = grow(c, c->dg_blk_cnt, nblk + 1)) || (rc = grow(c, c->dg_blk_pre, nblk + 1)) ||
         (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nblk + 1) + 16)))
       return rc;
     D.blk_cnt = c->dg_blk_cnt.p;
-    D.hits = c->dg_hits.p;
-    D.hit_cap = (uint32_t)dev_hits;
-    D.nhits = c->d_scalars + 8;
-    HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, st));
-    HIPCHK(c, hipEventRecord(c->dev_ev[0], st));
-    HIPCHK(c, a5x_launch_digest_stream(D, 0, dig_grid(c), st));
-    HIPCHK(c, hipEventRecord(c->dev_ev[1], st));
-    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    float ms = 0;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->dev_ev[0], c->dev_ev[1]));
-    ms_dig += ms;
-    const uint32_t e = c->h_scalars[2] & ~(1u << 10);
-    if (e & (1u << 9))
-      return fail(c, A5X_E_UNSUPPORTED, "an NTLM candidate is longer than 64 UTF-16 code units (device limit)");
-    if ((rc = decode_dev_err(c, e))) return rc;
-    const uint64_t nh = c->h_scalars[8];
+    uint64_t nh = 0;
+    for (;;) {  // a range with more hits than the device buffer is digested again with room for all
+      D.hits = c->dg_hits.p;
+      D.hit_cap = (uint32_t)dev_hits;
+      D.nhits = c->d_scalars + 8;
+      HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
+      HIPCHK(c, hipEventRecord(c->dev_ev[0], J.st));
+      HIPCHK(c, a5x_launch_digest_stream(D, 0, dig_grid(c), J.st));
+      HIPCHK(c, hipEventRecord(c->dev_ev[1], J.st));
+      HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      float me = 0, md = 0;
+      HIPCHK(c, hipEventElapsedTime(&me, c->ev[1], c->ev[2]));
+      HIPCHK(c, hipEventElapsedTime(&md, c->dev_ev[0], c->dev_ev[1]));
+      ms_exp += me;
+      ms_dig += md;
+      const uint32_t e = c->h_scalars[2] & ~(1u << 10);
+      if (e & (1u << 9))
+        return fail(c, A5X_E_UNSUPPORTED, "an NTLM candidate is longer than 64 UTF-16 code units (device limit)");
+      if ((rc = decode_dev_err(c, e))) return rc;
+      nh = c->h_scalars[8];
+      if (nh <= dev_hits || copied >= hit_cap) break;
+      dev_hits = nh;  // grow and run this range's digest again (its candidates are still in scratch)
+      if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+      HIPCHK(c, hipMemsetAsync(c->d_scalars + 2, 0, 4, J.st));
+    }
     if (nh) {
       const uint64_t got = std::min<uint64_t>(nh, dev_hits);
       HIPCHK(c, a5x_launch_scan(c->dg_blk_cnt.p, c->dg_blk_cnt.p, nblk, c->dg_blk_pre.p, c->dg_blk_pre.p,
-                                c->scan_tmp.p, c->d_scalars + 2, st));
-      HIPCHK(c, a5x_launch_hits_resolve(c->dg_hits.p, (uint32_t)got, c->dg_blk_pre.p, g, c->dg_cand_off.p, nw, st));
-      const uint64_t room = found < hit_cap ? hit_cap - found : 0;
-      const uint64_t take = std::min(room, got);
-      if (take) HIPCHK(c, hipMemcpyAsync(hits + found, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, st));
-      HIPCHK(c, hipStreamSynchronize(st));
+                                c->scan_tmp.p, c->d_scalars + 2, J.st));
+      HIPCHK(c, a5x_launch_hits_resolve(c->dg_hits.p, (uint32_t)got, c->dg_blk_pre.p, R.cb, c->dg_cand_off.p, nw,
+                                        J.st));
+      const uint64_t take = std::min(hit_cap - std::min(hit_cap, copied), got);
+      if (take)
+        HIPCHK(c, hipMemcpyAsync(hits + copied, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      copied += take;
       found += nh;
     }
-    total.candidates += s.candidates;
-    total.bytes += s.bytes;
-    total.ms_keyspace += s.ms_keyspace;
-    total.ms_expand += s.ms_expand;
-    total.ms_total += s.ms_total + ms;
-    total.expand_launches += s.expand_launches;
-    g = ge;
-    if (s.bytes < cap / 2) step *= 2;
+    total.expand_launches += 1;
   }
+  total.ms_keyspace = 0;
+  {
+    float a = 0;
+    if (hipEventElapsedTime(&a, c->ev[0], c->ev[1]) == hipSuccess && ranges.size() <= 1) total.ms_keyspace = a;
+  }
+  total.ms_expand = ms_exp;
+  total.ms_total = total.ms_keyspace + ms_exp + ms_dig;
+  total.words_slow = J.B.nslow;
+  total.words_pass_b = J.B.nbig;
   if (n_hits) *n_hits = found;
   if (stats) *stats = total;
   if (found > hit_cap)

@@ -88,22 +88,37 @@ __device__ __forceinline__ u32 wave_incl_scan_u32(u32 x) {
 }
 __device__ __forceinline__ u32 lane63(u32 x) { return (u32)__builtin_amdgcn_readlane((int)x, 63); }
 __device__ __forceinline__ u32 readlane_u32(u32 x, u32 l) { return (u32)__builtin_amdgcn_readlane((int)x, (int)l); }
-__device__ __forceinline__ u64 wave_sum_u64(u64 x) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) x += shfl_xor_u64(x, m);
-  return x;
-}
-__device__ __forceinline__ i64 wave_sum_i64(i64 x) { return (i64)wave_sum_u64((u64)x); }
+// Whole-wave reductions on DPP (row_shr 1/2/4/8, row_bcast 15/31, as the scan above):
+// no cross-lane address registers (ds_bpermute index VGPRs that the compiler would
+// keep live through the whole kernel).  The result is uniform (lane 63).
+#define A5X_DPP_REDUCE(x, OP)                                                                 \
+  do {                                                                                         \
+    x = OP(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));            \
+    x = OP(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));            \
+    x = OP(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));            \
+    x = OP(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));            \
+    x = OP(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));            \
+    x = OP(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));            \
+  } while (0)
+__device__ __forceinline__ u32 a5x_max(u32 a, u32 b) { return a > b ? a : b; }
+__device__ __forceinline__ u32 a5x_or(u32 a, u32 b) { return a | b; }
 __device__ __forceinline__ u32 wave_max_u32(u32 x) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) x = max(x, (u32)__shfl_xor((int)x, m));
-  return x;
+  A5X_DPP_REDUCE(x, a5x_max);
+  return lane63(x);
 }
 __device__ __forceinline__ u32 wave_or_u32(u32 x) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) x |= (u32)__shfl_xor((int)x, m);
-  return x;
+  A5X_DPP_REDUCE(x, a5x_or);
+  return lane63(x);
 }
+// 64-bit sum (mod 2^64, so also for two's-complement i64) in three 24/24/16-bit parts:
+// each part's 64-lane sum fits 32 bits
+__device__ __forceinline__ u64 wave_sum_u64(u64 x) {
+  u32 a = wave_incl_scan_u32((u32)x & 0xFFFFFFu);
+  u32 b = wave_incl_scan_u32((u32)(x >> 24) & 0xFFFFFFu);
+  u32 c = wave_incl_scan_u32((u32)(x >> 48));
+  return (u64)lane63(a) + ((u64)lane63(b) << 24) + ((u64)lane63(c) << 48);
+}
+__device__ __forceinline__ i64 wave_sum_i64(i64 x) { return (i64)wave_sum_u64((u64)x); }
 // readfirstlane returns int: convert through u32 so nothing sign-extends
 __device__ __forceinline__ u32 uniform(u32 x) { return (u32)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ u64 uniform64(u64 x) {
@@ -876,8 +891,8 @@ struct ExpArgs {
   const u64* rec;        // FAST plan records (k_keyspace_thread)
   const u32* roff;       // per word: record offset into rec
   u64 rec_n;             // u64 in rec
-  u32 ablate;            // timing experiments only (A5X_ABLATE): 8 no rounds, 2 no ring
-                         // writes, 4 no global stores; output is garbage when set
+  u32 ablate;            // diagnostic build only (-DA5X_DIAG, A5X_ABLATE): 8 no rounds,
+                         // 4 no global stores; output is garbage when set
 };
 
 // Record the first tripped guard (code + context) and flag the call as failed.
@@ -1196,27 +1211,34 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 //           instruction, consecutive lanes consecutive addresses).
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
-#define FX_RING 4096  // per-wave linear output staging (bytes), then 4 trash dwords per lane;
+#ifndef FX_RING
+#define FX_RING 5120  // per-wave linear output staging (bytes), then one trash dword per lane;
+#endif
                       // during the window setup bytes [16, 16 + 8 FX_WREC) hold the window's
                       // small records (ring block 0 keeps the run's partial block)
-#define FX_TRASH 512  // trash dwords after the ring (64 lanes + 3, 4-B lane stride)
+#define FX_TRASH 256  // 64 lanes x 4 B
+#ifndef FX_WW
 #define FX_WW 32      // window words
+#endif
+#ifndef FX_NBE
 #define FX_NBE 256    // big entries per window (16 B each); [FX_ZBE] is the empty piece
+#endif
 #define FX_ZBE (FX_NBE - 1)
+#define FX6_ZBE FX_ZBE
+// window records: ring bytes [16, FX_RING) during the setup; the last u64 is the zero slot
+#define FX_RZ ((FX_RING - 16) / 8 - 1)
+#define FX_K 4        // candidates per lane run (a5x_fx6.h)
 
-// The window's small-piece records live in the ring (from byte 16, on into the
-// trash dwords) during the window setup (rec[FX_ZSLOT] = 0); the rounds then reuse
-// those bytes as output staging.
+// The window's small-piece records live in the ring (from byte 16) during the window
+// setup (rec[FX_ZSLOT] = 0); the rounds then reuse those bytes as output staging.
 struct FXWin {
   uint4 be[FX_NBE];        // big entries: 15 content bytes, length in byte 15
-  // per word j, big piece b: {magic, (R - 1) | base << 8 | x << 16} at wi[j][b / 2].{xy|zw};
-  // x of piece 0 = bits 0-15 of the word's first candidate c0, x of piece 1 = c0
-  // bits 16-23 | big piece count << 8 (ranks are taken mod 2^24: FW_PMAX_CNT)
-  uint4 wi[FX_WW][2];
+  uint4 wq[FX_WW][2];      // per word (a5x_fx6.h): magics; R - 1 | entry bases | first run
+  u32 rb[FX_WW + 4];       // first rank of the word inside the window
+  u32 re[FX_WW + 4];       // rank end of the word inside the window
   u32 mag[FB_RMAX + 4];    // fr_magic(R), R <= FB_RMAX
 };
-static_assert(FW_RMAX < FX_ZSLOT && FB_EMAX < FX_ZBE, "a FAST record must fit a window");
-static_assert(16 + 8 * FX_WREC <= FX_RING, "window records must fit the ring");
+static_assert(FW_RMAX < FX_RZ && FB_EMAX < FX_ZBE, "a FAST record must fit a window");
 
 // Closed-form bytes of candidates [0, r) of a FAST word (candidate r <-> index r + 1
 // in the piece mixed radix, piece 0 least significant).  rec = the word's record
@@ -1228,12 +1250,11 @@ __device__ u64 fast_prefix_bytes(const u64* rec, u64 r) {
   u32 Rl = 1;
   u64 G = 0;
   if (lane < np) { G = rec[1 + lane]; Rl = frd_R(G); }
-  u32 inc = Rl;  // inclusive prefix product of R over pieces
-#pragma unroll
-  for (int d = 1; d < 16; d <<= 1) {
-    const u32 y = (u32)__shfl_up((int)inc, d);
-    if ((int)lane >= d) inc *= y;
-  }
+  u32 inc = Rl;  // inclusive prefix product of R over pieces (one DPP row: np <= 16)
+  inc *= (u32)__builtin_amdgcn_update_dpp(1, (int)inc, 0x111, 0xf, 0xf, false);
+  inc *= (u32)__builtin_amdgcn_update_dpp(1, (int)inc, 0x112, 0xf, 0xf, false);
+  inc *= (u32)__builtin_amdgcn_update_dpp(1, (int)inc, 0x114, 0xf, 0xf, false);
+  inc *= (u32)__builtin_amdgcn_update_dpp(1, (int)inc, 0x118, 0xf, 0xf, false);
   i64 part = 0, base0 = 0;
   if (lane < np) {
     const u64* ent = rec + 1 + np + frd_ebase(G);
@@ -1254,7 +1275,7 @@ __device__ u64 fast_prefix_bytes(const u64* rec, u64 r) {
 // relative to out_base); bytes [lo, pos) belong to this wave's current run.
 struct FxRun {
   u64 B, lo, pos;
-  u32 carry;  // bytes [pos & ~3, pos) of the unfinished dword (not yet in the ring)
+  u32 carry;  // bytes [pos & ~3, pos) of the unfinished dword
   bool open;
 };
 
@@ -1267,8 +1288,11 @@ __device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) 
   const u64 B = uniform64(R.B);
   if (B + 16ull * nb > a.out_cap) { guard_trip(a, 1, B, R.lo, R.pos, a.out_cap); R.B = B + 16ull * nb; return; }
   const uint4* r4 = (const uint4*)ring;
+#ifdef A5X_DIAG
   if (a.ablate & 4u) {
-  } else if (B >= R.lo) {
+  } else
+#endif
+  if (B >= R.lo) {
     for (u32 b = lane; b < nb; b += 64) *(uint4*)(a.out + B + 16ull * b) = r4[b];
   } else {
     for (u32 b = lane; b < nb; b += 64) store_block(a, B + 16ull * b, r4[b], R.lo, R.pos);
@@ -1294,102 +1318,7 @@ __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) 
   R.open = false;
 }
 
-// One round: candidates [rr, rr + ncand); lane L takes candidates K L .. K L + K - 1
-// (one contiguous output run; candidate c of the lane in window word lo[c]).  NB >=
-// the big piece count of every word in the round.
-template <int NB, int K>
-__device__ __forceinline__ void fx_round(FXWin& F, u32* ring, const ExpArgs& a, FxRun& R, u64 rr, u32 ncand,
-                                         const u32 (&lo)[K]) {
-  const u32 lane = lane_id();
-  const u32 T = FX_RING / 4 + lane;  // the lane's trash dwords T .. T+3 (overlapping the next
-                                     // lanes': garbage; one store instruction hits consecutive dwords)
-  const u32 nact = (ncand + K - 1) / K;     // lanes with at least one candidate
-  // pass 1: big piece digits of n = rank + 1 -> entries, length
-  uint4 e[K][NB];
-  u32 len = 0;
-#pragma unroll
-  for (int c = 0; c < K; c++) {
-    const uint4 b01 = F.wi[lo[c]][0];
-    const uint4 b23 = NB > 2 ? F.wi[lo[c]][1] : make_uint4(0, 0, 0, 0);
-    const u32 wc = (b01.y >> 16) | (((b01.w >> 16) & 255u) << 16);
-    const u32 nb = K * lane + c < ncand ? (b01.w >> 24) & 7u : 0u;
-    u32 n = (((u32)rr + K * lane + c - wc) & 0xFFFFFFu) + 1u;
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-      const u32 magic = b == 0 ? b01.x : b == 1 ? b01.z : b == 2 ? b23.x : b23.z;
-      const u32 rb = b == 0 ? b01.y : b == 1 ? b01.w : b == 2 ? b23.y : b23.w;
-      const u32 rm1 = rb & 63u;
-      // R = 1 (magic 0): q = n, digit 0; branch-free
-      const u32 q = __umulhi(n, magic) + (magic ? 0u : n);
-      const u32 d = n - __umul24(q, rm1 + 1u);
-      n = q;
-      const u32 idx = (u32)b < nb ? ((rb >> 8) & 255u) + d : (u32)FX_ZBE;
-      e[c][b] = F.be[idx];
-      len += e[c][b].w >> 24;
-    }
-  }
-  const u32 incl = wave_incl_scan_u32(len);
-  const u32 tot = lane63(incl);
-  const u32 o = (u32)(R.pos - R.B) + incl - len;
-  // pass 2: append the pieces as whole aligned dwords (see fb_put)
-  u32 pn = o & 3u, D = o >> 2, acc = 0, hd = 0;
-  u32 pv = lane == 0 ? (R.carry << ((32u - 8u * pn) & 31u)) : 0u;
-  bool hp = lane != 0 && pn != 0;
-  if (!(a.ablate & 2u)) {
-#pragma unroll
-    for (int c = 0; c < K; c++) {
-#pragma unroll
-      for (int b = 0; b < NB; b++) {
-        const u32 ev[4] = {e[c][b].x, e[c][b].y, e[c][b].z, e[c][b].w};
-        fb_put(ev, pv, pn, D, hp, hd, acc, ring, T);
-      }
-    }
-  }
-  const u32 hnext = (u32)__shfl_down((int)hd, 1);
-  ring[(lane + 1 < nact && pn) ? D : T] = acc | hnext;
-  R.carry = readlane_u32(acc, nact - 1);
-  R.pos = uniform64(R.pos + tot);
-  WAVE_SYNC();
-  fx_flush(R, ring, a);
-}
-
-// Rounds of <= K nl consecutive candidates [g, gend) of the window's k words.  K = 1:
-// each round runs the body for the largest big piece count among the words it
-// spans (m3 / m4: window words with >= 3 / 4 big pieces); K = 2: no word of the
-// window has more than 2 big pieces.
-template <int K>
-__device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, const ExpArgs& a, FxRun& R, u64 g, u64 gend, u32 k,
-                                          u32 nl, u32 c0rel, u64 m3, u64 m4) {
-  const u32 lane = lane_id();
-  if (a.ablate & 8u) return;  // timing: window setup only
-  u32 jcur = 0;  // word holding the round's first candidate (uniform)
-  for (u64 rr = g; rr < gend; rr += (u64)K * nl) {
-    const u32 rrel = (u32)(rr - g);
-    const u32 ncand = uniform((u32)min((u64)K * nl, gend - rr));
-    // word of each candidate: count the word starts it has passed
-    u32 lo[K];
-#pragma unroll
-    for (int c = 0; c < K; c++) lo[c] = jcur;
-    const u32 jf = jcur;
-    for (;;) {
-      const u32 jn = uniform(jcur + 1);
-      if (jn >= k) break;
-      const u32 sj = uniform(readlane_u32(c0rel, jn));
-      if (sj >= rrel + ncand) break;
-      jcur = jn;
-#pragma unroll
-      for (int c = 0; c < K; c++) lo[c] += (rrel + K * lane + c >= sj) ? 1u : 0u;
-    }
-    if (K == 2) {
-      fx_round<2, K>(F, ring, a, R, rr, ncand, lo);
-    } else {
-      const u64 span = ((2ull << (jcur - jf)) - 1ull) << jf;  // words jf .. jcur
-      if (span & m4) fx_round<4, K>(F, ring, a, R, rr, ncand, lo);
-      else if (span & m3) fx_round<3, K>(F, ring, a, R, rr, ncand, lo);
-      else fx_round<2, K>(F, ring, a, R, rr, ncand, lo);
-    }
-  }
-}
+#include "a5x_fx6.h"
 
 // Window metadata of words w .. w + FX_WW - 1 (lane j <-> word w + j, same keyspace
 // tile), all loads issued together; the next window's is prefetched during rounds.
@@ -1412,6 +1341,38 @@ __device__ __forceinline__ FxMeta fx_meta(const ExpArgs& a, u64 w) {
 
 #define FX_PF 256  // prefetched record u64 (2 x 16 B per lane)
 
+// ring flush for a5x_fx6.h rounds
+struct FxFlush {
+  u32* ring;
+  const ExpArgs* a;
+  __device__ __forceinline__ void operator()(FxRun& R) { fx_flush(R, ring, *a); }
+};
+
+// The window's rounds: T runs of K candidates, nl runs per round; each round takes
+// the largest big-piece count among the words it spans (m2 / m3 / m4: window words
+// with >= 2 / 3 / 4 big pieces).
+template <int K>
+__device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FxFlush& fl, u32 T, u32 k, u32 rw, u64 m2,
+                                          u64 m3, u64 m4) {
+  const u32 lane = lane_id();
+  const u32 ringa = fx6_addr(ring), trash = ringa + FX_RING + 4u * lane;
+  const u32 cap = FX_RING - 32u;
+  u32 jcur = 0;
+  for (u32 rr = 0; rr < T;) {
+    const u32 nr = min(64u, T - rr);
+    const u32 j = fx6_word(rw, k, rr, nr, jcur);
+    const bool act = lane < nr;
+    const u32 jl = readlane_u32(j, nr - 1u);
+    const u64 span = ((2ull << (jl - jcur)) - 1ull) << jcur;  // words jcur .. jl
+    u32 took;
+    if (span & m4) took = fx6_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
+    else if (span & m3) took = fx6_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
+    else if (span & m2) took = fx6_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
+    else took = fx6_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
+    rr += took;
+  }
+}
+
 __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
   u64* const rec = (u64*)(ring + 4);  // ring bytes [16, 16 + 8 FX_WREC)
@@ -1428,6 +1389,8 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
   u64 g = g0;
   FxRun R;
   R.open = false; R.B = 0; R.lo = 0; R.pos = 0; R.carry = 0;
+  FxFlush fl;
+  fl.ring = ring; fl.a = &a;
   FxMeta M = fx_meta(a, w);
   u64 pfb = ~0ull;  // records [pfb, pfb + FX_PF) prefetched into pf0 / pf1 (pfb even)
   uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;
@@ -1436,16 +1399,16 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
     // ---- window: lane j <-> word w + j ----
     const u64 c0 = M.c0, c1 = M.c1;
-    const u32 fl = M.fl;
+    const u32 fl_ = M.fl;
     const bool hasc = c1 > c0 && c0 != ~0ull;
-    const bool fast = (fl & A5X_WF_FAST) && c0 < g1;
-    const u32 rs = (fast && hasc) ? ff_rsize(fl) : 0u;
+    const bool fast = (fl_ & A5X_WF_FAST) && c0 < g1;
+    const u32 rs = (fast && hasc) ? ff_rsize(fl_) : 0u;
     const u32 incR = wave_incl_scan_u32(rs);
     // records must be one contiguous range (complex words have slots elsewhere)
     const u64 rm = __ballot(rs > 0);
     const u32 rbase = readlane_u32(M.roff, rm ? (u32)__builtin_ctzll(rm) : 0u);
     const bool contig = rs == 0 || M.roff == rbase + (incR - rs);
-    const bool ok = fast && incR < FX_ZSLOT && contig;
+    const bool ok = fast && incR < FX_RZ && contig;
     const u64 badm = __ballot(!ok);
     u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
     STAMP(0);
@@ -1475,8 +1438,8 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
       const u32 i0 = 2 * lane, i1 = 2 * (lane + 64);
       if (i0 >= d) rec[i0 - d] = ((u64)pf0.y << 32) | pf0.x;
       if (i0 + 1 >= d) rec[i0 + 1 - d] = ((u64)pf0.w << 32) | pf0.z;
-      if (i1 - d < FX_ZSLOT) rec[i1 - d] = ((u64)pf1.y << 32) | pf1.x;
-      if (i1 + 1 - d < FX_ZSLOT) rec[i1 + 1 - d] = ((u64)pf1.w << 32) | pf1.z;
+      if (i1 - d < FX_RZ) rec[i1 - d] = ((u64)pf1.y << 32) | pf1.x;
+      if (i1 + 1 - d < FX_RZ) rec[i1 + 1 - d] = ((u64)pf1.w << 32) | pf1.z;
     } else {
       const u64* s64 = a.rec + src0;
       if ((src0 & 1) == 0) {
@@ -1488,7 +1451,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     }
     const u32 rb = incR - rs;
     const u64 bo = M.bo;
-    if (lane == 0) rec[FX_ZSLOT] = 0;
+    if (lane == 0) rec[FX_RZ] = 0;
     WAVE_SYNC();
     STAMP(4);
     // ---- big pieces per word: R = product of the spanned small R ----
@@ -1508,6 +1471,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     if (over) k = (u32)__builtin_ctzll(over);  // the window ends where the big entries do not fit
     if (k == 0) { guard_trip(a, 6, chunk, w, E, incE); break; }
     // ---- prefetch the next window: metadata, and records if they continue this window's ----
+#ifndef FX_NOPF
     const FxMeta Mn = fx_meta(a, w + k);
     {
       const u64 nx = src0 + readlane_u32(incR, k - 1);
@@ -1520,16 +1484,31 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
         pfb = ~0ull;
       }
     }
-    const u32 maxl = lane < k ? frh_maxl(hdr) : 0u;
+#endif
+    const bool inw = lane < k;
+    const u32 maxl = inw ? frh_maxl(hdr) : 0u;
     const u32 winmax = wave_max_u32(maxl);
-    const u64 m3 = __ballot(lane < k && nbw >= 3), m4 = __ballot(lane < k && nbw >= 4);
+    const u64 m2 = __ballot(inw && nbw >= 2), m3 = __ballot(inw && nbw >= 3), m4 = __ballot(inw && nbw >= 4);
     const u32 ebase = incE - E;
-    if (lane < k) {
+    // ---- per-word info: magics, R - 1, entry bases (pieces past the count: R 1, the
+    // empty entry), the word's ranks inside [g, g1) and its runs ----
+    // candidates per run: a round always takes at least one run (K (longest) <= ring)
+    const u32 K = FX_K * winmax + 16u <= FX_RING - 32u ? FX_K : 1u;
+    const u64 wc0 = uniform64(c0);
+    const u32 rbw = lane == 0 ? (u32)(g - wc0) : 0u;
+    const u32 rew = inw ? (u32)(min(c1, g1) - c0) : 0u;
+    const u32 nrun = inw && rs ? (rew - rbw + K - 1u) / K : 0u;
+    const u32 incr = wave_incl_scan_u32(nrun);
+    const u32 rw = inw ? incr - nrun : 0xffffffffu;
+    const u32 T = readlane_u32(incr, k - 1);
+    if (inw) {
       const u32 b1 = ebase + R0, b2 = b1 + R1, b3 = b2 + R2;
-      const u32 c0lo = (u32)c0 & 0xFFFFFFu;
-      F.wi[lane][0] = make_uint4(F.mag[R0], (R0 - 1u) | (ebase << 8) | ((c0lo & 0xFFFFu) << 16), F.mag[R1],
-                                 (R1 - 1u) | (b1 << 8) | ((c0lo >> 16) << 16) | (nbw << 24));
-      F.wi[lane][1] = make_uint4(F.mag[R2], (R2 - 1u) | (b2 << 8), F.mag[R3], (R3 - 1u) | (b3 << 8));
+      const u32 e1 = nbw > 1 ? b1 : (u32)FX_ZBE, e2 = nbw > 2 ? b2 : (u32)FX_ZBE, e3 = nbw > 3 ? b3 : (u32)FX_ZBE;
+      const u32 rmk = (R0 - 1u) | ((R1 - 1u) << 6) | ((R2 - 1u) << 12) | ((R3 - 1u) << 18);
+      F.wq[lane][0] = make_uint4(F.mag[R0], F.mag[R1], F.mag[R2], F.mag[R3]);
+      F.wq[lane][1] = make_uint4(rmk, (nbw ? ebase : (u32)FX_ZBE) | (e1 << 16), e2 | (e3 << 16), rw);
+      F.rb[lane] = rbw;
+      F.re[lane] = rew;
     }
     WAVE_SYNC();
     STAMP(5);
@@ -1555,15 +1534,15 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
         const u32 nbj = (u32)__shfl((int)nbw, (int)j);
         if (t < etot) {
           // big piece b of word j holding entry u, and the combination c
-          const uint4 q01 = F.wi[j][0], q23 = F.wi[j][1];
-          const u32 b0 = (q01.y >> 8) & 255u;
-          const u32 s1 = ((q01.w >> 8) & 255u) - b0, s2 = ((q23.y >> 8) & 255u) - b0, s3 = ((q23.w >> 8) & 255u) - b0;
+          const uint4 q1 = F.wq[j][1];
+          const u32 b0 = q1.y & 0xFFFFu;
+          const u32 s1 = (q1.y >> 16) - b0, s2 = (q1.z & 0xFFFFu) - b0, s3 = (q1.z >> 16) - b0;
           u32 b = 0, cb = 0;
           if (nbj > 1 && u >= s1) { b = 1; cb = s1; }
           if (nbj > 2 && u >= s2) { b = 2; cb = s2; }
           if (nbj > 3 && u >= s3) { b = 3; cb = s3; }
           u32 ent[4];
-          fb_entry(rec, wrb, b, u - cb, ent);
+          fb_entry(rec, wrb, b, u - cb, ent, FX_RZ);
           F.be[t] = make_uint4(ent[0], ent[1], ent[2], ent[3]);
         }
       }
@@ -1571,7 +1550,6 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     WAVE_SYNC();
     STAMP(1);
     // ---- run position of g ----
-    const u64 wc0 = uniform64(c0);
     const u64 r0 = g - wc0;
     u64 pos = uniform64(bo) - a.out_base;
     if (r0) pos += fast_prefix_bytes(rec + readlane_u32(rb, 0), r0);
@@ -1581,19 +1559,21 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     }
     STAMP(2);
     // ---- rounds ----
-    const u64 gend = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
-    const u32 c0rel = (lane < k) ? (u32)(c0 > g ? c0 - g : 0) : 0xffffffffu;
-    if (m3 == 0) {
-      const u32 nl = uniform(min(64u, (FX_RING - 32) / (2u * max(winmax, 1u))));
-      fx_rounds<2>(F, ring, a, R, g, gend, k, nl, c0rel, m3, m4);
-    } else {
-      const u32 nl = uniform(min(64u, (FX_RING - 32) / max(winmax, 1u)));
-      fx_rounds<1>(F, ring, a, R, g, gend, k, nl, c0rel, m3, m4);
+#ifdef A5X_DIAG
+    if (!(a.ablate & 8u))
+#endif
+    {
+      if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4);
+      else fx_rounds<1>(F, ring, R, fl, T, k, rw, m2, m3, m4);
     }
     STAMP(3);
-    g = gend;
+    g = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     w += k;
+#ifndef FX_NOPF
     M = Mn;
+#else
+    M = fx_meta(a, w);
+#endif
     WAVE_SYNC();
   }
   fx_close(R, ring, a);
@@ -1603,7 +1583,10 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
 
 __device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + FX_TRASH + (u32)sizeof(FXWin) + 15u) & ~15u; }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_expand_fast(ExpArgs a) {
+#ifndef FX_WPE
+#define FX_WPE 3
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE))) k_expand_fast(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   uint8_t* mine = smem + wv * lds_per_wave_fast();
@@ -1671,7 +1654,7 @@ __global__ void __launch_bounds__(64) k_locate(ExpArgs a, const u64* cands, u32 
   __syncthreads();
   const Tab T = tab_view(smem);
   LdsB& S = *(LdsB*)(smem + ((a.table_bytes + 15u) & ~15u));
-  for (u32 i = 0; i < n; i++) {
+  for (u32 i = blockIdx.x; i < n; i += gridDim.x) {  // one wave per query
     const u64 g = cands[i];
     if (g >= a.cand_off[a.nw]) { if (lane_id() == 0) out_bytes[i] = a.byte_off[a.nw]; continue; }
     // largest w with cand_off[w] <= g (that word has count > 0)
@@ -1845,7 +1828,8 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
 
 hipError_t a5x_launch_locate(const A5xExpLaunch& L, const u64* cands, u32 n, u64* out_bytes, hipStream_t st) {
   ExpArgs a = exp_args(L);
-  hipLaunchKernelGGL(k_locate, dim3(1), dim3(64), a5x_keyspace_wave_lds(L.table_bytes), st, a, cands, n, out_bytes);
+  hipLaunchKernelGGL(k_locate, dim3(n < 1024 ? (n ? n : 1) : 1024), dim3(64), a5x_keyspace_wave_lds(L.table_bytes), st, a,
+                     cands, n, out_bytes);
   return hipGetLastError();
 }
 

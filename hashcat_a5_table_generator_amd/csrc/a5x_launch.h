@@ -125,7 +125,7 @@ struct A5xDigLaunch {
   uint64_t nbytes;
   int algo;            // A5X_ALGO_MD5 / A5X_ALGO_NTLM
   const uint32_t* bitmap;
-  uint32_t bm_log2;
+  uint32_t bm_mask;    // prefilter index mask: 2^k - 1 for a 2^k-bit bitmap (k <= 32)
   const uint4* table;  // open addressing, all-zero = empty
   uint64_t tmask;
   uint32_t has_zero_target;

@@ -729,7 +729,7 @@ A5X_HD u32 fb_R(const u64* wrec, u32 wrb, u64 h, u32 b) {
 }
 
 // entry c of big piece b (x, y, z, w = bytes 0-3, 4-7, 8-11, 12-14 + length)
-A5X_HD void fb_entry(const u64* wrec, u32 wrb, u32 b, u32 c, u32 out[4]) {
+A5X_HD void fb_entry(const u64* wrec, u32 wrb, u32 b, u32 c, u32 out[4], u32 zslot = FX_ZSLOT) {
   const u64 h = wrec[wrb];
   const u32 nb = frh_nbig(h), np = frh_np(h);
   const u32 sp0 = frh_bstart(h, b), sp1 = b + 1 < nb ? frh_bstart(h, b + 1) : np;
@@ -739,13 +739,13 @@ A5X_HD void fb_entry(const u64* wrec, u32 wrb, u32 b, u32 c, u32 out[4]) {
 #pragma unroll
   for (u32 i = 0; i < FB_SPAN; i++) {
     const bool valid = sp0 + i < sp1;
-    const u64 G = wrec[valid ? wrb + 1 + sp0 + i : (u32)FX_ZSLOT];
+    const u64 G = wrec[valid ? wrb + 1 + sp0 + i : zslot];
     const u32 ghi = (u32)(G >> 32);
     u32 q = (u32)(((u64)c * (u32)G) >> 32);
     q += c & (u32)((int)ghi >> 31);  // R = 1: q = c
     const u32 d = c - q * (((ghi >> 8) & 31u) + 1u);
     c = q;
-    const u64 ev = wrec[valid ? wbe + (ghi & 255u) + d : (u32)FX_ZSLOT];
+    const u64 ev = wrec[valid ? wbe + (ghi & 255u) + d : zslot];
     const u64 cv = ev & FW_M56;
     if (off < 8) {
       lo64 |= cv << (8 * off);
