@@ -124,6 +124,7 @@ struct a5x_ctx {
   uint64_t seg = 1024;        // candidates per per-word-path segment (a radix round there costs ~64x a FAST one)
   uint64_t chunk = 8192;      // candidates per expand wave (sweep on C3: 8192 < 16384 < 32768 ms)
   uint32_t waves_per_block = 4;
+  uint32_t waves_per_block_fast = 1;
   uint32_t ablate = 0;        // A5X_ABLATE: read only by the diagnostic build (-DA5X_DIAG)
 };
 
@@ -448,6 +449,7 @@ A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   E.CH = c->chunk; E.SEG = c->seg; E.mn = mn; E.mx = mx; E.err = c->d_scalars + 2;
   E.dbg = (uint64_t*)(c->d_scalars + 16);
   E.waves_per_block = c->waves_per_block;
+  E.waves_per_block_fast = c->waves_per_block_fast;
   E.rec = c->rec.p; E.roff = c->roff.p; E.rec_n = c->rec.cap;
   E.ablate = c->ablate;
   return E;
@@ -935,6 +937,7 @@ int a5x_create(int device, a5x_ctx** out) {
   if (const char* e = getenv("A5X_ABLATE")) c->ablate = (uint32_t)atoi(e);  // timing experiments only
 #endif
   if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
+  if (const char* e = getenv("A5X_FAST_WAVES")) c->waves_per_block_fast = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   *out = c;
   return A5X_OK;
 }

@@ -1212,7 +1212,7 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
 #ifndef FX_RING
-#define FX_RING 5120  // per-wave linear output staging (bytes), then one trash dword per lane;
+#define FX_RING 4096  // per-wave linear output staging (bytes), then one trash dword per lane;
 #endif
                       // during the window setup bytes [16, 16 + 8 FX_WREC) hold the window's
                       // small records (ring block 0 keeps the run's partial block)
@@ -1239,6 +1239,7 @@ struct FXWin {
   u32 mag[FB_RMAX + 4];    // fr_magic(R), R <= FB_RMAX
 };
 static_assert(FW_RMAX < FX_RZ && FB_EMAX < FX_ZBE, "a FAST record must fit a window");
+static_assert(FX_RING + FX_TRASH + sizeof(FXWin) <= 10240, "16 waves per CU need <= 10 KiB of LDS per wave");
 
 // Closed-form bytes of candidates [0, r) of a FAST word (candidate r <-> index r + 1
 // in the piece mixed radix, piece 0 least significant).  rec = the word's record
@@ -1321,7 +1322,8 @@ __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) 
 #include "a5x_fx6.h"
 
 // Window metadata of words w .. w + FX_WW - 1 (lane j <-> word w + j, same keyspace
-// tile), all loads issued together; the next window's is prefetched during rounds.
+// tile), all loads issued together.  (No prefetch across the rounds: the registers it
+// holds cost a wave per SIMD, and occupancy hides these loads better.)
 struct FxMeta {
   u64 c0, c1, bo;
   u32 fl, roff;
@@ -1338,8 +1340,6 @@ __device__ __forceinline__ FxMeta fx_meta(const ExpArgs& a, u64 w) {
   m.bo = (lane == 0 && w < a.nw) ? a.byte_off[w] : 0;
   return m;
 }
-
-#define FX_PF 256  // prefetched record u64 (2 x 16 B per lane)
 
 // ring flush for a5x_fx6.h rounds
 struct FxFlush {
@@ -1392,8 +1392,6 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
   FxFlush fl;
   fl.ring = ring; fl.a = &a;
   FxMeta M = fx_meta(a, w);
-  u64 pfb = ~0ull;  // records [pfb, pfb + FX_PF) prefetched into pf0 / pf1 (pfb even)
-  uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;
   STAMP_DECL
   while (g < g1) {
     if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
@@ -1423,7 +1421,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
       M = fx_meta(a, w);
       continue;
     }
-    // ---- small records -> LDS (one contiguous range; prefetched when it continues the last) ----
+    // ---- small records -> LDS (one contiguous range) ----
     const u64 fm = __ballot(lane < k && rs > 0);
     if (fm == 0) {  // only words without candidates: skip them
       w += k;
@@ -1433,14 +1431,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     const u32 jf = (u32)__builtin_ctzll(fm);
     const u64 src0 = (u64)readlane_u32(M.roff, jf);
     const u32 ntot = readlane_u32(incR, k - 1);
-    if (pfb <= src0 && src0 + ntot <= pfb + FX_PF) {
-      const u32 d = (u32)(src0 - pfb);  // 0 .. : the prefetched u64 i lands at rec[i - d]
-      const u32 i0 = 2 * lane, i1 = 2 * (lane + 64);
-      if (i0 >= d) rec[i0 - d] = ((u64)pf0.y << 32) | pf0.x;
-      if (i0 + 1 >= d) rec[i0 + 1 - d] = ((u64)pf0.w << 32) | pf0.z;
-      if (i1 - d < FX_RZ) rec[i1 - d] = ((u64)pf1.y << 32) | pf1.x;
-      if (i1 + 1 - d < FX_RZ) rec[i1 + 1 - d] = ((u64)pf1.w << 32) | pf1.z;
-    } else {
+    {
       const u64* s64 = a.rec + src0;
       if ((src0 & 1) == 0) {
         const uint4* src = (const uint4*)s64;
@@ -1470,21 +1461,6 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     const u64 over = __ballot(lane < k && incE > FX_ZBE);
     if (over) k = (u32)__builtin_ctzll(over);  // the window ends where the big entries do not fit
     if (k == 0) { guard_trip(a, 6, chunk, w, E, incE); break; }
-    // ---- prefetch the next window: metadata, and records if they continue this window's ----
-#ifndef FX_NOPF
-    const FxMeta Mn = fx_meta(a, w + k);
-    {
-      const u64 nx = src0 + readlane_u32(incR, k - 1);
-      pfb = nx & ~1ull;
-      if (pfb + FX_PF <= a.rec_n) {
-        const uint4* src = (const uint4*)(a.rec + pfb);
-        pf0 = src[lane];
-        pf1 = src[lane + 64];
-      } else {
-        pfb = ~0ull;
-      }
-    }
-#endif
     const bool inw = lane < k;
     const u32 maxl = inw ? frh_maxl(hdr) : 0u;
     const u32 winmax = wave_max_u32(maxl);
@@ -1569,11 +1545,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     STAMP(3);
     g = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     w += k;
-#ifndef FX_NOPF
-    M = Mn;
-#else
     M = fx_meta(a, w);
-#endif
     WAVE_SYNC();
   }
   fx_close(R, ring, a);
@@ -1584,7 +1556,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
 __device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + FX_TRASH + (u32)sizeof(FXWin) + 15u) & ~15u; }
 
 #ifndef FX_WPE
-#define FX_WPE 3
+#define FX_WPE 4  // 16 waves per CU: <= 128 VGPRs, <= 10 KiB LDS per wave
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE))) k_expand_fast(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1813,7 +1785,7 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   const u64 c0 = L.cand_begin / L.CH, c1 = (L.cand_end + L.CH - 1) / L.CH;
   const u64 nchunks = c1 - c0;
   if (nchunks == 0) return hipSuccess;
-  const u32 waves = L.waves_per_block;
+  const u32 waves = kind == 0 ? L.waves_per_block_fast : L.waves_per_block;
   const u64 nb = (nchunks + waves - 1) / waves;
   if (kind == 0)
     hipLaunchKernelGGL(k_expand_fast, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);

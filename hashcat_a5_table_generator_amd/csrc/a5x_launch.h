@@ -52,7 +52,8 @@ struct A5xExpLaunch {
   int mn, mx;
   uint32_t* err;
   uint64_t* dbg;
-  uint32_t waves_per_block;
+  uint32_t waves_per_block;       // k_expand_slow
+  uint32_t waves_per_block_fast;  // k_expand_fast (one wave per chunk; 1 measured fastest)
   const uint64_t* rec;
   const uint32_t* roff;
   uint64_t rec_n;   // u64 in rec
