@@ -37,19 +37,12 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_diag(verbose: bool = False, stamps: bool = True) -> str:
-    """Diagnostic variant in _build_diag/: per-phase s_memtime stamps (-DA5X_STAMPS) and the
-    A5X_ABLATE timing switches (-DA5X_DIAG); never loaded by the product or the tests."""
-    out = os.path.join(PKG, "_build_diag" if stamps else "_build_abl")
-    os.makedirs(out, exist_ok=True)
-    lib = os.path.join(out, "liba5x.so")
-    srcs = [os.path.join(CSRC, s) for s in LIB_SRCS]
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
-           *(["-DA5X_STAMPS"] if stamps else []), "-DA5X_DIAG", "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", lib]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    return lib
+def build_diag(verbose: bool = False) -> str:
+    """Diagnostic variant in _build_diag/: per-phase s_memtime stamps of the fast kernel
+    (-DA5X_STAMPS; tools/stamps.py).  Timing ablations are compile-time variants
+    (build_variant(name, ["FX_ABL=<mask>"]), a5x_kernels.hip FX_ABL).  Never loaded by
+    the product or the tests."""
+    return build_variant("diag", ["A5X_STAMPS"], verbose)
 
 
 def build_variant(name: str, defines, verbose: bool = False) -> str:

@@ -195,3 +195,95 @@ __device__ __forceinline__ u32 fx6_word(u32 rw, u32 k, u32 rr, u32 nl, u32& jcur
   }
   return j;
 }
+
+// ---------------------------------------------------------------------------
+// OR placement (FX_OR): the ring is kept zeroed between rounds and every piece ORs
+// its byte-shifted dwords into it (ds_or_b32).  Entries are zero past their length,
+// so the dwords a piece touches beyond its own bytes receive zeros: no ordering, no
+// pending-dword register, no shared-dword merge across lanes, no trash redirection.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fx7_or(u32 a, u32 v) {
+  __hip_atomic_fetch_or((fx6_lds32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// (NOOR: timing ablation of the diagnostic build -- the dwords are folded into sink
+// instead of stored)
+template <bool NOOR = false>
+__device__ __forceinline__ void fx7_put(const uint4 e, u32& P, u32& sink) {
+  const u32 n = P & 3u, base = P - n;
+  const u32 l = e.w >> 24, e3 = e.w & 0xFFFFFFu;
+  const u32 sel = fx6_sel(n);
+  const u32 t = n + l;
+  auto put = [&](u32 a, u32 v) {
+    if constexpr (NOOR) sink ^= v + a;
+    else fx7_or(a, v);
+  };
+  put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
+  put(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
+  if (__builtin_amdgcn_ballot_w64(t > 8u)) {  // pieces reaching a third dword (wave-uniform)
+    put(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
+    if (__builtin_amdgcn_ballot_w64(t > 12u)) {
+      put(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
+      if (__builtin_amdgcn_ballot_w64(t > 16u)) put(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
+    }
+  }
+  P += l;
+}
+
+// fx6_round with OR placement (same run / fit / scan logic; ring zero past R.pos)
+template <int NB, int K, bool NOOR = false, class FLUSH>
+__device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
+                                         u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush) {
+  const u32 lane = lane_id();
+  const uint4 q0 = wq[j][0], q1 = wq[j][1];
+  const u32 st = act ? (rr + lane - q1.w) * K + rb[j] : 0u;  // first rank of the run
+  const u32 cw = act ? re[j] : 0u;
+  const u32 nc = cw > st ? min((u32)K, cw - st) : 0u;
+  u32 d[4];
+  fx6_digits<NB>(st + 1u, q0, q1.x, d);
+  constexpr bool HOLD = NB <= 2;
+  uint4 ent[HOLD ? K : 1][HOLD ? NB : 1];
+  u32 idx[HOLD ? 1 : K][HOLD ? 1 : NB];
+  u32 len = 0;
+  const uint8_t* lenb = (const uint8_t*)be + 15;
+#pragma unroll
+  for (int c = 0; c < K; c++) {
+    if (c > 0) fx6_step<NB>(q1.x, d);
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const u32 ix = c < (int)nc ? fx6_eb(q1, b) + d[b] : (u32)FX6_ZBE;  // past the run: empty
+      if constexpr (HOLD) {
+        ent[c][b] = be[ix];
+        len += ent[c][b].w >> 24;
+      } else {
+        idx[c][b] = ix;
+        len += lenb[16u * ix];
+      }
+    }
+  }
+  const u32 incl = wave_incl_scan_u32(len);
+  const u32 used = (u32)(R.pos - R.B);
+  const bool fit = nc > 0 && used + incl <= cap;
+  const u32 nact = uniform((u32)__popcll(__ballot(fit)));
+  const u32 tot = nact ? readlane_u32(incl, nact - 1u) : 0u;
+  u32 P = ring + used + incl - len, sink = 0;
+  if (fit) {
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        uint4 e;
+        if constexpr (HOLD) e = ent[c][b];
+        else e = be[idx[c][b]];
+        fx7_put<NOOR>(e, P, sink);
+      }
+    }
+  }
+  if constexpr (NOOR) {
+    if (sink == 0x9E3779B9u) fx7_or(ring, 1u);  // keeps the folded dwords live
+  }
+  R.pos = uniform64(R.pos + tot);
+  WAVE_SYNC();
+  flush(R);
+  return nact;
+}

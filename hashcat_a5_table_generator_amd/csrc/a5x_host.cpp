@@ -125,7 +125,6 @@ struct a5x_ctx {
   uint64_t chunk = 8192;      // candidates per expand wave (sweep on C3: 8192 < 16384 < 32768 ms)
   uint32_t waves_per_block = 4;
   uint32_t waves_per_block_fast = 1;
-  uint32_t ablate = 0;        // A5X_ABLATE: read only by the diagnostic build (-DA5X_DIAG)
 };
 
 namespace {
@@ -451,7 +450,6 @@ A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   E.waves_per_block = c->waves_per_block;
   E.waves_per_block_fast = c->waves_per_block_fast;
   E.rec = c->rec.p; E.roff = c->roff.p; E.rec_n = c->rec.cap;
-  E.ablate = c->ablate;
   return E;
 }
 
@@ -933,9 +931,6 @@ int a5x_create(int device, a5x_ctx** out) {
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_MSEG")) c->mseg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_SEG")) c->seg = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
-#ifdef A5X_DIAG
-  if (const char* e = getenv("A5X_ABLATE")) c->ablate = (uint32_t)atoi(e);  // timing experiments only
-#endif
   if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   if (const char* e = getenv("A5X_FAST_WAVES")) c->waves_per_block_fast = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   *out = c;

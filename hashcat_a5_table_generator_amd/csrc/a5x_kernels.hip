@@ -891,8 +891,6 @@ struct ExpArgs {
   const u64* rec;        // FAST plan records (k_keyspace_thread)
   const u32* roff;       // per word: record offset into rec
   u64 rec_n;             // u64 in rec
-  u32 ablate;            // diagnostic build only (-DA5X_DIAG, A5X_ABLATE): 8 no rounds,
-                         // 4 no global stores; output is garbage when set
 };
 
 // Record the first tripped guard (code + context) and flag the call as failed.
@@ -1228,6 +1226,14 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 // window records: ring bytes [16, FX_RING) during the setup; the last u64 is the zero slot
 #define FX_RZ ((FX_RING - 16) / 8 - 1)
 #define FX_K 4        // candidates per lane run (a5x_fx6.h)
+#ifndef FX_ABL
+#define FX_ABL 0      // timing ablations (variant builds only; output is garbage when set):
+                      // 4 no global stores, 8 no rounds, 16 no big entries, 32 no prefix,
+                      // 64 no placement stores, 128 no ring re-zeroing
+#endif
+#ifndef FX_NOOR
+#define FX_OR         // OR placement into a zeroed ring (a5x_fx6.h fx7_round)
+#endif
 
 // The window's small-piece records live in the ring (from byte 16) during the window
 // setup (rec[FX_ZSLOT] = 0); the rounds then reuse those bytes as output staging.
@@ -1282,25 +1288,82 @@ struct FxRun {
 
 // Stream the complete 16-B blocks of [B, pos) and move the partial last block to
 // ring block 0.  The first block of a run may start before lo: byte-exact.
+#ifndef FX_NT
+#define FX_NT 1  // nontemporal output stores (write-once stream)
+#endif
+#ifndef FX_FLB
+#define FX_FLB 0 // flush: batch the ring block reads before the stores
+#endif
+static_assert(FX_RING / 16 <= 256, "fx_flush: at most 4 ring blocks per lane");
+__device__ __forceinline__ void fx_store16(uint8_t* p, const uint4 v) {
+#if FX_NT
+  typedef u32 v4u __attribute__((ext_vector_type(4)));
+  v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, (v4u*)p);
+#else
+  *(uint4*)p = v;
+#endif
+}
+
 __device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) {
   const u32 lane = lane_id();
   const u32 nb = uniform((u32)((R.pos - R.B) >> 4));
   if (nb == 0) return;
   const u64 B = uniform64(R.B);
   if (B + 16ull * nb > a.out_cap) { guard_trip(a, 1, B, R.lo, R.pos, a.out_cap); R.B = B + 16ull * nb; return; }
-  const uint4* r4 = (const uint4*)ring;
-#ifdef A5X_DIAG
-  if (a.ablate & 4u) {
-  } else
-#endif
-  if (B >= R.lo) {
-    for (u32 b = lane; b < nb; b += 64) *(uint4*)(a.out + B + 16ull * b) = r4[b];
-  } else {
-    for (u32 b = lane; b < nb; b += 64) store_block(a, B + 16ull * b, r4[b], R.lo, R.pos);
+  uint4* r4 = (uint4*)ring;
+#if FX_FLB
+  // all (<= 4) block reads in flight together, then the stores; block 0 of a run that
+  // starts inside it is stored byte-exact
+  uint4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const u32 b = lane + 64u * i;
+    if (b < nb) v[i] = r4[b];
   }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const u32 b = lane + 64u * i;
+    if (b < nb && !(FX_ABL & 4)) {
+      const u64 gb = B + 16ull * b;
+      if (i == 0 && gb < R.lo) store_block(a, gb, v[i], R.lo, R.pos);
+      else fx_store16(a.out + gb, v[i]);
+    }
+  }
+#ifdef FX_OR
+  // (OR placement: the flushed blocks back to zero)
+  if (!(FX_ABL & 128)) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const u32 b = lane + 64u * i;
+      if (b < nb) r4[b] = make_uint4(0, 0, 0, 0);
+    }
+  }
+#endif
+#else
+  // (OR placement: every flushed block is zeroed again behind its read)
+  if (B >= R.lo) {
+    for (u32 b = lane; b < nb; b += 64) {
+      if (!(FX_ABL & 4)) fx_store16(a.out + B + 16ull * b, r4[b]);
+#ifdef FX_OR
+      if (!(FX_ABL & 128)) r4[b] = make_uint4(0, 0, 0, 0);
+#endif
+    }
+  } else {
+    for (u32 b = lane; b < nb; b += 64) {
+      if (!(FX_ABL & 4)) store_block(a, B + 16ull * b, r4[b], R.lo, R.pos);
+#ifdef FX_OR
+      if (!(FX_ABL & 128)) r4[b] = make_uint4(0, 0, 0, 0);
+#endif
+    }
+  }
+#endif
   if (lane == 0) {
     const uint4 t = r4[nb];
-    ((uint4*)ring)[0] = t;
+#ifdef FX_OR
+    r4[nb] = make_uint4(0, 0, 0, 0);
+#endif
+    r4[0] = t;
   }
   R.B = B + 16ull * nb;
   WAVE_SYNC();
@@ -1309,12 +1372,19 @@ __device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) 
 // write the carried partial dword, flush everything up to pos (tail block byte-exact)
 __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) {
   if (!R.open) return;
+#ifndef FX_OR
   if (R.pos & 3u) {
     if (lane_id() == 0) ring[(u32)(R.pos - R.B) >> 2] = R.carry;
     WAVE_SYNC();
   }
+#endif
   fx_flush(R, ring, a);
-  if (R.pos > R.B && lane_id() == 0) store_block(a, R.B, ((const uint4*)ring)[0], max(R.lo, R.B), R.pos);
+  if (R.pos > R.B && lane_id() == 0) {
+    store_block(a, R.B, ((const uint4*)ring)[0], max(R.lo, R.B), R.pos);
+#ifdef FX_OR
+    ((uint4*)ring)[0] = make_uint4(0, 0, 0, 0);
+#endif
+  }
   WAVE_SYNC();
   R.open = false;
 }
@@ -1365,15 +1435,58 @@ __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FxFlush
     const u32 jl = readlane_u32(j, nr - 1u);
     const u64 span = ((2ull << (jl - jcur)) - 1ull) << jcur;  // words jcur .. jl
     u32 took;
+#ifdef FX_OR
+    (void)trash;
+#if FX_ABL & 64
+    if (true) {
+      if (span & m4) took = fx7_round<4, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+      else if (span & m3) took = fx7_round<3, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+      else if (span & m2) took = fx7_round<2, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+      else took = fx7_round<1, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+    } else
+#endif
+    if (span & m4) took = fx7_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+    else if (span & m3) took = fx7_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+    else if (span & m2) took = fx7_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+    else took = fx7_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+#else
     if (span & m4) took = fx6_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
     else if (span & m3) took = fx6_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
     else if (span & m2) took = fx6_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
     else took = fx6_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
+#endif
     rr += took;
   }
 }
 
-__device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
+// Big entry (a5x_plan.h fb_entry, same bytes): combination c of the span <= FB_SPAN small
+// pieces whose descriptors are rec[d0 ..], entries rec[wbe ..]; the loop runs smax
+// (wave-uniform) iterations instead of FB_SPAN.
+__device__ __forceinline__ uint4 fx_entry(const u64* rec, u32 d0, u32 wbe, u32 span, u32 smax, u32 c) {
+  u64 lo64 = 0, hi64 = 0;
+  u32 off = 0;
+#pragma unroll
+  for (u32 i = 0; i < FB_SPAN; i++) {
+    if (i >= smax) break;
+    const bool valid = i < span;
+    const u64 G = rec[valid ? d0 + i : (u32)FX_RZ];
+    const u32 ghi = (u32)(G >> 32);
+    u32 q = __umulhi(c, (u32)G);
+    q += c & (u32)((int)ghi >> 31);  // R = 1: q = c
+    const u32 d = c - q * (((ghi >> 8) & 31u) + 1u);
+    c = q;
+    const u64 ev = rec[valid ? wbe + (ghi & 255u) + d : (u32)FX_RZ];
+    const u64 cv = ev & FW_M56;
+    const u32 sh = 8u * off;
+    const u64 x = cv << (sh & 63u), y = cv >> ((64u - sh) & 63u);
+    lo64 |= off < 8u ? x : 0ull;
+    hi64 |= off < 8u ? (off ? y : 0ull) : x;
+    off += fw_len(ev);
+  }
+  return make_uint4((u32)lo64, (u32)(lo64 >> 32), (u32)hi64, ((u32)(hi64 >> 32) & 0xFFFFFFu) | (off << 24));
+}
+
+__device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
   u64* const rec = (u64*)(ring + 4);  // ring bytes [16, 16 + 8 FX_WREC)
   const u64 g0 = max(a.cand_begin, chunk * a.CH);
@@ -1384,6 +1497,9 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
   while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
   if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
   if (lane == 0) F.be[FX_ZBE] = make_uint4(0, 0, 0, 0);
+#ifdef FX_OR
+  for (u32 i = lane; i < FX_RING / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+#endif
   F.mag[lane] = fr_magic(lane);
   if (lane == 0) F.mag[FB_RMAX] = fr_magic(FB_RMAX);
   u64 g = g0;
@@ -1489,6 +1605,7 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     WAVE_SYNC();
     STAMP(5);
     // ---- build the big entries: lanes over the window's entries ----
+    if (!(FX_ABL & 16))
     {
       const u32 etot = readlane_u32(incE, k - 1);
       const u32 est = lane < k ? ebase : 0xffffffffu;
@@ -1508,19 +1625,21 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
         const u32 wrb = (u32)__shfl((int)rb, (int)j);
         const u32 u = t - (u32)__shfl((int)ebase, (int)j);
         const u32 nbj = (u32)__shfl((int)nbw, (int)j);
-        if (t < etot) {
-          // big piece b of word j holding entry u, and the combination c
-          const uint4 q1 = F.wq[j][1];
-          const u32 b0 = q1.y & 0xFFFFu;
-          const u32 s1 = (q1.y >> 16) - b0, s2 = (q1.z & 0xFFFFu) - b0, s3 = (q1.z >> 16) - b0;
-          u32 b = 0, cb = 0;
-          if (nbj > 1 && u >= s1) { b = 1; cb = s1; }
-          if (nbj > 2 && u >= s2) { b = 2; cb = s2; }
-          if (nbj > 3 && u >= s3) { b = 3; cb = s3; }
-          u32 ent[4];
-          fb_entry(rec, wrb, b, u - cb, ent, FX_RZ);
-          F.be[t] = make_uint4(ent[0], ent[1], ent[2], ent[3]);
-        }
+        const bool on = t < etot;
+        // big piece b of word j holding entry u, the combination c, its small pieces
+        const uint4 q1 = F.wq[on ? j : 0][1];
+        const u32 b0 = q1.y & 0xFFFFu;
+        const u32 s1 = (q1.y >> 16) - b0, s2 = (q1.z & 0xFFFFu) - b0, s3 = (q1.z >> 16) - b0;
+        u32 b = 0, cb = 0;
+        if (nbj > 1 && u >= s1) { b = 1; cb = s1; }
+        if (nbj > 2 && u >= s2) { b = 2; cb = s2; }
+        if (nbj > 3 && u >= s3) { b = 3; cb = s3; }
+        const u64 h = rec[on ? wrb : (u32)FX_RZ];
+        const u32 np = frh_np(h), nbh = frh_nbig(h);
+        const u32 sp0 = frh_bstart(h, b), sp1 = b + 1 < nbh ? frh_bstart(h, b + 1) : np;
+        const u32 span = on ? sp1 - sp0 : 0u;
+        const uint4 e = fx_entry(rec, wrb + 1u + sp0, wrb + 1u + np, span, wave_max_u32(span), u - cb);
+        if (on) F.be[t] = e;
       }
     }
     WAVE_SYNC();
@@ -1528,16 +1647,20 @@ __device__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chu
     // ---- run position of g ----
     const u64 r0 = g - wc0;
     u64 pos = uniform64(bo) - a.out_base;
+    if (!(FX_ABL & 32))
     if (r0) pos += fast_prefix_bytes(rec + readlane_u32(rb, 0), r0);
     if (!R.open || R.pos != pos) {
       fx_close(R, ring, a);
       R.B = pos & ~15ull; R.lo = pos; R.pos = pos; R.carry = 0; R.open = true;
     }
+#ifdef FX_OR
+    // the records' ring bytes [16, 16 + 8 ntot) back to zero for the OR rounds
+    for (u32 i = 1 + lane; i <= (ntot + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+    WAVE_SYNC();
+#endif
     STAMP(2);
     // ---- rounds ----
-#ifdef A5X_DIAG
-    if (!(a.ablate & 8u))
-#endif
+    if (!(FX_ABL & 8))
     {
       if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4);
       else fx_rounds<1>(F, ring, R, fl, T, k, rw, m2, m3, m4);
@@ -1768,7 +1891,7 @@ static ExpArgs exp_args(const A5xExpLaunch& L) {
   a.cand_off = L.cand_off; a.byte_off = L.byte_off; a.flags = L.flags; a.chunk_w0 = L.chunk_w0;
   a.segs = L.segs; a.nsegs = L.nsegs; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.SEG = L.SEG; a.out = L.out;
   a.out_base = L.out_base; a.out_cap = L.out_cap; a.mn = L.mn; a.mx = L.mx; a.err = L.err; a.dbg = L.dbg;
-  a.rec = L.rec; a.roff = L.roff; a.ablate = L.ablate; a.rec_n = L.rec_n;
+  a.rec = L.rec; a.roff = L.roff; a.rec_n = L.rec_n;
   return a;
 }
 

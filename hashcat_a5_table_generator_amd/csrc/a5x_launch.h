@@ -57,7 +57,6 @@ struct A5xExpLaunch {
   const uint64_t* rec;
   const uint32_t* roff;
   uint64_t rec_n;   // u64 in rec
-  uint32_t ablate;  // timing experiments only (A5X_ABLATE); garbage output when set
 };
 
 hipError_t a5x_set_kernel_attrs();

@@ -3,7 +3,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-export A5X_LIB_PATH=$R/hashcat_a5_table_generator_amd/_build_abl/liba5x.so A5X_WAVES=1
+export A5X_LIB_PATH=$R/hashcat_a5_table_generator_amd/_build_abl/liba5x.so
 for ab in 0 8; do
  i=0
  while read -r grp; do
