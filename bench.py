@@ -8,9 +8,12 @@ One "step" = one full pass of the hot path over one batch already resident in HB
 keyspace (k_keyspace_*) -> prefix scans -> chunk plan -> expansion (k_expand_fast [+ k_expand_slow, k_expand_b])
 into an HBM output buffer, i.e. a5x_expand_device() of include/a5x.h.  The default
 workload is BASELINE.json configs[2]: czech.table + german.table over a synthetic
-10M-word [a-z] list (len U[6,12]) per GPU.  Multi-GPU = weak scaling: every rank
-expands its own 10M-word shard (independent words, no data-path collective);
-the only collectives are the barrier and the max/sum reductions of the timing.
+[a-z] list (len U[6,12]) of 10M words per GPU.  Multi-GPU (north_star (e)): ONE
+global list of 10M x N words (synth.global_words) is split across the N ranks by
+balanced output-byte prefix -- each rank keyspaces an equal word-count block, then
+one all-gather of block totals + one all-reduce(MIN) give a5x_partition's split
+(dist.distributed_split) -- and every rank expands its shard with no data-path
+collective; the other collectives are the barrier and the max/sum timing reductions.
 
 Prints ONE JSON line (rank 0) with the driver's fields plus "roofline" (expansion
 kernel: algorithmic bytes = sum(len(cand)+1) per launch / average launch time from
@@ -48,7 +51,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3", help="c1 c2 c2a c3 c4 c5 (hashcat_a5_table_generator_amd/synth.py)")
-    ap.add_argument("--words", type=int, default=10_000_000, help="words per GPU")
+    ap.add_argument("--words", type=int, default=10_000_000,
+                    help="words per GPU: the global list has words x N words, split by output bytes")
     ap.add_argument("--min", type=int, default=0)
     ap.add_argument("--max", type=int, default=15)
     ap.add_argument("--mode", type=int, default=0, choices=(0, 1, 2, 3),
@@ -93,6 +97,39 @@ class Dist:
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
+
+
+SEED = 0x5A5
+
+
+PARALLELISM = ("partition: one global list of words_per_gpu x {world} words, split over {world} rank(s) by "
+               "balanced output-byte prefix (a5x_partition semantics: all-gather of block totals + all-reduce MIN); "
+               "no data-path collective")
+
+
+def shard_for_rank(args, D, ctx):
+    """This rank's shard of ONE global list of words_per_gpu x N words (north_star (e),
+    main.go:70-95 data parallelism): every rank keyspaces an equal word-count block,
+    and the balanced split by output bytes (a5x_partition semantics) comes from one
+    all-gather of block totals + one all-reduce(MIN) (dist.distributed_split).  Returns
+    (tables, data, offs, (w0, w1))."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer, dist as hd, synth
+    n_total = args.words * D.world
+    b0, b1 = hd.block_bounds(n_total, D.world, D.rank)
+    tables, (bd, bo) = synth.global_words(args.workload, b0, b1, seed=SEED)
+    if D.world == 1:
+        return tables, bd, bo, (0, n_total)
+    ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
+    dw, do = DeviceBuffer.from_array(ctx, bd), DeviceBuffer.from_array(ctx, bo)
+    lp = DeviceBuffer(ctx, (b1 - b0 + 1) * 8)
+    ctx.keyspace_device(dw.ptr, do.ptr, b1 - b0, args.mode, args.min, args.max, d_byte_off=lp.ptr)
+    split = hd.distributed_split(D.dist, lp.to_array(np.uint64, count=b1 - b0 + 1), b0, n_total, D.world, "nccl")
+    for b in (dw, do, lp):
+        b.free()
+    ctx.clear_table()
+    w0, w1 = int(split[D.rank]), int(split[D.rank + 1])
+    _, (data, offs) = synth.global_words(args.workload, w0, w1, seed=SEED)
+    return tables, data, offs, (w0, w1)
 
 
 def latest_profile_traffic(workload: str):
@@ -161,9 +198,9 @@ def run_digest(args, D):
     """Fused expansion + MD5/NTLM + target lookup over a resident batch (configs[4] shape)."""
     from hashcat_a5_table_generator_amd import ALGO_MD5, ALGO_NTLM, Context, DeviceBuffer, pack_words, synth
     algo = ALGO_MD5 if args.digest == "md5" else ALGO_NTLM
-    tables, (data, offs) = synth.config_words(args.workload, args.words, seed=0x5A5 + 7919 * D.rank)
-    n = len(offs) - 1
     ctx = Context(D.local)
+    tables, data, offs, (w0, w1) = shard_for_rank(args, D, ctx)
+    n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)
     do = DeviceBuffer.from_array(ctx, offs)
@@ -218,7 +255,7 @@ def run_digest(args, D):
                        "targets": args.targets, "planted": len(planted), "hits_all_ranks": hits_all,
                        "mode": MODE_NAMES[args.mode], "table_min": args.min, "table_max": args.max,
                        "scratch_bytes": scratch,
-                       "parallelism": f"weak: {D.world} x independent word shards; hit counts all-reduced"},
+                       "parallelism": PARALLELISM.format(world=D.world) + "; hit counts all-reduced"},
             "roofline": {"bound": "valu", "kernel": f"k_digest_stream<{args.digest}>",
                          "ms_digest_per_step": ms_dig, "ms_expand_per_step": ms_exp,
                          "digest_cand_per_s": tc / (ms_dig * 1e-3),
@@ -238,14 +275,14 @@ def main():
         return run_digest(args, D)
     from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
 
-    tables, (data, offs) = synth.config_words(args.workload, args.words, seed=0x5A5 + 7919 * D.rank)
-    n = len(offs) - 1
     ctx = Context(D.local)
+    tables, data, offs, (w0, w1) = shard_for_rank(args, D, ctx)
+    n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)
     do = DeviceBuffer.from_array(ctx, offs)
     tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max)
-    log(f"rank {D.rank}: {ctx.device_name}: {n} words -> {tc} candidates, {tb / 1e9:.2f} GB")
+    log(f"rank {D.rank}: {ctx.device_name}: words [{w0}, {w1}) -> {tc} candidates, {tb / 1e9:.2f} GB")
     out = DeviceBuffer(ctx, max(tb, 16))
     boff = DeviceBuffer(ctx, (n + 1) * 8)
 
@@ -309,7 +346,7 @@ def main():
                 "table_min": args.min,
                 "table_max": args.max,
                 "mode": MODE_NAMES[args.mode],
-                "parallelism": f"weak: {D.world} x independent word shards, no data-path collective",
+                "parallelism": PARALLELISM.format(world=D.world),
             },
             "roofline": {
                 "bound": "hbm",

@@ -23,6 +23,40 @@ def shard_bounds(prefix: np.ndarray, world: int, rank: int) -> Tuple[int, int]:
     return int(split[rank]), int(split[rank + 1])
 
 
+def block_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Equal word-count block [b0, b1) of ``rank``: the words whose keyspace it computes."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def distributed_split(dist, local_prefix: np.ndarray, b0: int, n: int, world: int,
+                      backend: str = "nccl") -> np.ndarray:
+    """Balanced split of ONE global word list without any rank holding its whole prefix.
+
+    Rank r has computed the exclusive byte prefix of its equal-count block [b0, b1)
+    (``local_prefix``, b1 - b0 + 1 entries, from the keyspace pass).  One all-gather of
+    the block totals gives every block's global base; every rank then searches its own
+    block for each target and one all-reduce(MIN) of the W + 1 candidates yields the
+    split.  The result equals ``a5x_partition`` (engine.partition) over the global
+    prefix: split[r] = first word whose global start offset >= total * r // W."""
+    lp = np.asarray(local_prefix, dtype=np.uint64)
+    totals = allgather_u64(dist, [int(lp[-1])], backend)[:, 0]
+    base = int(totals[:dist_rank(dist)].sum()) if world > 1 else 0
+    total = int(totals.sum())
+    cand = np.full(world + 1, n, dtype=np.uint64)
+    cand[0] = 0
+    for r in range(1, world):
+        t = total * r // world - base  # target relative to this block's base
+        if t <= int(lp[-1]):
+            # first local index with prefix >= t (index len-1 = the block's end = next block's start)
+            i = int(np.searchsorted(lp, np.uint64(max(t, 0)), side="left"))
+            cand[r] = b0 + i
+    return allreduce_min_u64(dist, cand, backend)
+
+
+def dist_rank(dist) -> int:
+    return dist.get_rank() if dist is not None and dist.is_initialized() else 0
+
+
 def shard_words(data: np.ndarray, offs: np.ndarray, w0: int, w1: int) -> Tuple[np.ndarray, np.ndarray]:
     """The packed sub-batch of words [w0, w1) (bytes re-based to 0, 16-byte pad kept)."""
     b0, b1 = int(offs[w0]), int(offs[w1])
@@ -62,3 +96,42 @@ def allreduce_u64(dist, values, backend: str = "nccl") -> np.ndarray:
         dist.all_reduce(t)
     h = t.cpu().numpy().astype(np.uint64)
     return (h[0] + (h[1] << np.uint64(32))).astype(np.uint64)
+
+
+def _world(dist) -> int:
+    return dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+
+
+def _to_halves(v: np.ndarray) -> np.ndarray:
+    return np.stack([v & np.uint64(0xFFFFFFFF), v >> np.uint64(32)]).astype(np.int64)
+
+
+def _from_halves(h: np.ndarray) -> np.ndarray:
+    h = h.astype(np.uint64)
+    return (h[..., 0, :] + (h[..., 1, :] << np.uint64(32))).astype(np.uint64)
+
+
+def allgather_u64(dist, values, backend: str = "nccl") -> np.ndarray:
+    """(world, k) array of every rank's k u64 values (exact: 32-bit halves)."""
+    import torch
+    v = np.asarray(values, dtype=np.uint64)
+    dev = "cuda" if backend == "nccl" else "cpu"
+    t = torch.from_numpy(_to_halves(v)).to(dev)
+    world = _world(dist)
+    if world == 1:
+        return v.reshape(1, -1)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    return np.stack([_from_halves(o.cpu().numpy()) for o in outs])
+
+
+def allreduce_min_u64(dist, values, backend: str = "nccl") -> np.ndarray:
+    """Element-wise MIN of u64 vectors across ranks (values < 2^63)."""
+    import torch
+    v = np.asarray(values, dtype=np.uint64)
+    if _world(dist) == 1:
+        return v.copy()
+    dev = "cuda" if backend == "nccl" else "cpu"
+    t = torch.from_numpy(v.astype(np.int64)).to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return t.cpu().numpy().astype(np.uint64)

@@ -72,3 +72,27 @@ CONFIGS = {
 def config_words(name: str, n: int, seed: int = 0x5A5):
     tables, gen, kw, _ = CONFIGS[name]
     return tables, gen(n, seed=seed, **kw)
+
+
+GLOBAL_BLOCK = 1 << 20  # words per independently seeded block of a global list
+
+
+def global_words(name: str, w0: int, w1: int, seed: int = 0x5A5):
+    """Words [w0, w1) of ONE unbounded deterministic list for config ``name``.
+
+    The list is made of GLOBAL_BLOCK-word blocks, block b generated with seed
+    (seed, b), so any rank can build any slice of the global list without the
+    rest (bench.py's north_star partition: one list, split by byte prefix)."""
+    tables, gen, kw, _ = CONFIGS[name]
+    parts, lens = [], []
+    b = w0 // GLOBAL_BLOCK
+    while b * GLOBAL_BLOCK < w1:
+        data, offs = gen(GLOBAL_BLOCK, seed=int(np.random.SeedSequence([seed, b]).generate_state(1)[0]), **kw)
+        lo = max(w0, b * GLOBAL_BLOCK) - b * GLOBAL_BLOCK
+        hi = min(w1, (b + 1) * GLOBAL_BLOCK) - b * GLOBAL_BLOCK
+        parts.append(data[int(offs[lo]):int(offs[hi])])
+        lens.append(np.diff(offs[lo:hi + 1].astype(np.int64)))
+        b += 1
+    lengths = np.concatenate(lens) if lens else np.zeros(0, dtype=np.int64)
+    body = np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8)
+    return tables, _pack(lengths, body)

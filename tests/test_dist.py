@@ -9,6 +9,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 from conftest import ROOT
 
@@ -64,6 +65,71 @@ def test_gloo_two_ranks_shard_and_reduce(tmp_path):
     assert res[0]["shard"][0] == 0 and res[0]["shard"][1] == res[1]["shard"][0] and res[1]["shard"][1] == 3000
     b0, b1 = res[0]["bytes"], res[1]["bytes"]
     assert abs(b0 - b1) / (b0 + b1) < 0.05
+
+
+SPLIT_WORKER = r"""
+import os, sys, json
+sys.path.insert(0, {root!r})
+import numpy as np
+from hashcat_a5_table_generator_amd import dist as D, synth, partition
+from oracle import c_oracle as co
+dist, rank, world, _ = D.init_from_env("gloo")
+n = {n}
+tables, (data, offs) = synth.global_words("c3", 0, n, seed=23)
+# this rank's equal-count block: its keyspace prefix (bytes per word; the C oracle stands
+# in for the keyspace kernel on CPU) -> distributed split
+b0, b1 = D.block_bounds(n, world, rank)
+t = co.CTable([os.path.join({root!r}, "tests", "golden", "tables", x + ".table") for x in tables])
+sd, so = D.shard_words(data, offs, b0, b1)
+lp = np.zeros(b1 - b0 + 1, dtype=np.uint64); lp[1:] = np.cumsum(t.digest_batch(sd, so, 0, 0, 15, nthreads=1)[:, 1])
+split = D.distributed_split(dist, lp, b0, n, world, "gloo")
+# rank 0 checks against a5x_partition over the whole prefix
+ok = True
+if rank == 0:
+    full = np.zeros(n + 1, dtype=np.uint64); full[1:] = np.cumsum(t.digest_batch(data, offs, 0, 0, 15, nthreads=1)[:, 1])
+    ok = bool(np.array_equal(split, partition(full, world)))
+print(json.dumps(dict(rank=rank, split=[int(x) for x in split], ok=ok)), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def _run_ranks(tmp_path, src, world):
+    script = tmp_path / f"w{world}.py"
+    script.write_text(src)
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), A5X_DIST_BACKEND="gloo")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e[-2000:]
+        outs.append(o.strip().splitlines()[-1])
+    import json
+    return sorted((json.loads(x) for x in outs), key=lambda d: d["rank"])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_split_equals_global_partition(tmp_path, world):
+    """north_star (e): each rank keyspaces only its equal-count block; an all-gather of
+    block totals + all-reduce(MIN) gives exactly a5x_partition over the global prefix."""
+    res = _run_ranks(tmp_path, SPLIT_WORKER.format(root=ROOT, n=4000), world)
+    assert all(r["ok"] for r in res), res
+    assert all(r["split"] == res[0]["split"] for r in res), res
+    s = res[0]["split"]
+    assert s[0] == 0 and s[-1] == 4000 and s == sorted(s)
+
+
+def test_global_words_slices_are_consistent(monkeypatch):
+    from hashcat_a5_table_generator_amd import synth
+    monkeypatch.setattr(synth, "GLOBAL_BLOCK", 1000)  # slices that cross block seeds
+    _, (d, o) = synth.global_words("c4", 0, 2500, seed=5)
+    _, (d2, o2) = synth.global_words("c4", 700, 1900, seed=5)
+    assert bytes(d[int(o[700]):int(o[1900])]) == bytes(d2[:int(o2[-1])])
+    assert np.array_equal(np.diff(o[700:1901].astype(np.int64)), np.diff(o2.astype(np.int64)))
 
 
 def test_partition_properties():

@@ -1,0 +1,110 @@
+"""BASELINE.json config shapes on the HIP path (C4 shard, C5 lookup), checked against
+the C oracle (oracle/a5_oracle.c, the restatement of main.go:168-205 / :308-440) by
+per-word order-independent digests {count, bytes, sum h, sum h^2}.
+
+C4 = configs[3]: qwerty-cyrillic x length-10 [a-z] words, 1023 candidates per word,
+one global list split across GPUs by output bytes (bench.py shard_for_rank).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import table_path
+
+pytestmark = pytest.mark.gpu
+
+NTH = min(16, os.cpu_count() or 1)  # the GPU box's CPU share
+
+
+def _gpu_digest(ctx, data, offs, mode=0, mn=0, mx=15):
+    """Expand the batch into one HBM buffer and digest every word on the device."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer
+    n = len(offs) - 1
+    dw = DeviceBuffer.from_array(ctx, data)
+    do = DeviceBuffer.from_array(ctx, offs)
+    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, mode, mn, mx)
+    out = DeviceBuffer(ctx, max(tb, 16))
+    boff = DeviceBuffer(ctx, (n + 1) * 8)
+    st = ctx.expand_device(dw.ptr, do.ptr, n, out.ptr, tb, mode, mn, mx, d_byte_off=boff.ptr)
+    assert st["candidates"] == tc and st["bytes"] == tb
+    dig = DeviceBuffer(ctx, n * 32)
+    ctx.digest_device(out.ptr, boff.ptr, 0, n, dig.ptr)
+    got = dig.to_array(np.uint64).reshape(n, 4)
+    for b in (out, boff, dig, dw, do):
+        b.free()
+    return tc, tb, got
+
+
+def _check(got, want, data, offs):
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert len(bad) == 0, [(bytes(data[int(offs[i]):int(offs[i + 1])]), got[i], want[i]) for i in bad[:5]]
+
+
+@pytest.fixture(scope="module")
+def c4_ctx():
+    from hashcat_a5_table_generator_amd import Context
+    c = Context(0)
+    c.load_tables([table_path("qwerty-cyrillic")])
+    yield c
+    c.close()
+
+
+def test_c4_shape_one_million_words(c4_ctx):
+    """1M length-10 words x qwerty-cyrillic (1.02e9 candidates, ~16 GB) == C oracle."""
+    from hashcat_a5_table_generator_amd import synth
+    from oracle import c_oracle as co
+    _, (data, offs) = synth.global_words("c4", 0, 1_000_000, seed=0xC4)
+    tc, tb, got = _gpu_digest(c4_ctx, data, offs)
+    assert tc == 1023 * 1_000_000  # every [a-z] letter has exactly one cyrillic value
+    want = co.CTable([table_path("qwerty-cyrillic")]).digest_batch(data, offs, 0, 0, 15, nthreads=NTH)
+    _check(got, want, data, offs)
+
+
+def test_c4_shard_past_u32_limits(c4_ctx):
+    """A C4 shard past 2^32 candidates and 64 GiB of output in ONE call (the per-GPU
+    shard of the 100M-word run is 1.28e10 candidates): counts, offsets and chunk
+    indices must not wrap.  Words [w0, w1) of the global list, as bench.py's partition
+    hands them to a rank."""
+    from hashcat_a5_table_generator_amd import synth
+    from oracle import c_oracle as co
+    w0, w1 = 3_000_000, 7_300_000
+    _, (data, offs) = synth.global_words("c4", w0, w1, seed=0xC4)
+    n = w1 - w0
+    tc, tb, got = _gpu_digest(c4_ctx, data, offs)
+    assert tc == 1023 * n and tc > (1 << 32) and tb > (64 << 30)
+    want = co.CTable([table_path("qwerty-cyrillic")]).digest_batch(data, offs, 0, 0, 15, nthreads=NTH)
+    _check(got, want, data, offs)
+
+
+def test_c4_partition_shards_cover_the_list(c4_ctx):
+    """The north_star split on one device: the keyspace prefix of the whole list, split
+    for 8 ranks (a5x_partition); the 8 shards expanded separately give the same per-word
+    digests as the whole list, and the shards' output bytes are balanced."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer, partition, synth
+    _, (data, offs) = synth.global_words("c3", 0, 400_000, seed=0xC3)
+    c4_ctx.clear_table()
+    c4_ctx.load_tables([table_path("czech"), table_path("german")])
+    try:
+        n = len(offs) - 1
+        dw, do = DeviceBuffer.from_array(c4_ctx, data), DeviceBuffer.from_array(c4_ctx, offs)
+        pre = DeviceBuffer(c4_ctx, (n + 1) * 8)
+        tc, tb = c4_ctx.keyspace_device(dw.ptr, do.ptr, n, d_byte_off=pre.ptr)
+        prefix = pre.to_array(np.uint64, count=n + 1)
+        assert int(prefix[-1]) == tb
+        split = partition(prefix, 8)
+        _, _, whole = _gpu_digest(c4_ctx, data, offs)
+        parts, sizes = [], []
+        for r in range(8):
+            a, b = int(split[r]), int(split[r + 1])
+            sd = np.zeros(int(offs[b] - offs[a]) + 16, dtype=np.uint8)
+            sd[: int(offs[b] - offs[a])] = data[int(offs[a]):int(offs[b])]
+            so = (offs[a:b + 1] - offs[a]).astype(np.uint64)
+            _, sb, g = _gpu_digest(c4_ctx, sd, so)
+            parts.append(g)
+            sizes.append(sb)
+        assert np.array_equal(np.concatenate(parts), whole)
+        assert sum(sizes) == tb and max(sizes) - min(sizes) < 0.01 * tb
+    finally:
+        c4_ctx.clear_table()
+        c4_ctx.load_tables([table_path("qwerty-cyrillic")])
