@@ -132,17 +132,57 @@ def shard_for_rank(args, D, ctx):
     return tables, data, offs, (w0, w1)
 
 
-def latest_profile_traffic(workload: str):
-    """HBM bytes per expansion launch from the committed rocprofv3 --pmc pass (or None)."""
+KERNEL_SRCS = ("a5x_kernels.hip", "a5x_fx6.h", "a5x_plan.h", "a5x_launch.h")
+
+
+def kernel_src_sha() -> str:
+    """sha256 of the expansion kernel sources: a PMC traffic profile counts only for them."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SRCS:
+        with open(os.path.join(ROOT, "hashcat_a5_table_generator_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def digest_src_sha() -> str:
+    """sha256 of the fused-digest kernel sources (profiles/pmc_digest_*.json are keyed on it)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("a5x_digest.hip", "a5x_launch.h"):
+        with open(os.path.join(ROOT, "hashcat_a5_table_generator_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def digest_profile(algo: str, words: int):
+    """VALU evidence of k_digest_stream for THESE sources (tools/gpu_digest_prof.sh), else None."""
+    sha = digest_src_sha()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_digest_*.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except Exception:
+            continue
+        if d.get("algo") == algo and d.get("words") == words and d.get("kernel_src_sha") == sha:
+            return d
+    return None
+
+
+def latest_profile_traffic(workload: str, words: int):
+    """HBM bytes per expansion launch from a committed rocprofv3 --pmc pass
+    (tools/gpu_pmc_traffic.sh) of THESE kernel sources on this workload and size, else None."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    sha = kernel_src_sha()
     for f in reversed(files):
         try:
             with open(f) as fh:
                 d = json.load(fh)
-            if d.get("workload") == workload and d.get("bytes_per_launch"):
-                return d
         except Exception:
             continue
+        if (d.get("workload") == workload and d.get("words") == words and d.get("kernel_src_sha") == sha
+                and d.get("bytes_per_launch")):
+            return d
     return None
 
 
@@ -192,6 +232,24 @@ def digest_cpu_baseline(tables, args):
             "sample": f"{nwords} words of workload {args.workload} (seed 0xC0FFEE): {n} candidates; C restatement "
                       f"of main.go expansion + {'hashlib MD5' if args.digest == 'md5' else 'RFC 1320 MD4 in Python (NTLM)'}"
                       f" per candidate, 1 thread"}
+
+
+def digest_roofline(args, tc, ms_dig, ms_exp):
+    """Digest stage: VALU-bound.  achieved = integer lane-ops/s of k_digest_stream (int ops
+    per candidate from the committed PMC profile of these sources x candidates / digest
+    time); peak = 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz 32-bit VALU ops (a wave64
+    VALU instruction issues over 2 cycles: MI355X_MICROARCH.md; = the 157.3 TF f32 FMA peak / 2)."""
+    prof = digest_profile(args.digest, args.words)
+    peak = 256 * 4 * 32 * 2.4e9 / 1e12  # Tops/s
+    r = {"bound": "valu", "kernel": f"k_digest_stream<{args.digest}>", "unit": "Tops/s (int32 lane ops)",
+         "peak": peak, "ms_digest_per_step": ms_dig, "ms_expand_per_step": ms_exp,
+         "digest_cand_per_s": tc / (ms_dig * 1e-3), "achieved": None, "frac": None, "profile": None}
+    if prof:
+        ach = prof["int_ops_per_cand"] * tc / (ms_dig * 1e-3) / 1e12
+        r.update(achieved=ach, frac=ach / peak, int_ops_per_cand=prof["int_ops_per_cand"],
+                 valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"),
+                 profile=f"profiles/pmc_digest_{args.digest}_c5.json (kernel_src_sha {prof['kernel_src_sha'][:12]})")
+    return r
 
 
 def run_digest(args, D):
@@ -256,10 +314,7 @@ def run_digest(args, D):
                        "mode": MODE_NAMES[args.mode], "table_min": args.min, "table_max": args.max,
                        "scratch_bytes": scratch,
                        "parallelism": PARALLELISM.format(world=D.world) + "; hit counts all-reduced"},
-            "roofline": {"bound": "valu", "kernel": f"k_digest_stream<{args.digest}>",
-                         "ms_digest_per_step": ms_dig, "ms_expand_per_step": ms_exp,
-                         "digest_cand_per_s": tc / (ms_dig * 1e-3),
-                         "note": "VALU-bound; instruction counts per candidate: profiles/pmc_*digest*.json"},
+            "roofline": digest_roofline(args, tc, ms_dig, ms_exp),
             "cpu_baseline": None if args.no_cpu_baseline else digest_cpu_baseline(tables, args),
         }
         print(json.dumps(res_line), flush=True)
@@ -319,7 +374,7 @@ def main():
 
     if D.rank == 0:
         achieved = tb / (ms_exp * 1e-3) / 1e9  # GB/s, algorithmic bytes per launch / launch time
-        prof = latest_profile_traffic(args.workload) if args.mode == 0 else None
+        prof = latest_profile_traffic(args.workload, n) if args.mode == 0 and D.world == 1 else None
         traffic = None
         if prof:
             traffic = prof["bytes_per_launch"]

@@ -108,3 +108,47 @@ def test_c4_partition_shards_cover_the_list(c4_ctx):
     finally:
         c4_ctx.clear_table()
         c4_ctx.load_tables([table_path("qwerty-cyrillic")])
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_c5_shape_lookup_one_million_targets(algo):
+    """C5 = configs[4]: greek-hebrew x Greek words, fused expansion + MD5 (0) / NTLM (1)
+    + lookup against 1M targets (1000 planted candidates + random digests).  Every
+    planted (word, candidate) is found; every hit is a real candidate whose digest is a
+    target; no random target hits."""
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
+    from oracle import digest_oracle as dg
+    f = dg.ALGOS[algo]
+    _, (data, offs) = synth.global_words("c5", 0, 200_000, seed=0xC5 + algo)
+    n = len(offs) - 1
+    rng = np.random.default_rng(0xC5 + algo)
+    with Context(0) as ctx:
+        ctx.load_tables([table_path("greek-hebrew")])
+        wsample = sorted(set(int(x) for x in rng.choice(n, size=1200, replace=False)))
+        words = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in wsample]
+        cands = ctx.expand_words(words, 0, 0, 15)
+        planted, plains = {}, set()
+        for w, cs in zip(wsample, cands):
+            if cs and len(planted) < 1000:
+                c = int(rng.integers(0, len(cs)))
+                planted[(w, c)] = f(cs[c])
+                plains.add(cs[c])
+        rand = rng.integers(0, 256, size=(1_000_000 - len(planted), 16), dtype=np.uint8)
+        targets = np.concatenate([np.frombuffer(b"".join(planted.values()), dtype=np.uint8).reshape(-1, 16), rand])
+        ctx.set_targets(algo, targets)
+        dw, do = DeviceBuffer.from_array(ctx, data), DeviceBuffer.from_array(ctx, offs)
+        tc, _ = ctx.keyspace_device(dw.ptr, do.ptr, n)
+        hits, st = ctx.expand_digest_device(dw.ptr, do.ptr, n, 0, 0, 15, scratch_bytes=1 << 30, hit_cap=1 << 16)
+        assert st["candidates"] == tc and tc > 200_000_000
+        got = {(w, c): d for w, c, d in hits}
+        assert len(got) == len(hits)  # no duplicate reports
+        missing = [k for k in planted if k not in got]
+        assert not missing, missing[:5]
+        tset = set(planted.values())
+        hw = sorted({w for w, _ in got})
+        hc = dict(zip(hw, ctx.expand_words([bytes(data[int(offs[w]):int(offs[w + 1])]) for w in hw], 0, 0, 15)))
+        for (w, c), d in got.items():
+            assert f(hc[w][c]) == d and d in tset, (w, c, d.hex())
+        # zero false hits: a hit beyond the planted pairs is another occurrence of a planted
+        # plain (the same candidate text from another word or position), never a random target
+        assert all(hc[w][c] in plains for w, c in set(got) - set(planted))

@@ -13,7 +13,9 @@ for grp in WRITE_SIZE FETCH_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "k_expand_fast" -d $R/gpurun_out/pmct_${T}_$grp -o run --output-format csv -- python3 $R/bench.py $ARGS > $R/gpurun_out/pmct_${T}_$grp.log 2>&1 || { echo "pmc $grp failed"; tail -5 $R/gpurun_out/pmct_${T}_$grp.log; exit 21; }
 done
 cd $R && python3 - <<PY
-import csv, glob, json
+import csv, glob, json, sys
+sys.path.insert(0, ".")
+from bench import kernel_src_sha
 vals = {}
 for grp in ("WRITE_SIZE", "FETCH_SIZE"):
     rows = list(csv.DictReader(open(glob.glob("gpurun_out/pmct_${T}_%s/run_counter_collection.csv" % grp)[0])))
@@ -21,7 +23,7 @@ for grp in ("WRITE_SIZE", "FETCH_SIZE"):
     vals[grp] = sum(v) / len(v)   # per dispatch (KiB)
 write_b = vals["WRITE_SIZE"] * 1024
 fetch_b = vals["FETCH_SIZE"] * 1024 * 2
-out = {"workload": "${WL}", "words": ${W}, "kernel": "k_expand_fast",
+out = {"workload": "${WL}", "words": ${W}, "kernel": "k_expand_fast", "kernel_src_sha": kernel_src_sha(),
        "write_size_kib": vals["WRITE_SIZE"], "fetch_size_kib": vals["FETCH_SIZE"],
        "bytes_per_launch": write_b + fetch_b, "write_bytes": write_b, "fetch_bytes_corrected": fetch_b,
        "note": "rocprofv3 --pmc WRITE_SIZE / FETCH_SIZE in separate passes; KiB; FETCH_SIZE x2 (gfx950)"}
