@@ -7,13 +7,13 @@ of ``include/a5x.h`` (``_build/liba5x.so``).
 """
 from ._lib import A5xError, LIB_PATH
 from .engine import (ALGO_MD5, ALGO_NTLM, DeviceBuffer, MODE_DEFAULT, MODE_REVERSE, MODE_SUBALL, MODE_SUBALL_REVERSE, Context, decode_hex_notation,
-                     generate, mode_of, pack_words, partition, process_word, process_word_reverse,
+                     format_plain, generate, mode_of, pack_words, partition, process_word, process_word_reverse,
                      process_word_substitute_all, process_word_substitute_all_reverse, read_substitution_table,
                      split_words)
 
 __all__ = [
     "A5xError", "LIB_PATH", "ALGO_MD5", "ALGO_NTLM", "Context", "DeviceBuffer", "MODE_DEFAULT", "MODE_REVERSE", "MODE_SUBALL", "MODE_SUBALL_REVERSE",
-    "decode_hex_notation", "generate", "mode_of", "pack_words", "partition", "process_word",
+    "decode_hex_notation", "format_plain", "generate", "mode_of", "pack_words", "partition", "process_word",
     "process_word_reverse", "process_word_substitute_all", "process_word_substitute_all_reverse",
     "read_substitution_table", "split_words",
 ]

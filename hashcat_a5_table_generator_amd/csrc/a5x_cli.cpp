@@ -6,11 +6,20 @@
 //
 //   a5x_generator <dict-file> -t <table> [-t <table> ...] [-m N] [-x N]
 //                 [--threads N] [-s] [-r] [--device N]
+//                 [--hashes <file> [--algo md5|ntlm]]
+//
+// --hashes (a5x extension): instead of printing the candidates for a
+// hashcat pipe (README.MD:69), hash them on the GPU (fused MD5 / NTLM + lookup) against
+// the hex digests of <file> and print what hashcat would report, "hash:plain" (plains
+// that hashcat would hexify as $HEX[...]), each target once, at its first candidate in
+// stream order (README.MD:74-106, :168).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "a5x.h"
@@ -28,12 +37,44 @@ static void usage(FILE* f) {
           "      --threads=-1                  Number of threads (accepted; the GPU needs none)\n"
           "  -s, --substitute-all              Substitution Cipher, see Transliteration Attack\n"
           "  -r, --reverse-sub                 Reverse substitution direction\n"
-          "      --device=0                    GPU ordinal (a5x extension)\n");
+          "      --device=0                    GPU ordinal (a5x extension)\n"
+          "      --hashes=FILE                 Crack: print hash:plain for the digests in FILE (a5x extension)\n"
+          "      --algo=md5                    Digest of --hashes: md5 (hashcat -m 0) or ntlm (-m 1000)\n");
 }
 
 static int sink_stdout(void* user, const uint8_t* data, size_t len) {
   (void)user;
   return fwrite(data, 1, len, stdout) == len ? 0 : 1;
+}
+
+static int hexv(int c) {
+  return c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+}
+
+// target digests: one hex digest per line (32 hex digits; anything after them, e.g. a
+// ":plain" of a potfile line, is ignored); other lines are counted and skipped
+static int load_targets(a5x_ctx* ctx, const char* path, int algo) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return A5X_E_IO;
+  std::vector<uint8_t> dig;
+  char line[4096];
+  uint64_t bad = 0;
+  while (fgets(line, sizeof line, f)) {
+    size_t k = 0;
+    uint8_t d[16];
+    for (; k < 32; k++) {
+      const int v = hexv((unsigned char)line[k]);
+      if (v < 0) break;
+      if (k & 1) d[k / 2] |= (uint8_t)v; else d[k / 2] = (uint8_t)(v << 4);
+    }
+    const char t = line[32];
+    if (k == 32 && (t == 0 || t == '\n' || t == '\r' || t == ':')) dig.insert(dig.end(), d, d + 16);
+    else if (line[0] != '\n' && line[0] != '\r') bad++;
+  }
+  fclose(f);
+  if (bad) fprintf(stderr, "a5_generator: %llu line(s) of %s are not 32-hex-digit hashes (skipped)\n",
+                   (unsigned long long)bad, path);
+  return a5x_set_targets(ctx, algo, dig.empty() ? nullptr : dig.data(), dig.size() / 16);
 }
 
 static bool parse_int(const char* s, int* out) {
@@ -47,7 +88,8 @@ static bool parse_int(const char* s, int* out) {
 int main(int argc, char** argv) {
   std::vector<std::string> tables;
   std::string dict;
-  int tmin = 0, tmax = 15, threads = -1, device = 0;
+  int tmin = 0, tmax = 15, threads = -1, device = 0, algo = A5X_ALGO_MD5;
+  std::string hashes;
   bool suball = false, rev = false;
   auto need = [&](int& i, const char* flag) -> const char* {
     if (i + 1 >= argc) {
@@ -90,6 +132,13 @@ int main(int argc, char** argv) {
     } else if (s.rfind("--device", 0) == 0) {
       if (!parse_int(val_of("--device"), &v)) { fprintf(stderr, "a5_generator: error: --device: bad int\n"); return 80; }
       device = v;
+    } else if (s.rfind("--hashes", 0) == 0) {
+      hashes = val_of("--hashes");
+    } else if (s.rfind("--algo", 0) == 0) {
+      std::string v = val_of("--algo");
+      if (v == "md5" || v == "0") algo = A5X_ALGO_MD5;
+      else if (v == "ntlm" || v == "1000") algo = A5X_ALGO_NTLM;
+      else { fprintf(stderr, "a5_generator: error: --algo: md5 or ntlm\n"); return 80; }
     } else if (s == "--substitute-all") suball = true;
     else if (s == "--reverse-sub") rev = true;
     else if (s.size() > 1 && s[0] == '-' && s[1] != '-') {
@@ -131,14 +180,40 @@ int main(int argc, char** argv) {
   static char obuf[1 << 22];
   setvbuf(stdout, obuf, _IOFBF, sizeof obuf);
   const int mode = (suball ? A5X_MODE_SUBALL : A5X_MODE_DEFAULT) + (rev ? 1 : 0);
+  if (!hashes.empty() && (rc = load_targets(ctx, hashes.c_str(), algo))) {
+    fprintf(stderr, "a5_generator: %s\n", rc == A5X_E_IO ? "cannot read --hashes file" : a5x_last_error(ctx));
+    a5x_destroy(ctx);
+    return 1;
+  }
   const uint64_t B = 1u << 22;
   std::vector<uint64_t> sub;
+  std::vector<a5x_hit> hits(1 << 16);
+  std::unordered_set<std::string> cracked;  // each target reported once (hashcat potfile)
   for (uint64_t b0 = 0; b0 < n && rc == 0; b0 += B) {
     const uint64_t b1 = b0 + B < n ? b0 + B : n;
     sub.resize(b1 - b0 + 1);
     for (uint64_t i = b0; i <= b1; i++) sub[i - b0] = off[i] - off[b0];
-    rc = a5x_expand(ctx, words.data() + off[b0], sub.data(), b1 - b0, mode, tmin, tmax, sink_stdout, nullptr,
-                    nullptr);
+    const uint8_t* wb = words.data() + off[b0];
+    if (hashes.empty()) {
+      rc = a5x_expand(ctx, wb, sub.data(), b1 - b0, mode, tmin, tmax, sink_stdout, nullptr, nullptr);
+      continue;
+    }
+    uint64_t nh = 0;
+    rc = a5x_expand_digest(ctx, wb, sub.data(), b1 - b0, mode, tmin, tmax, hits.data(), hits.size(), &nh, nullptr);
+    if (rc == A5X_E_CAPACITY && nh > hits.size()) {
+      hits.resize(nh);
+      rc = a5x_expand_digest(ctx, wb, sub.data(), b1 - b0, mode, tmin, tmax, hits.data(), hits.size(), &nh, nullptr);
+    }
+    if (rc) break;
+    // stream order, then the first candidate of each digest
+    std::sort(hits.begin(), hits.begin() + nh, [](const a5x_hit& x, const a5x_hit& y) {
+      return x.word != y.word ? x.word < y.word : x.cand < y.cand;
+    });
+    std::vector<a5x_hit> first;
+    for (uint64_t h = 0; h < nh; h++)
+      if (cracked.insert(std::string((const char*)hits[h].digest, 16)).second) first.push_back(hits[h]);
+    rc = a5x_format_hits(ctx, wb, sub.data(), b1 - b0, mode, tmin, tmax, first.data(), first.size(), sink_stdout,
+                         nullptr);
   }
   fflush(stdout);
   if (rc) fprintf(stderr, "a5_generator: %s\n", a5x_last_error(ctx));

@@ -1571,6 +1571,107 @@ int a5x_partition(const uint64_t* prefix, uint64_t n, uint32_t parts, uint64_t* 
   return A5X_OK;
 }
 
+// ---- hashcat-style hit output (README.MD:74-106, :168) ------------
+// hashcat's outfile auto-hex convention, restated (hashcat is not part of the
+// reference): a plain is written as $HEX[lowercase hex] when it is not valid UTF-8
+// (Go utf8.Valid rules), contains a control byte (< 0x20 or 0x7f, which would break
+// the "hash:plain" line), or itself has the $HEX[...] form.
+static bool plain_needs_hex(const uint8_t* p, size_t n) {
+  if (n >= 6 && memcmp(p, "$HEX[", 5) == 0 && p[n - 1] == ']') return true;
+  for (size_t i = 0; i < n;) {
+    if (p[i] < 0x20 || p[i] == 0x7f) return true;
+    int sz;
+    const int r = a5x::gosem::decode_rune(p + i, n - i, &sz);
+    if (r == a5x::gosem::kRuneError && sz == 1) return true;  // invalid byte (a literal U+FFFD has sz 3)
+    i += (size_t)sz;
+  }
+  return false;
+}
+
+static void append_plain(std::string& o, const uint8_t* p, size_t n) {
+  static const char* hx = "0123456789abcdef";
+  if (!plain_needs_hex(p, n)) {
+    o.append((const char*)p, n);
+    return;
+  }
+  o += "$HEX[";
+  for (size_t i = 0; i < n; i++) {
+    o += hx[p[i] >> 4];
+    o += hx[p[i] & 15];
+  }
+  o += ']';
+}
+
+int a5x_format_plain(const uint8_t* plain, size_t len, uint8_t* out, size_t cap, size_t* out_len) {
+  if ((!plain && len) || !out_len) return A5X_E_ARG;
+  std::string o;
+  append_plain(o, plain, len);
+  *out_len = o.size();
+  if (!out || cap < o.size()) return out ? A5X_E_CAPACITY : A5X_OK;
+  memcpy(out, o.data(), o.size());
+  return A5X_OK;
+}
+
+static int collect_sink(void* user, const uint8_t* data, size_t len) {
+  ((std::string*)user)->append((const char*)data, len);
+  return 0;
+}
+
+int a5x_format_hits(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
+                    const a5x_hit* hits, uint64_t n_hits, a5x_sink_fn sink, void* user) {
+  if (!c || !sink || (n_hits && (!hits || !words || !woff))) return A5X_E_ARG;
+  if (!n_hits) return A5X_OK;
+  // the hit words, once each, as a sub-batch; their candidates regenerated on the device
+  std::vector<uint64_t> uw(n_hits);
+  for (uint64_t h = 0; h < n_hits; h++) {
+    if (hits[h].word >= nw) return fail(c, A5X_E_ARG, "hit word index beyond the batch");
+    uw[h] = hits[h].word;
+  }
+  std::sort(uw.begin(), uw.end());
+  uw.erase(std::unique(uw.begin(), uw.end()), uw.end());
+  std::vector<uint8_t> sb;
+  std::vector<uint64_t> so(1, 0);
+  for (uint64_t w : uw) {
+    sb.insert(sb.end(), words + woff[w], words + woff[w + 1]);
+    so.push_back(sb.size());
+  }
+  sb.resize(sb.size() + 16, 0);
+  std::vector<uint64_t> cnt(uw.size()), byt(uw.size());
+  int rc;
+  if ((rc = a5x_keyspace(c, sb.data(), so.data(), uw.size(), mode, mn, mx, cnt.data(), byt.data()))) return rc;
+  std::string cand;
+  if ((rc = a5x_expand(c, sb.data(), so.data(), uw.size(), mode, mn, mx, collect_sink, &cand, nullptr))) return rc;
+  std::vector<uint64_t> base(uw.size() + 1, 0);
+  for (size_t k = 0; k < uw.size(); k++) base[k + 1] = base[k] + byt[k];
+  if (base.back() != cand.size()) return fail(c, A5X_E_ARG, "hit words re-expanded to an unexpected size");
+  std::vector<std::vector<uint32_t>> starts(uw.size());  // line starts per hit word (built on demand)
+  static const char* hx = "0123456789abcdef";
+  std::string o;
+  for (uint64_t h = 0; h < n_hits; h++) {
+    const size_t k = (size_t)(std::lower_bound(uw.begin(), uw.end(), hits[h].word) - uw.begin());
+    if (hits[h].cand >= cnt[k]) return fail(c, A5X_E_ARG, "hit candidate index beyond its word's keyspace");
+    auto& st = starts[k];
+    if (st.empty()) {
+      st.push_back(0);
+      for (uint64_t i = base[k]; i < base[k + 1]; i++)
+        if (cand[i] == '\n') st.push_back((uint32_t)(i + 1 - base[k]));
+    }
+    const uint64_t a = base[k] + st[hits[h].cand], e = base[k] + st[hits[h].cand + 1] - 1;
+    for (int i = 0; i < 16; i++) {
+      o += hx[hits[h].digest[i] >> 4];
+      o += hx[hits[h].digest[i] & 15];
+    }
+    o += ':';
+    append_plain(o, (const uint8_t*)cand.data() + a, e - a);
+    o += '\n';
+    if (o.size() >= (1u << 20) || h + 1 == n_hits) {
+      if (sink(user, (const uint8_t*)o.data(), o.size())) return fail(c, A5X_E_SINK, "sink returned non-zero");
+      o.clear();
+    }
+  }
+  return A5X_OK;
+}
+
 int a5x_dev_alloc(a5x_ctx* c, void** p, size_t bytes) {
   if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
   if (!c || !p) return A5X_E_ARG;

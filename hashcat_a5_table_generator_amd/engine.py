@@ -242,6 +242,25 @@ class Context:
                                                    stream or None))
         return self._hits(arr, min(nh.value, hit_cap)), st.as_dict()
 
+    def format_hits(self, words: np.ndarray, offs: np.ndarray, hits, mode: int = MODE_DEFAULT, mn: int = 0,
+                    mx: int = 15) -> bytes:
+        """hashcat "hexdigest:plain\\n" lines for hits [(word, cand, digest)] of this batch
+        (a5x_format_hits; plains in $HEX[] form when hashcat's outfile would hexify them)."""
+        arr = (_lib.Hit * max(1, len(hits)))()
+        for k, (w, c, d) in enumerate(hits):
+            arr[k].word, arr[k].cand = int(w), int(c)
+            ctypes.memmove(arr[k].digest, bytes(d), 16)
+        chunks: List[bytes] = []
+
+        def _cb(_u, p, n):
+            chunks.append(ctypes.string_at(p, n))
+            return 0
+
+        cb = _lib.SINK(_cb)
+        self._chk(self._L.a5x_format_hits(self.h, words.ctypes.data, offs.ctypes.data, len(offs) - 1, mode, mn, mx,
+                                          arr, len(hits), cb, None))
+        return b"".join(chunks)
+
     def digest_lines_device(self, algo: int, d_lines: int, nbytes: int, d_digests: int, cap: int,
                             stream: int = 0) -> int:
         """16-byte digest of every line of a device "cand\n" stream; returns the line count."""
@@ -271,6 +290,16 @@ def _split_lines(seg: bytes, count: int) -> List[bytes]:
     assert parts[-1] == b""
     parts = parts[:-1]
     return parts
+
+
+def format_plain(plain: bytes) -> bytes:
+    """The plain as a hashcat outfile line writes it (``a5x_format_plain``)."""
+    L = _lib.load()
+    n = ctypes.c_size_t()
+    check(L.a5x_format_plain(plain, len(plain), None, 0, ctypes.byref(n)))
+    out = ctypes.create_string_buffer(max(1, n.value))
+    check(L.a5x_format_plain(plain, len(plain), out, n.value, ctypes.byref(n)))
+    return out.raw[:n.value]
 
 
 def partition(prefix: np.ndarray, parts: int) -> np.ndarray:

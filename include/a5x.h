@@ -182,6 +182,20 @@ A5X_API int a5x_expand_digest(a5x_ctx* ctx, const uint8_t* words, const uint64_t
 A5X_API int a5x_digest_lines_device(a5x_ctx* ctx, int algo, const uint8_t* d_lines, uint64_t nbytes,
                                     uint8_t* d_digests, uint64_t digests_cap, uint64_t* n_lines, void* stream);
 
+/* ---- hashcat-style hit output: "hash:plain" lines --------------- */
+/* The plain as hashcat's outfile writes it: unchanged, or $HEX[lowercase hex] when it
+ * is not valid UTF-8, contains a control byte (< 0x20, 0x7f) or has the $HEX[...] form
+ * itself (README.MD:171-176 uses the same notation for input).  *out_len = the size;
+ * out == NULL: size only; A5X_E_CAPACITY when cap is too small.  Pure host function. */
+A5X_API int a5x_format_plain(const uint8_t* plain, size_t len, uint8_t* out, size_t cap, size_t* out_len);
+/* One "hexdigest:plain\n" line per hit, in hit order, through sink (hashcat -m 0 /
+ * -m 1000 potfile form, README.MD:74-106): the plains are regenerated on the device
+ * from the hit's (word, cand) with the same batch (host buffers), mode and limits the
+ * hits were found with. */
+A5X_API int a5x_format_hits(a5x_ctx* ctx, const uint8_t* words, const uint64_t* word_off, uint64_t n_words,
+                            int mode, int min, int max, const a5x_hit* hits, uint64_t n_hits, a5x_sink_fn sink,
+                            void* user);
+
 /* ---- multi-GPU partition --------------------------------------- */
 /* Balanced split of [0, total) for `parts` ranks from an inclusive/exclusive
  * prefix (n+1 entries, e.g. per-word byte offsets): split[r] = first word of
