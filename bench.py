@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--mode", type=int, default=0, choices=(0, 1, 2, 3),
                     help="0 processWord (headline), 1 -r, 2 -s, 3 -s -r (main.go:80-92)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-words", type=int, default=50_000)
+    ap.add_argument("--cpu-sample-words", type=int, default=120_000)
     ap.add_argument("--verify", action="store_true", help="digest-check the last step against the C oracle")
     ap.add_argument("--digest", default="none", choices=("none", "md5", "ntlm"),
                     help="fused expansion + digest + lookup (SURVEY 8(a) a8, configs[4]); use with --workload c5")
@@ -132,31 +132,24 @@ def shard_for_rank(args, D, ctx):
     return tables, data, offs, (w0, w1)
 
 
-KERNEL_SRCS = ("a5x_kernels.hip", "a5x_fx6.h", "a5x_plan.h", "a5x_launch.h")
-
-
 def kernel_src_sha() -> str:
-    """sha256 of the expansion kernel sources: a PMC traffic profile counts only for them."""
+    """sha256 of every source under csrc/: a committed PMC profile counts only for the
+    exact sources it was measured on."""
     import hashlib
     h = hashlib.sha256()
-    for f in KERNEL_SRCS:
-        with open(os.path.join(ROOT, "hashcat_a5_table_generator_amd", "csrc", f), "rb") as fh:
-            h.update(fh.read())
+    d = os.path.join(ROOT, "hashcat_a5_table_generator_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".h", ".hip", ".cpp")):
+            with open(os.path.join(d, f), "rb") as fh:
+                h.update(f.encode() + b"\0" + fh.read())
     return h.hexdigest()
 
 
-def digest_src_sha() -> str:
-    """sha256 of the fused-digest kernel sources (profiles/pmc_digest_*.json are keyed on it)."""
-    import hashlib
-    h = hashlib.sha256()
-    for f in ("a5x_digest.hip", "a5x_launch.h"):
-        with open(os.path.join(ROOT, "hashcat_a5_table_generator_amd", "csrc", f), "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()
+digest_src_sha = kernel_src_sha
 
 
-def digest_profile(algo: str, words: int):
-    """VALU evidence of k_digest_stream for THESE sources (tools/gpu_digest_prof.sh), else None."""
+def digest_profile(algo: str, words: int, kernel: str):
+    """VALU evidence of the digest kernel for THESE sources (tools/gpu_digest_prof.sh), else None."""
     sha = digest_src_sha()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_digest_*.json")), reverse=True):
         try:
@@ -164,7 +157,8 @@ def digest_profile(algo: str, words: int):
                 d = json.load(fh)
         except Exception:
             continue
-        if d.get("algo") == algo and d.get("words") == words and d.get("kernel_src_sha") == sha:
+        if (d.get("algo") == algo and d.get("words") == words and d.get("kernel_src_sha") == sha
+                and d.get("kernel") == kernel):
             return d
     return None
 
@@ -186,29 +180,53 @@ def latest_profile_traffic(workload: str, words: int):
     return None
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: every core this process may use, capped at the
+    GPU box's per-GPU CPU share (16; nproc there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(tables, args):
-    """The reference algorithm restated in C (oracle/a5_oracle.c), main.go:58-98 structure."""
+    """The reference algorithm restated in C (oracle/a5_oracle.c) with main.go:58-98's
+    structure -- one worker per word from a pool, every candidate sent on a 1000-slot
+    channel, one writer with a 4 KiB buffer -- timed at 1 thread and at all host threads."""
     from oracle import c_oracle as co
     from hashcat_a5_table_generator_amd import synth
     t = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", x + ".table") for x in tables])
     fd = os.open(os.devnull, os.O_WRONLY)
-    best = None
-    for th in sorted({1, min(16, os.cpu_count() or 1)}):
-        nwords = args.cpu_sample_words if th == 1 else max(1000, args.cpu_sample_words // 5)
+    runs = []
+    nmax = cpu_threads()
+    for th in sorted({1, nmax}):
+        nwords = args.cpu_sample_words
         _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
         t0 = time.perf_counter()
         c, b = t.run_pipeline(data, offs, args.mode, args.min, args.max, th, fd)
         dt = time.perf_counter() - t0
-        r = {"value": c / dt, "unit": "candidates/s", "cores": th, "kind": "port",
-             "sample": f"{nwords} words of workload {args.workload} (seed 0xC0FFEE): {c} candidates, "
-                       f"{b} bytes to /dev/null in {dt:.2f} s; C restatement of main.go with {th} worker thread(s), "
-                       f"a 1000-slot channel and one 4 KiB writer (best of 1 and {min(16, os.cpu_count() or 1)} "
-                       f"threads)"}
+        runs.append({"threads": th, "value": c / dt, "seconds": dt, "candidates": c})
         log(f"cpu baseline threads={th}: {c / dt / 1e6:.2f} Mcand/s ({dt:.2f} s)")
-        if best is None or r["value"] > best["value"]:
-            best = r
     os.close(fd)
-    return best
+    best = max(runs, key=lambda r: r["value"])
+    return {"value": best["value"], "unit": "candidates/s", "cores": best["threads"], "kind": "port",
+            "cpu_model": cpu_model(), "runs": runs,
+            "sample": f"{args.cpu_sample_words} words of workload {args.workload} (seed 0xC0FFEE) to /dev/null; "
+                      f"C restatement of main.go (oracle/a5_oracle.c) with its goroutine pool, 1000-slot channel "
+                      f"(lock-free ring, spin-then-yield like Go's runtime) and one 4 KiB writer; best of 1 and "
+                      f"{nmax} worker thread(s) ({cpu_model()})"}
 
 
 def digest_cpu_baseline(tables, args):
@@ -235,17 +253,23 @@ def digest_cpu_baseline(tables, args):
 
 
 def digest_roofline(args, tc, ms_dig, ms_exp):
-    """Digest stage: VALU-bound.  achieved = integer lane-ops/s of k_digest_stream (int ops
-    per candidate from the committed PMC profile of these sources x candidates / digest
-    time); peak = 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz 32-bit VALU ops (a wave64
-    VALU instruction issues over 2 cycles: MI355X_MICROARCH.md; = the 157.3 TF f32 FMA peak / 2)."""
-    prof = digest_profile(args.digest, args.words)
+    """Digest stage: VALU-bound.  achieved = integer lane-ops/s of the digest kernel (int
+    ops per candidate from the committed PMC profile of these sources x candidates /
+    stage time); peak = 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz 32-bit VALU ops (a
+    wave64 VALU instruction issues over 2 cycles: MI355X_MICROARCH.md; = the 157.3 TF f32
+    FMA peak / 2).  Fused path (MD5, all-FAST batch): k_expand_fast_md5 expands, hashes
+    and probes in one kernel, so the stage time is the expansion time."""
+    fused = ms_dig < 1e-3
+    kernel = "k_expand_fast_md5" if fused else "k_digest_stream"
+    ms_stage = ms_exp if fused else ms_dig
+    prof = digest_profile(args.digest, args.words, kernel)
     peak = 256 * 4 * 32 * 2.4e9 / 1e12  # Tops/s
-    r = {"bound": "valu", "kernel": f"k_digest_stream<{args.digest}>", "unit": "Tops/s (int32 lane ops)",
-         "peak": peak, "ms_digest_per_step": ms_dig, "ms_expand_per_step": ms_exp,
-         "digest_cand_per_s": tc / (ms_dig * 1e-3), "achieved": None, "frac": None, "profile": None}
+    r = {"bound": "valu", "kernel": kernel + ("" if fused else f"<{args.digest}>"), "fused": fused,
+         "unit": "Tops/s (int32 lane ops)", "peak": peak, "ms_digest_per_step": ms_stage if not fused else 0.0,
+         "ms_expand_per_step": ms_exp, "digest_cand_per_s": tc / (ms_stage * 1e-3), "achieved": None, "frac": None,
+         "profile": None}
     if prof:
-        ach = prof["int_ops_per_cand"] * tc / (ms_dig * 1e-3) / 1e12
+        ach = prof["int_ops_per_cand"] * tc / (ms_stage * 1e-3) / 1e12
         r.update(achieved=ach, frac=ach / peak, int_ops_per_cand=prof["int_ops_per_cand"],
                  valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"),
                  profile=f"profiles/pmc_digest_{args.digest}_c5.json (kernel_src_sha {prof['kernel_src_sha'][:12]})")

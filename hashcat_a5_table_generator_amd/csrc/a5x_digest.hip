@@ -22,6 +22,7 @@
 
 #include "a5x.h"
 #include "a5x_launch.h"
+#include "a5x_md.h"
 
 namespace {
 
@@ -47,86 +48,6 @@ __device__ __forceinline__ u32 d_incl_scan(u32 x) {
     if ((int)lane >= d) x += y;
   }
   return x;
-}
-
-__device__ __forceinline__ u32 rotl(u32 x, u32 s) { return __builtin_amdgcn_alignbit(x, x, 32u - s); }
-
-// ---------------------------------------------------------------------------
-// MD5 (RFC 1321) and MD4 (RFC 1320) compression functions
-// ---------------------------------------------------------------------------
-#define MD5_STEP(f, a, b, c, d, x, t, s) \
-  a += f(b, c, d) + (x) + (t);           \
-  a = rotl(a, s) + b;
-#define MD5_F(x, y, z) (((x) & (y)) | (~(x) & (z)))
-#define MD5_G(x, y, z) (((x) & (z)) | ((y) & ~(z)))
-#define MD5_H(x, y, z) ((x) ^ (y) ^ (z))
-#define MD5_I(x, y, z) ((y) ^ ((x) | ~(z)))
-
-__device__ __forceinline__ void md5_block(u32* st, const u32* M) {
-  u32 a = st[0], b = st[1], c = st[2], d = st[3];
-  MD5_STEP(MD5_F, a, b, c, d, M[0], 0xd76aa478u, 7) MD5_STEP(MD5_F, d, a, b, c, M[1], 0xe8c7b756u, 12)
-  MD5_STEP(MD5_F, c, d, a, b, M[2], 0x242070dbu, 17) MD5_STEP(MD5_F, b, c, d, a, M[3], 0xc1bdceeeu, 22)
-  MD5_STEP(MD5_F, a, b, c, d, M[4], 0xf57c0fafu, 7) MD5_STEP(MD5_F, d, a, b, c, M[5], 0x4787c62au, 12)
-  MD5_STEP(MD5_F, c, d, a, b, M[6], 0xa8304613u, 17) MD5_STEP(MD5_F, b, c, d, a, M[7], 0xfd469501u, 22)
-  MD5_STEP(MD5_F, a, b, c, d, M[8], 0x698098d8u, 7) MD5_STEP(MD5_F, d, a, b, c, M[9], 0x8b44f7afu, 12)
-  MD5_STEP(MD5_F, c, d, a, b, M[10], 0xffff5bb1u, 17) MD5_STEP(MD5_F, b, c, d, a, M[11], 0x895cd7beu, 22)
-  MD5_STEP(MD5_F, a, b, c, d, M[12], 0x6b901122u, 7) MD5_STEP(MD5_F, d, a, b, c, M[13], 0xfd987193u, 12)
-  MD5_STEP(MD5_F, c, d, a, b, M[14], 0xa679438eu, 17) MD5_STEP(MD5_F, b, c, d, a, M[15], 0x49b40821u, 22)
-  MD5_STEP(MD5_G, a, b, c, d, M[1], 0xf61e2562u, 5) MD5_STEP(MD5_G, d, a, b, c, M[6], 0xc040b340u, 9)
-  MD5_STEP(MD5_G, c, d, a, b, M[11], 0x265e5a51u, 14) MD5_STEP(MD5_G, b, c, d, a, M[0], 0xe9b6c7aau, 20)
-  MD5_STEP(MD5_G, a, b, c, d, M[5], 0xd62f105du, 5) MD5_STEP(MD5_G, d, a, b, c, M[10], 0x02441453u, 9)
-  MD5_STEP(MD5_G, c, d, a, b, M[15], 0xd8a1e681u, 14) MD5_STEP(MD5_G, b, c, d, a, M[4], 0xe7d3fbc8u, 20)
-  MD5_STEP(MD5_G, a, b, c, d, M[9], 0x21e1cde6u, 5) MD5_STEP(MD5_G, d, a, b, c, M[14], 0xc33707d6u, 9)
-  MD5_STEP(MD5_G, c, d, a, b, M[3], 0xf4d50d87u, 14) MD5_STEP(MD5_G, b, c, d, a, M[8], 0x455a14edu, 20)
-  MD5_STEP(MD5_G, a, b, c, d, M[13], 0xa9e3e905u, 5) MD5_STEP(MD5_G, d, a, b, c, M[2], 0xfcefa3f8u, 9)
-  MD5_STEP(MD5_G, c, d, a, b, M[7], 0x676f02d9u, 14) MD5_STEP(MD5_G, b, c, d, a, M[12], 0x8d2a4c8au, 20)
-  MD5_STEP(MD5_H, a, b, c, d, M[5], 0xfffa3942u, 4) MD5_STEP(MD5_H, d, a, b, c, M[8], 0x8771f681u, 11)
-  MD5_STEP(MD5_H, c, d, a, b, M[11], 0x6d9d6122u, 16) MD5_STEP(MD5_H, b, c, d, a, M[14], 0xfde5380cu, 23)
-  MD5_STEP(MD5_H, a, b, c, d, M[1], 0xa4beea44u, 4) MD5_STEP(MD5_H, d, a, b, c, M[4], 0x4bdecfa9u, 11)
-  MD5_STEP(MD5_H, c, d, a, b, M[7], 0xf6bb4b60u, 16) MD5_STEP(MD5_H, b, c, d, a, M[10], 0xbebfbc70u, 23)
-  MD5_STEP(MD5_H, a, b, c, d, M[13], 0x289b7ec6u, 4) MD5_STEP(MD5_H, d, a, b, c, M[0], 0xeaa127fau, 11)
-  MD5_STEP(MD5_H, c, d, a, b, M[3], 0xd4ef3085u, 16) MD5_STEP(MD5_H, b, c, d, a, M[6], 0x04881d05u, 23)
-  MD5_STEP(MD5_H, a, b, c, d, M[9], 0xd9d4d039u, 4) MD5_STEP(MD5_H, d, a, b, c, M[12], 0xe6db99e5u, 11)
-  MD5_STEP(MD5_H, c, d, a, b, M[15], 0x1fa27cf8u, 16) MD5_STEP(MD5_H, b, c, d, a, M[2], 0xc4ac5665u, 23)
-  MD5_STEP(MD5_I, a, b, c, d, M[0], 0xf4292244u, 6) MD5_STEP(MD5_I, d, a, b, c, M[7], 0x432aff97u, 10)
-  MD5_STEP(MD5_I, c, d, a, b, M[14], 0xab9423a7u, 15) MD5_STEP(MD5_I, b, c, d, a, M[5], 0xfc93a039u, 21)
-  MD5_STEP(MD5_I, a, b, c, d, M[12], 0x655b59c3u, 6) MD5_STEP(MD5_I, d, a, b, c, M[3], 0x8f0ccc92u, 10)
-  MD5_STEP(MD5_I, c, d, a, b, M[10], 0xffeff47du, 15) MD5_STEP(MD5_I, b, c, d, a, M[1], 0x85845dd1u, 21)
-  MD5_STEP(MD5_I, a, b, c, d, M[8], 0x6fa87e4fu, 6) MD5_STEP(MD5_I, d, a, b, c, M[15], 0xfe2ce6e0u, 10)
-  MD5_STEP(MD5_I, c, d, a, b, M[6], 0xa3014314u, 15) MD5_STEP(MD5_I, b, c, d, a, M[13], 0x4e0811a1u, 21)
-  MD5_STEP(MD5_I, a, b, c, d, M[4], 0xf7537e82u, 6) MD5_STEP(MD5_I, d, a, b, c, M[11], 0xbd3af235u, 10)
-  MD5_STEP(MD5_I, c, d, a, b, M[2], 0x2ad7d2bbu, 15) MD5_STEP(MD5_I, b, c, d, a, M[9], 0xeb86d391u, 21)
-  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-}
-
-#define MD4_F(x, y, z) (((x) & (y)) | (~(x) & (z)))
-#define MD4_G(x, y, z) (((x) & (y)) | ((x) & (z)) | ((y) & (z)))
-#define MD4_H(x, y, z) ((x) ^ (y) ^ (z))
-#define MD4_R1(a, b, c, d, k, s) a = rotl(a + MD4_F(b, c, d) + M[k], s);
-#define MD4_R2(a, b, c, d, k, s) a = rotl(a + MD4_G(b, c, d) + M[k] + 0x5a827999u, s);
-#define MD4_R3(a, b, c, d, k, s) a = rotl(a + MD4_H(b, c, d) + M[k] + 0x6ed9eba1u, s);
-
-__device__ __forceinline__ void md4_block(u32* st, const u32* M) {
-  u32 a = st[0], b = st[1], c = st[2], d = st[3];
-  MD4_R1(a, b, c, d, 0, 3) MD4_R1(d, a, b, c, 1, 7) MD4_R1(c, d, a, b, 2, 11) MD4_R1(b, c, d, a, 3, 19)
-  MD4_R1(a, b, c, d, 4, 3) MD4_R1(d, a, b, c, 5, 7) MD4_R1(c, d, a, b, 6, 11) MD4_R1(b, c, d, a, 7, 19)
-  MD4_R1(a, b, c, d, 8, 3) MD4_R1(d, a, b, c, 9, 7) MD4_R1(c, d, a, b, 10, 11) MD4_R1(b, c, d, a, 11, 19)
-  MD4_R1(a, b, c, d, 12, 3) MD4_R1(d, a, b, c, 13, 7) MD4_R1(c, d, a, b, 14, 11) MD4_R1(b, c, d, a, 15, 19)
-  MD4_R2(a, b, c, d, 0, 3) MD4_R2(d, a, b, c, 4, 5) MD4_R2(c, d, a, b, 8, 9) MD4_R2(b, c, d, a, 12, 13)
-  MD4_R2(a, b, c, d, 1, 3) MD4_R2(d, a, b, c, 5, 5) MD4_R2(c, d, a, b, 9, 9) MD4_R2(b, c, d, a, 13, 13)
-  MD4_R2(a, b, c, d, 2, 3) MD4_R2(d, a, b, c, 6, 5) MD4_R2(c, d, a, b, 10, 9) MD4_R2(b, c, d, a, 14, 13)
-  MD4_R2(a, b, c, d, 3, 3) MD4_R2(d, a, b, c, 7, 5) MD4_R2(c, d, a, b, 11, 9) MD4_R2(b, c, d, a, 15, 13)
-  MD4_R3(a, b, c, d, 0, 3) MD4_R3(d, a, b, c, 8, 9) MD4_R3(c, d, a, b, 4, 11) MD4_R3(b, c, d, a, 12, 15)
-  MD4_R3(a, b, c, d, 2, 3) MD4_R3(d, a, b, c, 10, 9) MD4_R3(c, d, a, b, 6, 11) MD4_R3(b, c, d, a, 14, 15)
-  MD4_R3(a, b, c, d, 1, 3) MD4_R3(d, a, b, c, 9, 9) MD4_R3(c, d, a, b, 5, 11) MD4_R3(b, c, d, a, 13, 15)
-  MD4_R3(a, b, c, d, 3, 3) MD4_R3(d, a, b, c, 11, 9) MD4_R3(c, d, a, b, 7, 11) MD4_R3(b, c, d, a, 15, 15)
-  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-}
-
-// 4 message bytes at byte offset off of an LDS buffer (two aligned reads + funnel shift)
-__device__ __forceinline__ u32 lds4(const uint8_t* base, u32 off) {
-  const u32* p = (const u32*)(base + (off & ~3u));
-  return __builtin_amdgcn_alignbyte(p[1], p[0], off & 3u);
 }
 
 __device__ __forceinline__ u32 glob4(const uint8_t* base, u64 off, u64 lim) {
@@ -207,18 +128,7 @@ __device__ u32 utf16le(const uint8_t* lbase, u32 loff, const uint8_t* gbase, u64
 }
 
 __device__ __forceinline__ bool probe(const A5xDigLaunch& a, const u32* d) {
-  if ((d[0] | d[1] | d[2] | d[3]) == 0u) return a.has_zero_target != 0;
-  const u32 bi = d[0] & a.bm_mask;
-  if (!((a.bitmap[bi >> 5] >> (bi & 31u)) & 1u)) return false;
-  const u64 h = ((u64)d[1] | ((u64)d[2] << 32)) * 0x9E3779B97F4A7C15ull;
-  u64 slot = (h >> 20) & a.tmask;
-  for (u64 n = 0; n <= a.tmask; n++) {
-    const uint4 e = a.table[slot];
-    if (e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3]) return true;
-    if ((e.x | e.y | e.z | e.w) == 0u) return false;
-    slot = (slot + 1) & a.tmask;
-  }
-  return false;
+  return md_probe(a.bitmap, a.bm_mask, a.table, a.tmask, a.has_zero_target != 0, d);
 }
 
 template <u32 BLK>

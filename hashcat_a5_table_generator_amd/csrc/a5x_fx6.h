@@ -25,16 +25,7 @@
 
 // (FxRun, the wave's staging state, and the ring flush are defined by the includer.)
 
-// LDS byte addresses as plain u32 (ds_* instructions take a VGPR address + an offset)
-typedef __attribute__((address_space(3))) u32 fx6_lds32;
-__device__ __forceinline__ u32 fx6_addr(const void* p) {
-  return (u32)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ void fx6_st(u32 a, u32 v) { *(fx6_lds32*)(uintptr_t)a = v; }
-
-// byte shift of a piece: w_k = bytes [4k - n, 4k - n + 4) of the piece (v_perm selector;
-// n replicated into every byte by a perm with selector 0)
-__device__ __forceinline__ u32 fx6_sel(u32 n) { return 0x07060504u - __builtin_amdgcn_perm(0u, n, 0u); }
+#include "a5x_ring.h"
 
 // One piece (entry e: 15 content bytes + length in byte 15) appended at LDS byte
 // address P.  Only the piece's complete dwords are written (t = (P & 3) + length:
@@ -196,44 +187,18 @@ __device__ __forceinline__ u32 fx6_word(u32 rw, u32 k, u32 rr, u32 nl, u32& jcur
   return j;
 }
 
-// ---------------------------------------------------------------------------
-// OR placement (FX_OR): the ring is kept zeroed between rounds and every piece ORs
-// its byte-shifted dwords into it (ds_or_b32).  Entries are zero past their length,
-// so the dwords a piece touches beyond its own bytes receive zeros: no ordering, no
-// pending-dword register, no shared-dword merge across lanes, no trash redirection.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void fx7_or(u32 a, u32 v) {
-  __hip_atomic_fetch_or((fx6_lds32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
-
-// (NOOR: timing ablation of the diagnostic build -- the dwords are folded into sink
-// instead of stored)
-template <bool NOOR = false>
-__device__ __forceinline__ void fx7_put(const uint4 e, u32& P, u32& sink) {
-  const u32 n = P & 3u, base = P - n;
-  const u32 l = e.w >> 24, e3 = e.w & 0xFFFFFFu;
-  const u32 sel = fx6_sel(n);
-  const u32 t = n + l;
-  auto put = [&](u32 a, u32 v) {
-    if constexpr (NOOR) sink ^= v + a;
-    else fx7_or(a, v);
-  };
-  put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
-  put(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
-  if (__builtin_amdgcn_ballot_w64(t > 8u)) {  // pieces reaching a third dword (wave-uniform)
-    put(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
-    if (__builtin_amdgcn_ballot_w64(t > 12u)) {
-      put(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
-      if (__builtin_amdgcn_ballot_w64(t > 16u)) put(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
-    }
-  }
-  P += l;
-}
-
 // fx6_round with OR placement (same run / fit / scan logic; ring zero past R.pos)
+// A lane's run of the last round, for the fused digest (FLUSH::DIGEST): ring byte
+// offset of its first candidate, candidate lengths ('\n' included), window word, rank.
+struct FxLaneRun {
+  u32 off, nc, j, st;
+  u32 clen[4];
+};
+
 template <int NB, int K, bool NOOR = false, class FLUSH>
 __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
-                                         u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush) {
+                                         u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush, FxLaneRun& lr) {
+  static_assert(K <= 4, "FxLaneRun holds 4 candidates");
   const u32 lane = lane_id();
   const uint4 q0 = wq[j][0], q1 = wq[j][1];
   const u32 st = act ? (rr + lane - q1.w) * K + rb[j] : 0u;  // first rank of the run
@@ -244,22 +209,24 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
   constexpr bool HOLD = NB <= 2;
   uint4 ent[HOLD ? K : 1][HOLD ? NB : 1];
   u32 idx[HOLD ? 1 : K][HOLD ? 1 : NB];
-  u32 len = 0;
+  u32 len = 0, clen[K];
   const uint8_t* lenb = (const uint8_t*)be + 15;
 #pragma unroll
   for (int c = 0; c < K; c++) {
     if (c > 0) fx6_step<NB>(q1.x, d);
+    clen[c] = 0;
 #pragma unroll
     for (int b = 0; b < NB; b++) {
       const u32 ix = c < (int)nc ? fx6_eb(q1, b) + d[b] : (u32)FX6_ZBE;  // past the run: empty
       if constexpr (HOLD) {
         ent[c][b] = be[ix];
-        len += ent[c][b].w >> 24;
+        clen[c] += ent[c][b].w >> 24;
       } else {
         idx[c][b] = ix;
-        len += lenb[16u * ix];
+        clen[c] += lenb[16u * ix];
       }
     }
+    len += clen[c];
   }
   const u32 incl = wave_incl_scan_u32(len);
   const u32 used = (u32)(R.pos - R.B);
@@ -284,6 +251,15 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
   }
   R.pos = uniform64(R.pos + tot);
   WAVE_SYNC();
-  flush(R);
+  if constexpr (FLUSH::DIGEST) {  // the caller hashes the runs where they were placed
+    lr.off = used + incl - len;
+    lr.nc = fit ? nc : 0u;
+    lr.j = j;
+    lr.st = st;
+#pragma unroll
+    for (int c = 0; c < 4; c++) lr.clen[c] = c < K ? clen[c] : 0u;
+  } else {
+    flush(R);
+  }
   return nact;
 }

@@ -1410,6 +1410,8 @@ int a5x_set_targets(a5x_ctx* c, int algo, const uint8_t* dig, uint64_t n) {
   return A5X_OK;
 }
 
+static_assert(sizeof(a5x_hit) == sizeof(A5xHitRaw), "resolved device hits are copied out as a5x_hit");
+
 int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode,
                              int mn, int mx, uint64_t scratch_bytes, a5x_hit* hits, uint64_t hit_cap,
                              uint64_t* n_hits, a5x_stats* stats, void* stream) {
@@ -1424,6 +1426,60 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
   if ((rc = grow(c, c->dg_cand_off, nw + 1)) || (rc = grow(c, c->dg_byte_off, nw + 1))) return rc;
   if ((rc = job_prepare(c, J, c->dg_cand_off.p, c->dg_byte_off.p, true))) return rc;
   const uint64_t tc = J.B.total_cands, tb = J.B.total_bytes;
+  // Fused path (default mode, MD5, every candidate-bearing word FAST): k_expand_fast_md5
+  // hashes each candidate in the LDS ring where it is built -- no HBM scratch, no second
+  // pass, hits already (word, candidate).  Otherwise the two-pass range loop below.
+  const bool fused = mode == A5X_MODE_DEFAULT && c->t_algo == A5X_ALGO_MD5 && J.B.nslow == 0 && J.B.nbig == 0 &&
+                     tc > 0 && !getenv("A5X_NO_FUSED_DIGEST");
+  if (fused) {
+    uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
+    if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+    uint64_t nh = 0;
+    float ms = 0;
+    for (;;) {
+      A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
+      const A5xDigLaunch D = dig_launch(c);
+      E.cand_begin = 0;
+      E.cand_end = tc;
+      E.dg_bitmap = D.bitmap; E.dg_bm_mask = D.bm_mask; E.dg_has_zero = D.has_zero_target;
+      E.dg_table = D.table; E.dg_tmask = D.tmask;
+      E.dg_hits = c->dg_hits.p; E.dg_hit_cap = (uint32_t)dev_hits; E.dg_nhits = c->d_scalars + 8;
+      HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
+      HIPCHK(c, hipEventRecord(c->ev[1], J.st));
+      HIPCHK(c, a5x_launch_expand(E, 3, J.st));
+      HIPCHK(c, hipEventRecord(c->ev[2], J.st));
+      HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      HIPCHK(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+      if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+      nh = c->h_scalars[8];
+      if (nh <= dev_hits || hit_cap <= dev_hits) break;
+      dev_hits = std::min<uint64_t>(nh, hit_cap);  // run again with room for every hit the caller takes
+      if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+    }
+    const uint64_t take = std::min(std::min(nh, dev_hits), hit_cap);
+    if (take) {
+      HIPCHK(c, hipMemcpyAsync(hits, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+    }
+    a5x_stats total;
+    memset(&total, 0, sizeof total);
+    total.words = nw;
+    total.candidates = tc;
+    total.bytes = tb;
+    total.expand_launches = 1;
+    float a = 0;
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    total.ms_keyspace = a;
+    total.ms_expand = ms;  // expansion + digest + lookup, fused
+    total.ms_total = a + ms;
+    if (n_hits) *n_hits = nh;
+    if (stats) *stats = total;
+    if (nh > hit_cap)
+      return fail(c, A5X_E_CAPACITY, "%llu hits, buffer has %llu", (unsigned long long)nh,
+                  (unsigned long long)hit_cap);
+    return A5X_OK;
+  }
   uint64_t cap = scratch_bytes ? scratch_bytes : ((uint64_t)2 << 30);
   cap = std::max<uint64_t>(4096, std::min<uint64_t>(cap, tb + 64));
   std::vector<Range> ranges;

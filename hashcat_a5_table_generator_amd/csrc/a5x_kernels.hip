@@ -25,8 +25,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "a5x_format.h"
 #include "a5x_plan.h"
+#include "a5x_launch.h"
 
 #define WAVE_SYNC()                                          \
   do {                                                       \
@@ -891,6 +894,13 @@ struct ExpArgs {
   const u64* rec;        // FAST plan records (k_keyspace_thread)
   const u32* roff;       // per word: record offset into rec
   u64 rec_n;             // u64 in rec
+  // fused digest (k_expand_fast_dig): target set (a5x_md.h md_probe) and hits
+  const u32* dg_bitmap;
+  u32 dg_bm_mask, dg_has_zero, dg_hit_cap;
+  const uint4* dg_table;
+  u64 dg_tmask;
+  A5xHitRaw* dg_hits;    // (word, candidate in word, digest)
+  u32* dg_nhits;
 };
 
 // Record the first tripped guard (code + context) and flag the call as failed.
@@ -1390,6 +1400,7 @@ __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) 
 }
 
 #include "a5x_fx6.h"
+#include "a5x_md.h"
 
 // Window metadata of words w .. w + FX_WW - 1 (lane j <-> word w + j, same keyspace
 // tile), all loads issued together.  (No prefetch across the rounds: the registers it
@@ -1413,16 +1424,60 @@ __device__ __forceinline__ FxMeta fx_meta(const ExpArgs& a, u64 w) {
 
 // ring flush for a5x_fx6.h rounds
 struct FxFlush {
+  static constexpr bool DIGEST = false;
   u32* ring;
   const ExpArgs* a;
+  u64 wbase;
   __device__ __forceinline__ void operator()(FxRun& R) { fx_flush(R, ring, *a); }
+  __device__ __forceinline__ void digest(const FxLaneRun&) {}
+};
+
+// Fused digest (main.go:66's candidates hashed where they are built):
+// after a round's placement every lane MD5s its run's candidates straight out of the
+// LDS ring and probes the target set; nothing goes to HBM but the hits, which carry
+// (word, candidate in word) directly.  The ring is then zeroed for the next round.
+struct FxDigest {
+  static constexpr bool DIGEST = true;
+  u32* ring;
+  const ExpArgs* a;
+  u64 wbase;  // global index of window word 0
+  __device__ __forceinline__ void operator()(FxRun& R) {
+    const u32 lane = lane_id();
+    const u32 nb = (u32)(R.pos - R.B + 31u) / 16u;  // the round's bytes + the ORs' zero overhang
+    for (u32 b = lane; b < nb; b += 64) ((uint4*)ring)[b] = make_uint4(0, 0, 0, 0);
+    R.B = R.pos = R.lo = 0;
+    WAVE_SYNC();
+  }
+  __device__ __forceinline__ void digest(const FxLaneRun& lr) {
+    const uint8_t* base = (const uint8_t*)ring;
+    u32 off = lr.off;
+#pragma unroll 1
+    for (u32 c = 0; c < 4; c++) {
+      const u32 l = c == 0 ? lr.clen[0] : c == 1 ? lr.clen[1] : c == 2 ? lr.clen[2] : lr.clen[3];
+      const bool on = c < lr.nc;
+      if (!__builtin_amdgcn_ballot_w64(on)) break;  // runs are filled from candidate 0
+      u32 d[4];
+      md_lds<true>(base, off, on ? l - 1u : 0u, d);  // the candidate without its '\n'
+      if (on && md_probe(a->dg_bitmap, a->dg_bm_mask, a->dg_table, a->dg_tmask, a->dg_has_zero != 0, d)) {
+        const u32 h = atomicAdd(a->dg_nhits, 1u);
+        if (h < a->dg_hit_cap) {
+          A5xHitRaw r;
+          r.blk = wbase + lr.j;
+          r.idx = lr.st + c;
+          r.d[0] = d[0]; r.d[1] = d[1]; r.d[2] = d[2]; r.d[3] = d[3];
+          a->dg_hits[h] = r;
+        }
+      }
+      off += l;
+    }
+  }
 };
 
 // The window's rounds: T runs of K candidates, nl runs per round; each round takes
 // the largest big-piece count among the words it spans (m2 / m3 / m4: window words
 // with >= 2 / 3 / 4 big pieces).
-template <int K>
-__device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FxFlush& fl, u32 T, u32 k, u32 rw, u64 m2,
+template <int K, class FL>
+__device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FL& fl, u32 T, u32 k, u32 rw, u64 m2,
                                           u64 m3, u64 m4) {
   const u32 lane = lane_id();
   const u32 ringa = fx6_addr(ring), trash = ringa + FX_RING + 4u * lane;
@@ -1435,26 +1490,31 @@ __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FxFlush
     const u32 jl = readlane_u32(j, nr - 1u);
     const u64 span = ((2ull << (jl - jcur)) - 1ull) << jcur;  // words jcur .. jl
     u32 took;
+    FxLaneRun lr;
 #ifdef FX_OR
     (void)trash;
 #if FX_ABL & 64
     if (true) {
-      if (span & m4) took = fx7_round<4, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
-      else if (span & m3) took = fx7_round<3, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
-      else if (span & m2) took = fx7_round<2, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
-      else took = fx7_round<1, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+      if (span & m4) took = fx7_round<4, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+      else if (span & m3) took = fx7_round<3, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+      else if (span & m2) took = fx7_round<2, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+      else took = fx7_round<1, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
     } else
 #endif
-    if (span & m4) took = fx7_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
-    else if (span & m3) took = fx7_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
-    else if (span & m2) took = fx7_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
-    else took = fx7_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl);
+    if (span & m4) took = fx7_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+    else if (span & m3) took = fx7_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+    else if (span & m2) took = fx7_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+    else took = fx7_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
 #else
     if (span & m4) took = fx6_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
     else if (span & m3) took = fx6_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
     else if (span & m2) took = fx6_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
     else took = fx6_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
 #endif
+    if constexpr (FL::DIGEST) {
+      fl.digest(lr);
+      fl(R);
+    }
     rr += took;
   }
 }
@@ -1486,6 +1546,7 @@ __device__ __forceinline__ uint4 fx_entry(const u64* rec, u32 d0, u32 wbe, u32 s
   return make_uint4((u32)lo64, (u32)(lo64 >> 32), (u32)hi64, ((u32)(hi64 >> 32) & 0xFFFFFFu) | (off << 24));
 }
 
+template <bool DIG>
 __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
   u64* const rec = (u64*)(ring + 4);  // ring bytes [16, 16 + 8 FX_WREC)
@@ -1505,8 +1566,8 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
   u64 g = g0;
   FxRun R;
   R.open = false; R.B = 0; R.lo = 0; R.pos = 0; R.carry = 0;
-  FxFlush fl;
-  fl.ring = ring; fl.a = &a;
+  typename std::conditional<DIG, FxDigest, FxFlush>::type fl;
+  fl.ring = ring; fl.a = &a; fl.wbase = 0;
   FxMeta M = fx_meta(a, w);
   STAMP_DECL
   while (g < g1) {
@@ -1530,7 +1591,7 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
       // word w is a hole here (slow / BIG) or empty
       const u64 w0c1 = uniform64(c1);
       if (w0c1 > g && w0c1 != ~0ull) {
-        fx_close(R, ring, a);
+        if (!DIG) fx_close(R, ring, a);
         g = min(w0c1, g1);
       }
       w++;
@@ -1644,15 +1705,18 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     }
     WAVE_SYNC();
     STAMP(1);
-    // ---- run position of g ----
-    const u64 r0 = g - wc0;
-    u64 pos = uniform64(bo) - a.out_base;
-    if (!(FX_ABL & 32))
-    if (r0) pos += fast_prefix_bytes(rec + readlane_u32(rb, 0), r0);
-    if (!R.open || R.pos != pos) {
-      fx_close(R, ring, a);
-      R.B = pos & ~15ull; R.lo = pos; R.pos = pos; R.carry = 0; R.open = true;
+    // ---- run position of g (the fused digest writes nothing: its ring restarts at 0) ----
+    if (!DIG) {
+      const u64 r0 = g - wc0;
+      u64 pos = uniform64(bo) - a.out_base;
+      if (!(FX_ABL & 32))
+      if (r0) pos += fast_prefix_bytes(rec + readlane_u32(rb, 0), r0);
+      if (!R.open || R.pos != pos) {
+        fx_close(R, ring, a);
+        R.B = pos & ~15ull; R.lo = pos; R.pos = pos; R.carry = 0; R.open = true;
+      }
     }
+    fl.wbase = w;
 #ifdef FX_OR
     // the records' ring bytes [16, 16 + 8 ntot) back to zero for the OR rounds
     for (u32 i = 1 + lane; i <= (ntot + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
@@ -1671,7 +1735,7 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     M = fx_meta(a, w);
     WAVE_SYNC();
   }
-  fx_close(R, ring, a);
+  if (!DIG) fx_close(R, ring, a);
   STAMP(6);
   STAMP_FLUSH();
 }
@@ -1681,7 +1745,8 @@ __device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + FX_TRASH 
 #ifndef FX_WPE
 #define FX_WPE 4  // 16 waves per CU: <= 128 VGPRs, <= 10 KiB LDS per wave
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE))) k_expand_fast(ExpArgs a) {
+template <bool DIG>
+__device__ __forceinline__ void expand_fast_body(const ExpArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   uint8_t* mine = smem + wv * lds_per_wave_fast();
@@ -1689,7 +1754,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE
   FXWin& F = *(FXWin*)(mine + FX_RING + FX_TRASH);
   const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
   if (chunk * a.CH >= a.cand_end) return;
-  expand_chunk_fast(F, ring, a, chunk);
+  expand_chunk_fast<DIG>(F, ring, a, chunk);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE))) k_expand_fast(ExpArgs a) {
+  expand_fast_body<false>(a);
+}
+
+// the same chunks, hashed (MD5) and probed in the ring instead of written (FxDigest)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE))) k_expand_fast_md5(ExpArgs a) {
+  expand_fast_body<true>(a);
 }
 
 // k_expand_slow / k_expand_b: one k_segments item (a slow or BIG word's run of <= CH
@@ -1892,6 +1966,8 @@ static ExpArgs exp_args(const A5xExpLaunch& L) {
   a.segs = L.segs; a.nsegs = L.nsegs; a.cand_begin = L.cand_begin; a.cand_end = L.cand_end; a.CH = L.CH; a.SEG = L.SEG; a.out = L.out;
   a.out_base = L.out_base; a.out_cap = L.out_cap; a.mn = L.mn; a.mx = L.mx; a.err = L.err; a.dbg = L.dbg;
   a.rec = L.rec; a.roff = L.roff; a.rec_n = L.rec_n;
+  a.dg_bitmap = L.dg_bitmap; a.dg_bm_mask = L.dg_bm_mask; a.dg_has_zero = L.dg_has_zero; a.dg_hit_cap = L.dg_hit_cap;
+  a.dg_table = L.dg_table; a.dg_tmask = L.dg_tmask; a.dg_hits = L.dg_hits; a.dg_nhits = L.dg_nhits;
   return a;
 }
 
@@ -1902,7 +1978,7 @@ size_t a5x_expand_lds(u32 table_bytes, int kind, u32 waves) {
   return waves * ((FX_RING + FX_TRASH + sizeof(FXWin) + 15u) & ~(size_t)15u);
 }
 
-// kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b
+// kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b, 3: k_expand_fast_md5 (fused digest)
 hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   ExpArgs a = exp_args(L);
   const u64 c0 = L.cand_begin / L.CH, c1 = (L.cand_end + L.CH - 1) / L.CH;
@@ -1912,6 +1988,9 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   const u64 nb = (nchunks + waves - 1) / waves;
   if (kind == 0)
     hipLaunchKernelGGL(k_expand_fast, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);
+  else if (kind == 3)
+    hipLaunchKernelGGL(k_expand_fast_md5, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st,
+                       a);
   else if (kind == 1)
     hipLaunchKernelGGL(k_expand_slow, dim3(blocks_for(L.nsegs_bound, waves, 65536)), dim3(64 * waves),
                        a5x_expand_lds(L.table_bytes, 1, waves), st, a);

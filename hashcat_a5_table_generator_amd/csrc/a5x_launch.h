@@ -30,6 +30,7 @@ struct A5xKsLaunch {
   uint64_t cplx_base;
 };
 
+struct A5xHitRaw;
 struct A5xExpLaunch {
   const uint8_t* table;
   uint32_t table_bytes;
@@ -57,6 +58,13 @@ struct A5xExpLaunch {
   const uint64_t* rec;
   const uint32_t* roff;
   uint64_t rec_n;   // u64 in rec
+  // fused digest (kind 3): target set + hit buffer (see A5xDigLaunch)
+  const uint32_t* dg_bitmap;
+  uint32_t dg_bm_mask, dg_has_zero, dg_hit_cap;
+  const uint4* dg_table;
+  uint64_t dg_tmask;
+  A5xHitRaw* dg_hits;
+  uint32_t* dg_nhits;
 };
 
 hipError_t a5x_set_kernel_attrs();

@@ -39,11 +39,13 @@
 #include "a5x.h"
 #include "a5x_format.h"
 #include "a5x_launch.h"
+#include "a5x_ring.h"
 
 namespace {
 
 typedef uint64_t u64;
 typedef uint32_t u32;
+typedef int64_t i64;
 
 #define M_WAVE_SYNC()                                        \
   do {                                                       \
@@ -63,8 +65,21 @@ constexpr u32 M_ERR_CLEN = 1u << 8;   // a candidate longer than A5X_M_CBUF-1
 constexpr u32 LSTRIDE = A5X_M_CBUF + 4;
 constexpr u32 CMAXLEN = A5X_M_CBUF - 1;
 
+// positional -s / -s -r words (m_pos_setup): entries (a5x_ring.h) and the token list
+constexpr u32 MP_NE = 256;    // entries per word: per pattern [keep, values...], then literal chunks
+constexpr u32 MP_PMAX = 16;   // patterns per word (4-bit selector per pattern)
+constexpr u32 MP_VMAX = 14;   // values per pattern (selector 1 + v <= 15)
+
 struct MLds {
   u64 dp[A5X_M_DPMAX];
+  uint4 ent[MP_NE];
+  u32 tok[A5X_M_LMAX + 2];   // entry base | (pattern index + 1) << 16 (0: literal chunk)
+  uint8_t mpi[A5X_M_LMAX];   // pattern index + 1 matched at byte q (0: none)
+  uint8_t pb[MP_PMAX], occ[MP_PMAX];
+  uint8_t elen[MP_NE];       // entry lengths
+  u32 rmag[MP_PMAX];         // radix mode: magic of R_r = 1 + values of pattern r
+  uint8_t rr[MP_PMAX];       // R_r
+  u32 ntok, radix, shift;
   u32 bitmap[A5X_MTAB_KEYS_MAX / 32];
   uint8_t word[A5X_M_LMAX + 16];
   uint16_t pat[64];          // key index per sorted pattern (-s) / per position (-r)
@@ -303,7 +318,8 @@ __device__ MInfo m_setup(MLds& S, const MT& T, const A5xModeLaunch& a, u64 w) {
 
 // Build candidate t (0 <= t < count) of the word set up in S into this lane's
 // buffer; returns its length and the buffer holding it.
-__device__ u32 m_build(MLds& S, const MT& T, const MInfo& I, int mode, u64 t, const uint8_t** outp, u32& err) {
+__device__ u32 m_build(MLds& S, const MT& T, const MInfo& I, int mode, u64 t, const uint8_t** outp, u32& err,
+                       bool len_only = false) {
   const u32 lane = m_lane();
   uint8_t* b0 = S.buf[0] + lane * LSTRIDE;
   uint8_t* b1 = S.buf[1] + lane * LSTRIDE;
@@ -325,6 +341,17 @@ __device__ u32 m_build(MLds& S, const MT& T, const MInfo& I, int mode, u64 t, co
       c--;
     }
     u32 len = I.L;
+    if (len_only) {  // the result's length does not depend on where (or how wrongly) the
+                     // replacements land: L + sum (|subs[0]| - |key|); panics surface in the
+                     // expansion pass, which builds the candidate
+      int l = (int)len;
+      for (u64 m = sel; m; m &= m - 1) {
+        const A5xMKey K = T.keys[S.pat[__builtin_ctzll(m)]];
+        if (K.nvals) l += (int)T.vals[K.val_base].len - (int)K.klen;
+      }
+      *outp = nullptr;
+      return (u32)l;
+    }
     for (u32 i = 0; i < len; i++) b0[i] = S.word[i];
     // combo indices descending, running offset (main.go:249-257)
     int off = 0;
@@ -378,6 +405,275 @@ __device__ u32 m_build(MLds& S, const MT& T, const MInfo& I, int mode, u64 t, co
   return len;
 }
 
+// ---------------------------------------------------------------------------
+// Positional -s / -s -r words.  When every pattern present in the word is one valid
+// UTF-8 codepoint, every value of those patterns is valid UTF-8 of <= 15 bytes, and no
+// value of a pattern contains a LATER (sorted) pattern, the sequential ReplaceAll of a
+// leaf (main.go:339-341, applied in sorted order) equals replacing each ORIGINAL
+// occurrence of a chosen pattern by its value: occurrences of distinct codepoints never
+// overlap, a valid value cannot complete a codepoint across its boundaries, and only a
+// later pass could rewrite an inserted value.  Such a word is a token list (literal
+// chunks and pattern occurrences); a candidate is the concatenation of its tokens'
+// entries (a5x_ring.h) picked by the leaf's per-pattern choice, and its length is
+// L + sum_p occ_p (|v_p| - |p|): no pass builds a candidate only to measure it.
+// ---------------------------------------------------------------------------
+__device__ bool m_valid_utf8(const uint8_t* p, u32 n) {
+  for (u32 i = 0; i < n;) {
+    const u32 sz = m_rune_len(p + i, n - i);
+    if (sz == 1 && p[i] >= 0x80u) return false;
+    i += sz;
+  }
+  return true;
+}
+
+__device__ bool m_contains(const uint8_t* h, u32 hn, const uint8_t* nd, u32 nn) {
+  for (u32 i = 0; i + nn <= hn; i++) {
+    u32 k = 0;
+    while (k < nn && h[i + k] == nd[k]) k++;
+    if (k == nn) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint4 m_entry(const uint8_t* p, u32 n) {
+  u64 lo = 0, hi = 0;
+  for (u32 i = 0; i < n; i++) {
+    if (i < 8) lo |= (u64)p[i] << (8 * i);
+    else hi |= (u64)p[i] << (8 * (i - 8));
+  }
+  return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32) | (n << 24));
+}
+
+// Tokens and entries of the word set up in S (after m_setup, modes -s / -s -r):
+// returns the token count, or 0 when the word is not positional (byte builder path).
+__device__ u32 m_pos_setup(MLds& S, const MT& T, const MInfo& I, int mode) {
+  const u32 lane = m_lane(), n = I.n, L = I.L;
+  if (n == 0 || n > MP_PMAX) return 0;
+  u32 ok = 1, ne = 0;
+  if (lane < n) {
+    const A5xMKey K = T.keys[S.pat[lane]];
+    const uint8_t* kp = T.blob + K.key_off;
+    const u32 nv = mode == A5X_MODE_SUBALL ? K.nvals : (K.nvals ? 1u : 0u);
+    ok = K.klen >= 1 && K.klen <= 4 && m_rune_len(kp, K.klen) == K.klen && (K.klen > 1 || kp[0] < 0x80u) &&
+         nv <= MP_VMAX;
+    for (u32 v = 0; ok && v < nv; v++) {
+      const A5xMVal V = T.vals[K.val_base + v];
+      const uint8_t* vp = T.blob + V.off;
+      ok = V.len <= 15 && m_valid_utf8(vp, V.len);
+      for (u32 j = lane + 1; ok && j < n; j++) {
+        const A5xMKey Kj = T.keys[S.pat[j]];
+        ok = !m_contains(vp, V.len, T.blob + Kj.key_off, Kj.klen);
+      }
+    }
+    ne = 1 + nv;
+  }
+  if (__ballot(!ok)) return 0;
+  const u32 incl = m_incl_scan(ne);
+  const u32 npe = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+  if (npe > MP_NE) return 0;
+  M_WAVE_SYNC();
+  if (lane < n) {  // pattern entries: [keep, value 0, value 1, ...]
+    const u32 b = incl - ne;
+    const A5xMKey K = T.keys[S.pat[lane]];
+    S.pb[lane] = (uint8_t)b;
+    S.occ[lane] = 0;
+    S.ent[b] = m_entry(T.blob + K.key_off, K.klen);
+    for (u32 v = 0; v + 1 < ne; v++) {
+      const A5xMVal V = T.vals[K.val_base + v];
+      S.ent[b + 1 + v] = m_entry(T.blob + V.off, V.len);
+    }
+  }
+  for (u32 q = lane; q < L; q += 64) {  // occurrences (distinct codepoints: at most one per byte)
+    u32 m = 0;
+    for (u32 i = 0; i < n && !m; i++)
+      if (m_match(T, S.word, L, q, S.pat[i])) m = i + 1;
+    S.mpi[q] = (uint8_t)m;
+  }
+  M_WAVE_SYNC();
+  if (lane == 0) {  // token list: occurrences and <= 15-byte literal chunks, in byte order
+    u32 nt = 0, e = npe, q = 0;
+    bool over = false;
+    while (q < L) {
+      const u32 pi = S.mpi[q];
+      if (pi) {
+        S.tok[nt++] = S.pb[pi - 1] | (pi << 16);
+        S.occ[pi - 1]++;
+        q += T.keys[S.pat[pi - 1]].klen;
+      } else {
+        if (e >= MP_NE) { over = true; break; }
+        u32 k = 0;
+        u64 lo = 0, hi = 0;
+        while (q < L && !S.mpi[q] && k < 15) {
+          const u64 b = S.word[q];
+          if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
+          k++;
+          q++;
+        }
+        S.ent[e] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32) | (k << 24));
+        S.tok[nt++] = e++;
+      }
+    }
+    S.ntok = over ? 0u : nt;
+    // radix mode: no effective size window (min <= 1, max >= #patterns) -- the leaves are
+    // every per-pattern choice vector (minus the all-keep one when min = 1), enumerated
+    // as the mixed radix over patterns (pattern 0 least significant, digit 0 = keep);
+    // exact 32-bit magic division needs leaf (R - 1) < 2^32: count < 2^27
+    S.radix = (I.cmin <= 1 && I.cmax >= n && I.count + 1 < (1ull << 27)) ? 1u : 0u;
+    S.shift = I.cmin;  // leaf 0 (all keep) skipped when min = 1
+  }
+  if (lane < n) {
+    const A5xMKey K = T.keys[S.pat[lane]];
+    const u32 nv = mode == A5X_MODE_SUBALL ? K.nvals : (K.nvals ? 1u : 0u);
+    const u32 R = 1 + nv;
+    S.rr[lane] = (uint8_t)R;
+    S.rmag[lane] = R > 1 ? (u32)((((u64)1 << 32) + R - 1) / R) : 0u;
+  }
+  for (u32 e = lane; e < MP_NE; e += 64) S.elen[e] = (uint8_t)(S.ent[e].w >> 24);
+  M_WAVE_SYNC();
+  return (u32)__builtin_amdgcn_readfirstlane((int)S.ntok);
+}
+
+// Sum over leaves t in [0, x) of (len + 1) in radix mode (closed form; lanes over
+// patterns): x (L + 1) + sum_r occ_r sum_{t'} delta_r(digit_r(t')), t' = t + shift.
+__device__ u64 m_pos_prefix(const MLds& S, const MInfo& I, u64 x) {
+  const u32 lane = m_lane(), n = I.n;
+  auto G = [&](u64 y) -> i64 {  // this lane's pattern: sum_{t' < y} delta(digit(t'))
+    if (lane >= n) return 0;
+    u64 P = 1;  // place value of pattern lane
+    for (u32 q = 0; q < lane; q++) P *= S.rr[q];
+    const u32 b = S.pb[lane], R = S.rr[lane];
+    const int k0 = S.elen[b];
+    i64 sumd = 0;
+    for (u32 v = 1; v < R; v++) sumd += (int)S.elen[b + v] - k0;
+    const u64 cyc = P * R, full = y / cyc, rem = y - full * cyc, dv = rem / P;
+    i64 g = (i64)(full * P) * sumd;
+    for (u32 v = 1; v < dv; v++) g += (i64)P * ((int)S.elen[b + v] - k0);
+    if (dv >= 1 && dv < R) g += (i64)(rem - dv * P) * ((int)S.elen[b + dv] - k0);
+    return g * (i64)S.occ[lane];
+  };
+  i64 tot = G(x + S.shift) - G(S.shift);
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) tot += (i64)__shfl_xor((long long)tot, d, 64);
+  return x * (u64)(I.L + 1) + (u64)tot;
+}
+
+// Leaf t of a positional word: per-pattern selectors (4 bits each: 0 keep, 1 + v value
+// v) by walking the DP table as m_build does; returns the candidate length.
+__device__ u32 m_pos_sel(const MLds& S, const MT& T, const MInfo& I, int mode, u64 t, u64& sel) {
+  if (S.radix) {  // mixed-radix digits by magic division (pattern 0 least significant)
+    u32 x = (u32)t + S.shift, len = I.L;
+    u64 sv = 0;
+    for (u32 r = 0; r < I.n; r++) {
+      const u32 mg = S.rmag[r];
+      const u32 q = __umulhi(x, mg) + (mg ? 0u : x);
+      const u32 dgt = x - q * S.rr[r];
+      sv |= (u64)dgt << (4 * r);
+      len += (u32)((int)S.occ[r] * ((int)S.elen[S.pb[r] + dgt] - (int)S.elen[S.pb[r]]));
+      x = q;
+    }
+    sel = sv;
+    return len;
+  }
+  const u64* D = S.dp;
+  const u32 cols = I.cols, n = I.n;
+  u32 c = I.cmin;
+  while (c < I.cmax && t >= D[c]) { t -= D[c]; c++; }
+  int len = (int)I.L;
+  u64 sv = 0;
+  for (u32 r = 0; r < n && c > 0; r++) {
+    const u64 a0 = D[(r + 1) * cols + c];
+    if (t < a0) continue;
+    t -= a0;
+    const A5xMKey K = T.keys[S.pat[r]];
+    u32 v = 0;
+    if (mode == A5X_MODE_SUBALL && K.nvals > 1) {
+      const u64 b = D[(r + 1) * cols + c - 1];
+      v = ((t | b) >> 32) ? (u32)(t / b) : (u32)t / (u32)b;
+      t -= (u64)v * b;
+    }
+    len += (int)S.occ[r] * ((int)T.vals[K.val_base + v].len - (int)K.klen);
+    sv |= (u64)(1 + v) << (4 * r);
+    c--;
+  }
+  sel = sv;
+  return (u32)len;
+}
+
+// bytes [lo, hi) of the 16-B block at out offset X
+__device__ __forceinline__ void m_store_part(uint8_t* out, u64 X, const uint4 x, u64 lo, u64 hi) {
+  const u32 w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (u32 b = 0; b < 16; b++)
+    if (X + b >= lo && X + b < hi) out[X + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+}
+
+__device__ __forceinline__ void m_store16_nt(uint8_t* p, const uint4 x) {
+  typedef u32 v4u __attribute__((ext_vector_type(4)));
+  v4u y = {x.x, x.y, x.z, x.w};
+  __builtin_nontemporal_store(y, (v4u*)p);
+}
+
+// Expand leaves [tb, te) of the positional word set up in S; the first one's bytes
+// start at a.out + pos0.  64 leaves per round: lengths (formula) -> wave scan ->
+// every token's entry OR-placed into the zeroed ring (S.buf) -> complete 16-B blocks
+// streamed with dwordx4 stores (the item's first and last blocks byte-exact).
+__device__ void m_pos_expand(MLds& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 tb, u64 te, u64 pos0,
+                             u32 ntok, u32& err) {
+  const u32 lane = m_lane();
+  uint4* r4 = (uint4*)&S.buf[0][0];
+  constexpr u32 RB = sizeof(S.buf) / 16;
+  static_assert(sizeof(S.buf) >= 16 + 64 * A5X_M_CBUF + 32, "ring: one round of 64 candidates");
+  const u32 ringa = fx6_addr(r4);
+  for (u32 i = lane; i < RB; i += 64) r4[i] = make_uint4(0, 0, 0, 0);
+  M_WAVE_SYNC();
+  u64 B = pos0 & ~15ull, pos = pos0;
+  const u64 lo = pos0;
+  const uint4 nl = make_uint4(0x0Au, 0u, 0u, 1u << 24);
+  for (u64 t0 = tb; t0 < te; t0 += 64) {
+    const u64 t = t0 + lane;
+    u64 sel = 0;
+    u32 len = 0;
+    if (t < te) {
+      len = m_pos_sel(S, T, I, a.mode, t, sel) + 1;
+      if (len > A5X_M_CBUF) { err |= M_ERR_CLEN; len = 0; }
+    }
+    const u32 incl = m_incl_scan(len);
+    const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    u32 P = ringa + (u32)(pos - B) + incl - len, sink = 0;
+    if (len) {
+      for (u32 k = 0; k < ntok; k++) {
+        const u32 d = S.tok[k], pi = d >> 16;
+        const u32 ix = (d & 0xFFFFu) + (pi ? (u32)(sel >> (4 * (pi - 1))) & 15u : 0u);
+        fx7_put(S.ent[ix], P, sink);
+      }
+      fx7_put(nl, P, sink);
+    }
+    pos += tot;
+    M_WAVE_SYNC();
+    const u32 nb = (u32)((pos - B) >> 4);
+    if (B + 16ull * nb > a.out_cap) { err |= M_ERR_GUARD; return; }
+    for (u32 b = lane; b < nb; b += 64) {
+      const uint4 x = r4[b];
+      const u64 X = B + 16ull * b;
+      if (X >= lo) m_store16_nt(a.out + X, x);
+      else m_store_part(a.out, X, x, lo, X + 16);
+      r4[b] = make_uint4(0, 0, 0, 0);
+    }
+    if (lane == 0 && nb) {
+      const uint4 x = r4[nb];
+      r4[nb] = make_uint4(0, 0, 0, 0);
+      r4[0] = x;
+    }
+    B += 16ull * nb;
+    M_WAVE_SYNC();
+  }
+  if (lane == 0 && pos > B) {
+    if (pos > a.out_cap) err |= M_ERR_GUARD;
+    else m_store_part(a.out, B, r4[0], lo > B ? lo : B, pos);
+  }
+  M_WAVE_SYNC();
+}
+
 __device__ __forceinline__ void m_err(u32* e, u32 bits) {
   if (bits && m_lane() == 0) atomicOr(e, bits);
 }
@@ -404,7 +700,7 @@ __global__ void __launch_bounds__(64) k_mode_count(A5xModeLaunch a) {
 // op 1 = write them at out[base + prefix - out_base] when their global index
 // (g0 + t) is inside [cand_begin, cand_end).
 __device__ u64 m_run(MLds& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 t0, u32 nc, int op,
-                     u64 g0, u64 base, u32& err) {
+                     u64 g0, u64 base, u32& err, u32 ntok = 0) {
   const u32 lane = m_lane();
   u64 run = 0;
   for (u32 k0 = 0; k0 < nc; k0 += 64) {
@@ -412,7 +708,13 @@ __device__ u64 m_run(MLds& S, const MT& T, const MInfo& I, const A5xModeLaunch& 
     const bool v = k < nc;
     const uint8_t* p = nullptr;
     u32 len = 0;
-    if (v) len = m_build(S, T, I, a.mode, t0 + k, &p, err) + 1;
+    if (v && ntok && op == 0) {  // positional word: the length formula
+      u64 sel;
+      len = m_pos_sel(S, T, I, a.mode, t0 + k, sel) + 1;
+      if (len > A5X_M_CBUF) { err |= M_ERR_CLEN; len = 0; }
+    } else if (v) {
+      len = m_build(S, T, I, a.mode, t0 + k, &p, err, op == 0 && a.mode == A5X_MODE_REVERSE) + 1;
+    }
     const u32 incl = m_incl_scan(len);
     const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
     if (op == 1 && v) {
@@ -445,10 +747,24 @@ __global__ void __launch_bounds__(64) k_mode_items(A5xModeLaunch a, int op) {
     const u32 nc = (u32)min(a.SEG, cnt - t0);
     const MInfo I = m_setup(S, T, a, w);
     if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); continue; }
+    const u32 ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
     u32 err = 0;
-    const u64 base = op == 1 ? a.seg_boff[i] : 0;
-    const u64 run = m_run(S, T, I, a, t0, nc, op, cw0, base, err);
-    if (op == 0 && m_lane() == 0) a.seg_bytes[i] = run;
+    if (ntok && op == 1) {
+      // the leaves of this item inside [cand_begin, cand_end); the first one's bytes start
+      // at seg_boff[i] (or at out_base itself when the range starts inside the item)
+      const u64 rb = a.cand_begin > cw0 ? a.cand_begin - cw0 : 0;
+      const u64 re = a.cand_end - cw0 < t0 + nc ? a.cand_end - cw0 : t0 + nc;  // (cand_end > cw0 here)
+      const u64 tb = rb > t0 ? rb : t0;
+      if (a.cand_end > cw0 && tb < re)
+        m_pos_expand(S, T, I, a, tb, re, tb == t0 ? a.seg_boff[i] - a.out_base : 0, ntok, err);
+    } else if (ntok && S.radix) {  // op 0, radix mode: closed form, no candidate is visited
+      const u64 run = m_pos_prefix(S, I, t0 + nc) - m_pos_prefix(S, I, t0);
+      if (m_lane() == 0) a.seg_bytes[i] = run;
+    } else {
+      const u64 base = op == 1 ? a.seg_boff[i] : 0;
+      const u64 run = m_run(S, T, I, a, t0, nc, op, cw0, base, err, ntok);
+      if (op == 0 && m_lane() == 0) a.seg_bytes[i] = run;
+    }
     m_err(a.err, m_wave_or(err));
   }
 }
@@ -478,7 +794,9 @@ __global__ void __launch_bounds__(64) k_mode_locate(A5xModeLaunch a, const u64* 
       const MInfo I = m_setup(S, T, a, w);
       if (I.bad || I.count != a.cand_off[w + 1] - a.cand_off[w]) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); continue; }
       u32 err = 0;
-      pre = m_run(S, T, I, a, t0, r, 0, 0, 0, err);
+      const u32 ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
+      if (ntok && S.radix) pre = m_pos_prefix(S, I, t0 + r) - m_pos_prefix(S, I, t0);
+      else pre = m_run(S, T, I, a, t0, r, 0, 0, 0, err, ntok);
       m_err(a.err, m_wave_or(err));
     }
     if (m_lane() == 0) { out[3 * q] = item; out[3 * q + 1] = r; out[3 * q + 2] = a.seg_boff[item] + pre; }

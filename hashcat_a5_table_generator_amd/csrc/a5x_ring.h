@@ -1,0 +1,56 @@
+// a5x_ring.h -- byte-stream placement into a per-wave LDS ring (device only; used by
+// k_expand_fast (a5x_fx6.h) and the -s / -s -r positional engine (a5x_modes.hip)).
+//
+// An entry is a uint4: 15 content bytes (zero past the length) + the length in byte
+// 15.  fx7_put appends one entry at LDS byte address P by OR-ing its byte-shifted
+// dwords into a ring that is kept zeroed between flushes (ds_or_b32): the dwords an
+// entry touches beyond its own bytes receive zeros, so no ordering between lanes or
+// entries is needed.
+#pragma once
+#include <stdint.h>
+
+// LDS byte addresses as plain uint32_t (ds_* instructions take a VGPR address + an offset)
+typedef __attribute__((address_space(3))) uint32_t fx6_lds32;
+__device__ __forceinline__ uint32_t fx6_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void fx6_st(uint32_t a, uint32_t v) { *(fx6_lds32*)(uintptr_t)a = v; }
+
+// byte shift of a piece: w_k = bytes [4k - n, 4k - n + 4) of the piece (v_perm selector;
+// n replicated into every byte by a perm with selector 0)
+__device__ __forceinline__ uint32_t fx6_sel(uint32_t n) { return 0x07060504u - __builtin_amdgcn_perm(0u, n, 0u); }
+
+// ---------------------------------------------------------------------------
+// OR placement: the ring is kept zeroed between rounds and every piece ORs
+// its byte-shifted dwords into it (ds_or_b32).  Entries are zero past their length,
+// so the dwords a piece touches beyond its own bytes receive zeros: no ordering, no
+// pending-dword register, no shared-dword merge across lanes, no trash redirection.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fx7_or(uint32_t a, uint32_t v) {
+  __hip_atomic_fetch_or((fx6_lds32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// (NOOR: timing ablation (FX_ABL & 64 builds) -- the dwords are folded into sink
+// instead of stored)
+template <bool NOOR = false>
+__device__ __forceinline__ void fx7_put(const uint4 e, uint32_t& P, uint32_t& sink) {
+  const uint32_t n = P & 3u, base = P - n;
+  const uint32_t l = e.w >> 24, e3 = e.w & 0xFFFFFFu;
+  const uint32_t sel = fx6_sel(n);
+  const uint32_t t = n + l;
+  auto put = [&](uint32_t a, uint32_t v) {
+    if constexpr (NOOR) sink ^= v + a;
+    else fx7_or(a, v);
+  };
+  put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
+  put(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
+  if (__builtin_amdgcn_ballot_w64(t > 8u)) {  // pieces reaching a third dword (wave-uniform)
+    put(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
+    if (__builtin_amdgcn_ballot_w64(t > 12u)) {
+      put(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
+      if (__builtin_amdgcn_ballot_w64(t > 16u)) put(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
+    }
+  }
+  P += l;
+}
+

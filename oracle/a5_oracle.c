@@ -24,6 +24,7 @@
 #define _GNU_SOURCE
 #include <errno.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -641,30 +642,68 @@ A5O_EXPORT int64_t a5o_expand_batch(const a5o_table *t, const uint8_t *words, co
 /* channel of capacity 1000 carrying one heap string per candidate, and one  */
 /* writer goroutine with a 4 KiB bufio.Writer doing WriteString(s + "\n").   */
 /* ------------------------------------------------------------------------ */
-#define CHAN_CAP 1000
-/* A buffered Go channel: one lock, a ring of CHAN_CAP, parked senders/receiver
- * are woken only when someone actually waits (Go's runtime hands off the same
- * way instead of signalling on every operation). */
+#define CHAN_CAP 1024  /* Go: make(chan string, 1000); a power of two for the ring index */
+/* A buffered Go channel as a bounded lock-free MPMC ring (D. Vyukov's sequence-number
+ * queue): a sender claims a slot with one CAS and publishes it with a release store;
+ * the receiver takes slots in order.  A full (empty) channel makes the sender
+ * (receiver) spin, then yield the core -- the cheap user-space park/unpark of Go's
+ * runtime, not a kernel condition variable per operation (which serialised 16
+ * senders on one futex and collapsed throughput). */
+typedef struct { _Atomic size_t seq; bstr v; } chan_slot;
 typedef struct {
-    pthread_mutex_t mu; pthread_cond_t not_full, not_empty;
-    bstr q[CHAN_CAP]; size_t head, len; int closed; int wait_send, wait_recv;
+    chan_slot q[CHAN_CAP];
+    _Alignas(64) _Atomic size_t tail;  /* next slot to send into */
+    _Alignas(64) _Atomic size_t head;  /* next slot to receive from (one receiver) */
+    _Alignas(64) _Atomic int closed;
 } chan_t;
 
+static void chan_init(chan_t *c) {
+    for (size_t i = 0; i < CHAN_CAP; i++) atomic_init(&c->q[i].seq, i);
+    atomic_init(&c->tail, 0); atomic_init(&c->head, 0); atomic_init(&c->closed, 0);
+}
+
+static void chan_backoff(unsigned *spins) {
+    if (++*spins < 64) __builtin_ia32_pause(); else { sched_yield(); *spins = 0; }
+}
+
 static void chan_send(chan_t *c, bstr s) {
-    pthread_mutex_lock(&c->mu);
-    while (c->len == CHAN_CAP) { c->wait_send++; pthread_cond_wait(&c->not_full, &c->mu); c->wait_send--; }
-    c->q[(c->head + c->len) % CHAN_CAP] = s; c->len++;
-    if (c->wait_recv) pthread_cond_signal(&c->not_empty);
-    pthread_mutex_unlock(&c->mu);
+    unsigned spins = 0;
+    size_t pos = atomic_load_explicit(&c->tail, memory_order_relaxed);
+    for (;;) {
+        chan_slot *sl = &c->q[pos & (CHAN_CAP - 1)];
+        const size_t seq = atomic_load_explicit(&sl->seq, memory_order_acquire);
+        const intptr_t d = (intptr_t)seq - (intptr_t)pos;
+        if (d == 0) {
+            if (atomic_compare_exchange_weak_explicit(&c->tail, &pos, pos + 1, memory_order_relaxed,
+                                                      memory_order_relaxed)) {
+                sl->v = s;
+                atomic_store_explicit(&sl->seq, pos + 1, memory_order_release);
+                return;
+            }
+        } else if (d < 0) {  /* full: park */
+            chan_backoff(&spins);
+            pos = atomic_load_explicit(&c->tail, memory_order_relaxed);
+        } else {
+            pos = atomic_load_explicit(&c->tail, memory_order_relaxed);
+        }
+    }
 }
 
 static int chan_recv(chan_t *c, bstr *s) {
-    pthread_mutex_lock(&c->mu);
-    while (c->len == 0 && !c->closed) { c->wait_recv++; pthread_cond_wait(&c->not_empty, &c->mu); c->wait_recv--; }
-    if (c->len == 0) { pthread_mutex_unlock(&c->mu); return 0; }
-    *s = c->q[c->head]; c->head = (c->head + 1) % CHAN_CAP; c->len--;
-    if (c->wait_send) pthread_cond_signal(&c->not_full);
-    pthread_mutex_unlock(&c->mu);
+    unsigned spins = 0;
+    const size_t pos = atomic_load_explicit(&c->head, memory_order_relaxed);
+    chan_slot *sl = &c->q[pos & (CHAN_CAP - 1)];
+    for (;;) {
+        const size_t seq = atomic_load_explicit(&sl->seq, memory_order_acquire);
+        if (seq == pos + 1) break;
+        if (atomic_load_explicit(&c->closed, memory_order_acquire) &&
+            atomic_load_explicit(&sl->seq, memory_order_acquire) != pos + 1)
+            return 0;  /* closed after every sender finished: nothing left */
+        chan_backoff(&spins);
+    }
+    *s = sl->v;
+    atomic_store_explicit(&sl->seq, pos + CHAN_CAP, memory_order_release);
+    atomic_store_explicit(&c->head, pos + 1, memory_order_relaxed);
     return 1;
 }
 
@@ -714,13 +753,11 @@ static void *pipe_writer(void *arg) {
 A5O_EXPORT int a5o_run_pipeline(const a5o_table *t, const uint8_t *words, const uint64_t *off, size_t nw,
                                 int mode, int mn, int mx, int nthreads, int fd,
                                 uint64_t *out_cands, uint64_t *out_bytes) {
-    pipe_job *j = (pipe_job *)calloc(1, sizeof(pipe_job));
+    pipe_job *j = NULL;
+    if (posix_memalign((void **)&j, 64, sizeof(pipe_job))) return -1;
+    memset(j, 0, sizeof(pipe_job));
     j->t = t; j->words = words; j->off = off; j->nw = nw; j->mode = mode; j->mn = mn; j->mx = mx; j->fd = fd;
-    pthread_mutexattr_t ma;
-    pthread_mutexattr_init(&ma);
-    pthread_mutexattr_settype(&ma, PTHREAD_MUTEX_ADAPTIVE_NP);  /* spin, then park (like Go's runtime lock) */
-    pthread_mutex_init(&j->ch.mu, &ma);
-    pthread_mutexattr_destroy(&ma); pthread_cond_init(&j->ch.not_full, NULL); pthread_cond_init(&j->ch.not_empty, NULL);
+    chan_init(&j->ch);
     atomic_init(&j->next, 0); atomic_init(&j->err, 0);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
@@ -728,7 +765,7 @@ A5O_EXPORT int a5o_run_pipeline(const a5o_table *t, const uint8_t *words, const 
     pthread_create(&wr, NULL, pipe_writer, j);
     for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, pipe_worker, j);
     for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
-    pthread_mutex_lock(&j->ch.mu); j->ch.closed = 1; pthread_cond_broadcast(&j->ch.not_empty); pthread_mutex_unlock(&j->ch.mu);
+    atomic_store_explicit(&j->ch.closed, 1, memory_order_release);  /* close(out) after wg.Wait() */
     pthread_join(wr, NULL);
     *out_cands = j->out_cands; *out_bytes = j->out_bytes;
     int rc = atomic_load(&j->err);

@@ -152,3 +152,45 @@ def test_c5_shape_lookup_one_million_targets(algo):
         # zero false hits: a hit beyond the planted pairs is another occurrence of a planted
         # plain (the same candidate text from another word or position), never a random target
         assert all(hc[w][c] in plains for w, c in set(got) - set(planted))
+
+
+@pytest.mark.parametrize("mode,mn", [(2, 0), (3, 0), (3, 1), (2, 2)])
+def test_c5_shape_substitute_all_modes(mode, mn):
+    """-s / -s -r at the C5 shape (README.MD:159,163: greek-hebrew -s, -s -r -m 1):
+    100k Greek words (positional fast path: single-codepoint patterns, repeated
+    letters tie their occurrences) == C oracle per-word digests."""
+    from hashcat_a5_table_generator_amd import Context, synth
+    from oracle import c_oracle as co
+    _, (data, offs) = synth.global_words("c5", 0, 100_000, seed=0x55 + mode)
+    with Context(0) as ctx:
+        ctx.load_tables([table_path("greek-hebrew")])
+        tc, tb, got = _gpu_digest(ctx, data, offs, mode, mn, 15)
+    want = co.CTable([table_path("greek-hebrew")]).digest_batch(data, offs, mode, mn, 15, nthreads=NTH)
+    assert tc == int(want[:, 0].sum()) and tc > 10_000_000
+    _check(got, want, data, offs)
+
+
+def test_fused_md5_equals_two_pass():
+    """The fused MD5 path (k_expand_fast_md5: candidates hashed in the LDS ring) and the
+    two-pass path (HBM scratch + k_digest_stream) report the same hits."""
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
+    from oracle import digest_oracle as dg
+    _, (data, offs) = synth.global_words("c3", 0, 50_000, seed=0xF5)
+    n = len(offs) - 1
+    rng = np.random.default_rng(3)
+    with Context(0) as ctx:
+        ctx.load_tables([table_path("czech"), table_path("german")])
+        ws = sorted(set(int(x) for x in rng.choice(n, size=300, replace=False)))
+        cands = ctx.expand_words([bytes(data[int(offs[i]):int(offs[i + 1])]) for i in ws], 0, 0, 15)
+        tg = [dg.md5(cs[int(rng.integers(0, len(cs)))]) for cs in cands if cs]
+        ctx.set_targets(0, b"".join(tg) + bytes(rng.integers(0, 256, 16 * 20000, dtype=np.uint8)))
+        dw, do = DeviceBuffer.from_array(ctx, data), DeviceBuffer.from_array(ctx, offs)
+        fused, st = ctx.expand_digest_device(dw.ptr, do.ptr, n, 0, 0, 15, hit_cap=1 << 14)
+        os.environ["A5X_NO_FUSED_DIGEST"] = "1"
+        try:
+            two, st2 = ctx.expand_digest_device(dw.ptr, do.ptr, n, 0, 0, 15, hit_cap=1 << 14)
+        finally:
+            os.environ.pop("A5X_NO_FUSED_DIGEST")
+    assert st["candidates"] == st2["candidates"]
+    assert st["ms_total"] - st["ms_keyspace"] - st["ms_expand"] < 1e-3 < st2["ms_total"] - st2["ms_keyspace"] - st2["ms_expand"]
+    assert sorted(fused) == sorted(two) and len(fused) >= len(tg)

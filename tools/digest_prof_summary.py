@@ -11,6 +11,7 @@ sys.path.insert(0, ROOT)
 from bench import digest_src_sha  # noqa: E402
 
 algo, words = sys.argv[1], int(sys.argv[2])
+kname = sys.argv[3] if len(sys.argv) > 3 else "k_digest_stream"
 out = os.path.join(ROOT, "gpurun_out")
 
 
@@ -31,10 +32,10 @@ for line in open(os.path.join(out, "dpmc1_%s.log" % algo)):
         bench = json.loads(line)
 cands = bench["config"]["candidates_per_gpu_step"]
 stats = list(csv.DictReader(open(glob.glob(os.path.join(out, "dprof_" + algo, "run_kernel_stats.csv"))[0])))
-dig = next((r for r in stats if "k_digest_stream" in r["Name"]), None)
+dig = next((r for r in stats if kname in r["Name"]), None)
 valu = sum(c1.get("SQ_INSTS_VALU", [0]))
 res = {
-    "workload": "c5", "words": words, "algo": algo, "kernel": "k_digest_stream", "kernel_src_sha": digest_src_sha(),
+    "workload": "c5", "words": words, "algo": algo, "kernel": kname, "kernel_src_sha": digest_src_sha(),
     "candidates_per_step": cands,
     "valu_wave_insts_per_cand": valu / cands,
     "int_ops_per_cand": valu * 64 / cands,
@@ -42,10 +43,10 @@ res = {
     "valu_busy_pct": (sum(c2["VALUBusy"]) / len(c2["VALUBusy"])) if c2.get("VALUBusy") else None,
     "valu_utilization_pct": (sum(c2["VALUUtilization"]) / len(c2["VALUUtilization"])) if c2.get("VALUUtilization") else None,
     "active_valu_per_wave_cycle": sum(c1.get("SQ_ACTIVE_INST_VALU", [0])) / max(1.0, sum(c1.get("SQ_WAVE_CYCLES", [1]))),
-    "k_digest_stream_avg_us": float(dig["AverageNs"]) / 1e3 if dig else None,
-    "k_digest_stream_calls": int(dig["Calls"]) if dig else None,
+    "kernel_avg_us": float(dig["AverageNs"]) / 1e3 if dig else None,
+    "kernel_calls": int(dig["Calls"]) if dig else None,
     "note": "SQ_INSTS_VALU summed over the k_digest_stream dispatches of one step (1 step, 0 warmup; the "
             "planted-target setup adds ~1e6 candidates); int_ops = wave instructions x 64 lanes",
 }
-json.dump(res, open(os.path.join(out, "pmc_digest_%s_c5.json" % algo), "w"), indent=1)
+json.dump(res, open(os.path.join(out, "pmc_digest_%s_%s_c5.json" % (algo, kname)), "w"), indent=1)
 print(json.dumps(res))
