@@ -1379,6 +1379,8 @@ int a5x_set_targets(a5x_ctx* c, int algo, const uint8_t* dig, uint64_t n) {
   // prefilter: >= 64 bits per target (false-positive rate <= 1/64), table: load <= 1/2
   uint32_t bm_log2 = 16;
   while (bm_log2 < 32 && (1ull << bm_log2) < n * 64) bm_log2++;
+  // (test hook: force the prefilter size, e.g. the 2^32-bit filter of > 2^26 targets)
+  if (const char* e = getenv("A5X_TARGET_BM_LOG2")) bm_log2 = std::max(16u, std::min(32u, (uint32_t)atoi(e)));
   uint64_t tsz = 16;
   while (tsz < 2 * n) tsz <<= 1;
   std::vector<uint32_t> bm((1ull << bm_log2) / 32, 0);

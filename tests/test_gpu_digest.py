@@ -107,3 +107,47 @@ def test_lookup_small_scratch_ranges(gpu_ctx):
     tg = {dg.md5(per_word[w][c]) for w, c in pl}
     want = sorted((w, c) for w, cs in enumerate(per_word) for c, x in enumerate(cs) if dg.md5(x) in tg)
     assert sorted((w, c) for w, c, _ in hits) == want  # every candidate with a target digest, once
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_digest_long_candidates_cross_block_edges(gpu_ctx, algo):
+    """250-300 B candidates (BIG-path words) whose lines straddle the digest stream's
+    4 KiB / 2 KiB block edges at many offsets: the line must be hashed from staged bytes
+    only (in_lds = e <= sl), bit-exact vs hashlib / RFC 1320 MD4."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer, pack_words
+    from oracle import digest_oracle as dg
+    gpu_ctx.clear_table()
+    gpu_ctx.load_tables([table_path("czech")])
+    rng = np.random.default_rng(11 + algo)
+    top = 300 if algo == 0 else 60  # NTLM device limit: 64 UTF-16 units
+    words = [b"1" * int(rng.integers(top - 50, top)) + b"a" for _ in range(200 if algo == 0 else 600)]
+    data, offs = pack_words(words)
+    dw, do = DeviceBuffer.from_array(gpu_ctx, data), DeviceBuffer.from_array(gpu_ctx, offs)
+    tc, tb = gpu_ctx.keyspace_device(dw.ptr, do.ptr, len(words))
+    out = DeviceBuffer(gpu_ctx, tb + 64)
+    gpu_ctx.expand_device(dw.ptr, do.ptr, len(words), out.ptr, tb)
+    lines = bytes(out.to_array(count=tb)).split(b"\n")[:-1]
+    assert len(lines) == tc and tb > 3 * (4096 if algo == 0 else 2048)  # several stream blocks
+    dig = DeviceBuffer(gpu_ctx, 16 * tc + 16)
+    assert gpu_ctx.digest_lines_device(algo, out.ptr, tb, dig.ptr, tc) == tc
+    got = dig.to_array(count=16 * tc).reshape(tc, 16)
+    f = dg.ALGOS[algo]
+    bad = [i for i, ln in enumerate(lines) if bytes(got[i]) != f(ln)]
+    assert not bad, [(len(lines[i]), bytes(got[i]).hex()) for i in bad[:5]]
+
+
+def test_lookup_with_a_full_32_bit_prefilter(gpu_ctx, monkeypatch):
+    """A 2^32-bit prefilter (what > 2^26 targets get): the device mask must be
+    0xffffffff, not (1 << 32) - 1 = 0.  Forced with the sizing test hook."""
+    from hashcat_a5_table_generator_amd import pack_words
+    from oracle import digest_oracle as dg
+    monkeypatch.setenv("A5X_TARGET_BM_LOG2", "32")
+    gpu_ctx.clear_table()
+    gpu_ctx.load_tables([table_path("czech"), table_path("german")])
+    words = _words(77, 400)
+    per_word = gpu_ctx.expand_words(words, 0, 0, 15)
+    pl = [(w, len(per_word[w]) // 2) for w in range(0, 400, 13) if per_word[w]]
+    gpu_ctx.set_targets(0, b"".join(dg.md5(per_word[w][c]) for w, c in pl))
+    hits, _ = gpu_ctx.expand_digest(*pack_words(words), 0, 0, 15)
+    got = {(w, c) for w, c, _ in hits}
+    assert set(pl) <= got

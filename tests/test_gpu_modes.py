@@ -180,3 +180,19 @@ def test_mode_ranges_concatenate(gpu_ctx, mode):
     want = _c_oracle(["czech", "german"], words, mode, 0, 15)
     lines = bytes(ref).split(b"\n")[:-1]
     assert sorted(lines) == sorted(x for ws in want for x in ws)
+
+
+def test_reverse_negative_min_window():
+    """-r with min < 0: generateCombinations(n, k < 0) recurses forever whenever the
+    subCount loop runs (min(max, n) >= min, main.go:238, 263-281) -- the reference dies;
+    with max < min the loop never runs and the output is empty."""
+    from hashcat_a5_table_generator_amd import A5xError, pack_words
+    c = _ctx(["qwerty-azerty"])
+    data, offs = pack_words([b"abc", b"qwerty"])
+    for mn, mx in [(-3, -2), (-1, 15), (-2, -2)]:
+        with pytest.raises(A5xError) as e:
+            c.keyspace(data, offs, 1, mn, mx)
+        assert "BOUNDS" in str(e.value), (mn, mx)
+    cnt, byt = c.keyspace(data, offs, 1, -3, -4)
+    assert int(cnt.sum()) == 0 and int(byt.sum()) == 0
+    c.close()
