@@ -1236,6 +1236,12 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 // window records: ring bytes [16, FX_RING) during the setup; the last u64 is the zero slot
 #define FX_RZ ((FX_RING - 16) / 8 - 1)
 #define FX_K 4        // candidates per lane run (a5x_fx6.h)
+#ifndef FX_SPEC
+#define FX_SPEC 0     // speculative next-window records with the metadata loads (A/B: no gain)
+#endif
+#ifndef FX_SPEC_N
+#define FX_SPEC_N 2   // ... KiB of them (uint4 per lane)
+#endif
 #ifndef FX_ABL
 #define FX_ABL 0      // timing ablations (variant builds only; output is garbage when set):
                       // 4 no global stores, 8 no rounds, 16 no big entries, 32 no prefix,
@@ -1569,6 +1575,14 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
   typename std::conditional<DIG, FxDigest, FxFlush>::type fl;
   fl.ring = ring; fl.a = &a; fl.wbase = 0;
   FxMeta M = fx_meta(a, w);
+#if FX_SPEC
+  // speculative records of the next window, loaded together with its metadata (records
+  // of consecutive windows are contiguous inside a keyspace tile): one global round trip
+  // per window setup instead of metadata -> records.  Live only between windows.
+  u64 spb = ~0ull;  // sp holds record u64 [spb, spb + 128 nsp) (spb even)
+  u32 nsp = 2;      // 1 KiB per step, sized from the last window's records
+  uint4 sp[FX_SPEC_N];
+#endif
   STAMP_DECL
   while (g < g1) {
     if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
@@ -1608,6 +1622,20 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     const u32 jf = (u32)__builtin_ctzll(fm);
     const u64 src0 = (u64)readlane_u32(M.roff, jf);
     const u32 ntot = readlane_u32(incR, k - 1);
+#if FX_SPEC
+    if (spb <= src0 && src0 + ntot <= spb + 128ull * nsp) {
+      const u32 d = (u32)(src0 - spb);  // speculated u64 i lands at rec[i - d]
+#pragma unroll
+      for (u32 q = 0; q < FX_SPEC_N; q++) {
+        if (q < nsp) {
+          const u32 i0 = 2 * (lane + 64 * q);
+          // (only the window's ntot: the OR rounds need the rest of the ring zero)
+          if (i0 >= d && i0 - d < ntot) rec[i0 - d] = ((u64)sp[q].y << 32) | sp[q].x;
+          if (i0 + 1 >= d && i0 + 1 - d < ntot) rec[i0 + 1 - d] = ((u64)sp[q].w << 32) | sp[q].z;
+        }
+      }
+    } else
+#endif
     {
       const u64* s64 = a.rec + src0;
       if ((src0 & 1) == 0) {
@@ -1733,6 +1761,18 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     g = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     w += k;
     M = fx_meta(a, w);
+#if FX_SPEC
+    {
+      // next records: right after this window's, or the start of the next tile's region
+      const u64 nx = (w % FW_TILE == 0) ? (w / FW_TILE) * (u64)FW_TILE_REC : src0 + ntot;
+      nsp = min((u32)FX_SPEC_N, (ntot + 2u * 128u - 1u) / 128u);  // this window's size + 1 KiB
+      spb = nx & ~1ull;
+      const uint4* src = (const uint4*)(a.rec + spb);
+#pragma unroll
+      for (u32 q = 0; q < FX_SPEC_N; q++)
+        if (q < nsp) sp[q] = spb + 2ull * (lane + 64 * q) + 2 <= a.rec_n ? src[lane + 64 * q] : make_uint4(0, 0, 0, 0);
+    }
+#endif
     WAVE_SYNC();
   }
   if (!DIG) fx_close(R, ring, a);
