@@ -1552,6 +1552,84 @@ __device__ __forceinline__ uint4 fx_entry(const u64* rec, u32 d0, u32 wbe, u32 s
   return make_uint4((u32)lo64, (u32)(lo64 >> 32), (u32)hi64, ((u32)(hi64 >> 32) & 0xFFFFFFu) | (off << 24));
 }
 
+#ifndef FX_DIRECT
+#define FX_DIRECT 0   // single-big-piece word runs built and placed without an entry table (A/B: neutral)
+#endif
+
+// Direct window (see expand_chunk_fast): words [0, k) of the window, each with at most
+// one big piece; rs = the word's record size (0: no candidates), rb = its record base
+// in rec (ring bytes 16.., moved here to the entry table's space first), ranks inside
+// [g, g1).  Passes of 64 candidates (one per lane): fx_entry -> DPP scan -> OR
+// placement; the ring is flushed when less than 1 KiB is left (FxDigest: every pass).
+template <class FL>
+__device__ __forceinline__ void fx_direct_window(FXWin& F, u32* ring, const u64* rec, const ExpArgs& a, FxRun& R,
+                                                 FL& fl, u32 rs, u32 rb, u32 k, u32 ntot, u64 g, u64 g1, u64 c0, u64 c1,
+                                                 u64 bo, u64 w) {
+  const u32 lane = lane_id();
+  u64* const rc = (u64*)F.be;  // the records, moved out of the ring
+  for (u32 i = lane; i < (ntot + 1) / 2; i += 64) ((uint4*)rc)[i] = ((const uint4*)rec)[i];
+  if (lane == 0) rc[FX_RZ] = 0;
+  const u64 wc0 = uniform64(c0);
+  if (!FL::DIGEST) {  // run position of g
+    const u64 r0 = g - wc0;
+    u64 pos = uniform64(bo) - a.out_base;
+    if (r0) pos += fast_prefix_bytes(rec + readlane_u32(rb, 0), r0);
+    if (!R.open || R.pos != pos) {
+      fx_close(R, ring, a);
+      R.B = pos & ~15ull; R.lo = pos; R.pos = pos; R.carry = 0; R.open = true;
+    }
+  }
+  WAVE_SYNC();
+  for (u32 i = 1 + lane; i <= (ntot + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);  // OR ring
+  const u32 rbw = lane == 0 ? (u32)(g - wc0) : 0u;
+  const u32 ncw = rs ? (u32)(min(c1, g1) - c0) - rbw : 0u;  // the word's candidates in [g, g1)
+  const u32 incN = wave_incl_scan_u32(lane < k ? ncw : 0u);
+  const u32 tot = readlane_u32(incN, k - 1);
+  const u32 est = lane < k ? incN - ncw : 0xffffffffu;
+  const u32 ringa = fx6_addr(ring), cap = FX_RING - 32u;
+  WAVE_SYNC();
+  u32 jb = 0;
+  for (u32 t0 = 0; t0 < tot; t0 += 64) {
+    if (!FL::DIGEST && (u32)(R.pos - R.B) + 64u * 16u > cap) fl(R);  // room for a pass
+    const u32 t = t0 + lane;
+    u32 j = jb;
+    for (;;) {
+      const u32 jn = uniform(jb + 1);
+      if (jn >= k) break;
+      const u32 sj = uniform(readlane_u32(est, jn));
+      if (sj >= t0 + 64) break;
+      jb = jn;
+      j += (t >= sj) ? 1u : 0u;
+    }
+    const u32 wrb = (u32)__shfl((int)rb, (int)j);
+    const u32 rank = t - (u32)__shfl((int)est, (int)j) + (u32)__shfl((int)rbw, (int)j);
+    const bool on = t < tot;
+    const u64 h = rc[on ? wrb : (u32)FX_RZ];
+    const u32 np = frh_np(h);
+    const u32 span = on ? np : 0u;  // the one big piece spans every small piece
+    const uint4 e = fx_entry(rc, wrb + 1u, wrb + 1u + np, span, wave_max_u32(span), rank + 1u);
+    const u32 len = on ? e.w >> 24 : 0u;
+    const u32 incl = wave_incl_scan_u32(len);
+    const u32 used = (u32)(R.pos - R.B);
+    u32 P = ringa + used + incl - len, sink = 0;
+    if (on) fx7_put(e, P, sink);
+    R.pos = uniform64(R.pos + readlane_u32(incl, 63));
+    WAVE_SYNC();
+    if constexpr (FL::DIGEST) {
+      FxLaneRun lr;
+      lr.off = used + incl - len;
+      lr.nc = on ? 1u : 0u;
+      lr.j = j;
+      lr.st = rank;
+      lr.clen[0] = len; lr.clen[1] = 0; lr.clen[2] = 0; lr.clen[3] = 0;
+      fl.digest(lr);
+      fl(R);
+    }
+  }
+  if (!FL::DIGEST) fl(R);  // the next window stages its records in ring bytes 16..
+  (void)w;
+}
+
 template <bool DIG>
 __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
@@ -1661,6 +1739,22 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
       R2 = frh_R(hdr, 2);
       R3 = frh_R(hdr, 3);
     }
+#if FX_DIRECT
+    // ---- a run of single-big-piece words: every candidate IS one big entry, so it is
+    // built (fx_entry) and placed straight away -- no entry table, and the window is
+    // limited by its records, not by 255 entries ----
+    if (!(__ballot(lane < k && rs > 0 && nbw >= 2) & 1ull)) {
+      const u64 m2w = __ballot(lane < k && rs > 0 && nbw >= 2);
+      if (m2w) k = (u32)__builtin_ctzll(m2w);
+      fl.wbase = w;
+      fx_direct_window(F, ring, rec, a, R, fl, lane < k ? rs : 0u, rb, k, ntot, g, g1, c0, c1, M.bo, w);
+      g = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
+      w += k;
+      M = fx_meta(a, w);
+      WAVE_SYNC();
+      continue;
+    }
+#endif
     const u32 E = R0 + R1 + R2 + R3 - (FB_NMAX - nbw);  // fb_R = 1 past the last big piece
     const u32 incE = wave_incl_scan_u32(E);
     const u64 over = __ballot(lane < k && incE > FX_ZBE);

@@ -364,6 +364,10 @@ struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
   A5X_HD void desc(u32 i, u64 v) { rec[1 + i] = v; }
 };
 
+#ifndef PL_FIXED_TRIP
+#define PL_FIXED_TRIP 0  // 1: CAP-iteration entry loops for every group (A/B)
+#endif
+
 // Cut a unit-radix word into pieces (see the record format above), one unit at a
 // time (unit() in word order, then finish()).  BUILD: also write the entries and
 // piece descriptors through the sink (the header is the caller's: fr_hdr of P).
@@ -400,7 +404,7 @@ struct Planner {
   }
   A5X_HD void close_group() {
     if constexpr (BUILD) {
-      for (u32 a = 0; a < CAP; a++)
+      for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : cR); a++)
         if (a < cR) sk.ent(P.ne + a, sk.gld(a));
       sk.desc(cpi, fr_desc(cR, P.ne));
     }
@@ -439,7 +443,7 @@ struct Planner {
       if constexpr (BUILD) {
         const u64 rb = run ? wd.ld(prev, run) : 0ull;
         const u32 inv = (256u + cR - 1u) / cR;  // t / cR = (t * inv) >> 8 for t < 16
-        for (int t = CAP - 1; t >= 0; t--) {
+        for (int t = (PL_FIXED_TRIP ? CAP : nR) - 1; t >= 0; t--) {
           if ((u32)t >= nR) continue;
           const u32 a2 = ((u32)t * inv) >> 8, a1 = (u32)t - a2 * cR;
           u32 cl = 0;
@@ -463,7 +467,7 @@ struct Planner {
       P.np++;
       if constexpr (BUILD) {
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
-        for (u32 a = 0; a < CAP; a++) {
+        for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : Ru); a++) {
           if (a >= Ru) continue;
           u32 cl = 0;
           const u64 cv = unit_choice_b(wd, U, T, a, cl, cb, cs);
@@ -480,7 +484,7 @@ struct Planner {
     if (open && cmax + tl <= FW_PLEN) {
       if constexpr (BUILD) {
         const u64 tb = (run ? wd.ld(prev, run) : 0ull) | (10ull << (8 * run));
-        for (u32 a = 0; a < CAP; a++) {
+        for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : cR); a++) {
           if (a >= cR) continue;
           const u64 old = sk.gld(a);
           const u32 ol = fw_len(old);
