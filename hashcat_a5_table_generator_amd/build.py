@@ -20,7 +20,7 @@ CLI = os.path.join(OUT, "a5x_generator")
 ARCH = os.environ.get("A5X_OFFLOAD_ARCH", "gfx950")
 
 LIB_SRCS = ["a5x_kernels.hip", "a5x_modes.hip", "a5x_digest.hip", "a5x_host.cpp"]
-HEADERS = ["a5x_format.h", "a5x_gosem.h", "a5x_launch.h", "a5x_plan.h"]
+HEADERS = ["a5x_format.h", "a5x_gosem.h", "a5x_launch.h", "a5x_plan.h", "a5x_fx6.h", "a5x_ring.h", "a5x_md.h"]
 
 
 def _hipcc() -> str:

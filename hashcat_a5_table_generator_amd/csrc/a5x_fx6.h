@@ -19,6 +19,9 @@
 //   flush   complete 16-B ring blocks -> global_store_dwordx4 (1 KiB per instruction).
 #pragma once
 
+#ifndef FX_HOLDNB
+#define FX_HOLDNB 2      // rounds of <= this many big pieces keep their entries in registers
+#endif
 #ifndef FX6_ZBE
 #define FX6_ZBE 255      // the window entry that holds the empty piece (set by the includer)
 #endif
@@ -117,7 +120,7 @@ __device__ __forceinline__ u32 fx6_round(const uint4* be, const uint4 (*wq)[2], 
   fx6_digits<NB>(st + 1u, q0, q1.x, d);
   // pass 1: entry indices and lengths; <= 2 pieces: the entries stay in registers,
   // else (register budget) pass 2 reads them again
-  constexpr bool HOLD = NB <= 2;
+  constexpr bool HOLD = NB <= FX_HOLDNB;
   uint4 ent[HOLD ? K : 1][HOLD ? NB : 1];
   u32 idx[HOLD ? 1 : K][HOLD ? 1 : NB];
   u32 len = 0;
@@ -195,9 +198,11 @@ struct FxLaneRun {
   u32 clen[4];
 };
 
+// nsm: fx8_put slot counts of big pieces 0-3 (4 bits each, wave-uniform)
 template <int NB, int K, bool NOOR = false, class FLUSH>
 __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
-                                         u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush, FxLaneRun& lr) {
+                                         u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush, FxLaneRun& lr,
+                                         u32 nsm) {
   static_assert(K <= 4, "FxLaneRun holds 4 candidates");
   const u32 lane = lane_id();
   const uint4 q0 = wq[j][0], q1 = wq[j][1];
@@ -206,7 +211,7 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
   const u32 nc = cw > st ? min((u32)K, cw - st) : 0u;
   u32 d[4];
   fx6_digits<NB>(st + 1u, q0, q1.x, d);
-  constexpr bool HOLD = NB <= 2;
+  constexpr bool HOLD = NB <= FX_HOLDNB;
   uint4 ent[HOLD ? K : 1][HOLD ? NB : 1];
   u32 idx[HOLD ? 1 : K][HOLD ? 1 : NB];
   u32 len = 0, clen[K];
@@ -235,6 +240,23 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
   const u32 tot = nact ? readlane_u32(incl, nact - 1u) : 0u;
   u32 P = ring + used + incl - len, sink = 0;
   if (fit) {
+#if FX_AB
+    if constexpr (!NOOR) {
+      u32 P1 = P - 1u;
+      asm volatile("" : "+s"(nsm));  // slot tests stay scalar branches here (not hoisted lane masks)
+#pragma unroll
+      for (int c = 0; c < K; c++) {
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+          uint4 e;
+          if constexpr (HOLD) e = ent[c][b];
+          else e = be[idx[c][b]];
+          fx8_put(e, P1, (nsm >> (4 * b)) & 15u);
+        }
+      }
+    } else
+#endif
+    {
 #pragma unroll
     for (int c = 0; c < K; c++) {
 #pragma unroll
@@ -245,7 +267,9 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
         fx7_put<NOOR>(e, P, sink);
       }
     }
+    }
   }
+  (void)nsm;
   if constexpr (NOOR) {
     if (sink == 0x9E3779B9u) fx7_or(ring, 1u);  // keeps the folded dwords live
   }

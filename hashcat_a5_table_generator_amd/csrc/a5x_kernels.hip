@@ -1236,6 +1236,9 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 // window records: ring bytes [16, FX_RING) during the setup; the last u64 is the zero slot
 #define FX_RZ ((FX_RING - 16) / 8 - 1)
 #define FX_K 4        // candidates per lane run (a5x_fx6.h)
+#ifndef FX_PFM
+#define FX_PFM 1      // next window's metadata loaded before the current window's rounds
+#endif
 #ifndef FX_SPEC
 #define FX_SPEC 0     // speculative next-window records with the metadata loads (A/B: no gain)
 #endif
@@ -1249,6 +1252,9 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #endif
 #ifndef FX_NOOR
 #define FX_OR         // OR placement into a zeroed ring (a5x_fx6.h fx7_round)
+#endif
+#ifndef FX_AB
+#define FX_AB 0       // 1: fx8_put (alignbyte shifts, per-window scalar slot counts; A/B: 1 % slower)
 #endif
 
 // The window's small-piece records live in the ring (from byte 16) during the window
@@ -1484,9 +1490,9 @@ struct FxDigest {
 // with >= 2 / 3 / 4 big pieces).
 template <int K, class FL>
 __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FL& fl, u32 T, u32 k, u32 rw, u64 m2,
-                                          u64 m3, u64 m4) {
+                                          u64 m3, u64 m4, u32 nsm) {
   const u32 lane = lane_id();
-  const u32 ringa = fx6_addr(ring), trash = ringa + FX_RING + 4u * lane;
+  const u32 ringa = fx6_addr(ring), trash = ringa - FX_TRASH + 4u * lane;
   const u32 cap = FX_RING - 32u;
   u32 jcur = 0;
   for (u32 rr = 0; rr < T;) {
@@ -1501,16 +1507,16 @@ __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FL& fl,
     (void)trash;
 #if FX_ABL & 64
     if (true) {
-      if (span & m4) took = fx7_round<4, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
-      else if (span & m3) took = fx7_round<3, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
-      else if (span & m2) took = fx7_round<2, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
-      else took = fx7_round<1, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+      if (span & m4) took = fx7_round<4, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
+      else if (span & m3) took = fx7_round<3, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
+      else if (span & m2) took = fx7_round<2, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
+      else took = fx7_round<1, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
     } else
 #endif
-    if (span & m4) took = fx7_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
-    else if (span & m3) took = fx7_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
-    else if (span & m2) took = fx7_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
-    else took = fx7_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+    if (span & m4) took = fx7_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
+    else if (span & m3) took = fx7_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
+    else if (span & m2) took = fx7_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
+    else took = fx7_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
 #else
     if (span & m4) took = fx6_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
     else if (span & m3) took = fx6_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
@@ -1788,6 +1794,7 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     WAVE_SYNC();
     STAMP(5);
     // ---- build the big entries: lanes over the window's entries ----
+    u32 thr = 0;  // bit 5 b + ceil(len / 4): the entry lengths of big piece b (fx8_slots)
     if (!(FX_ABL & 16))
     {
       const u32 etot = readlane_u32(incE, k - 1);
@@ -1823,7 +1830,17 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
         const u32 span = on ? sp1 - sp0 : 0u;
         const uint4 e = fx_entry(rec, wrb + 1u + sp0, wrb + 1u + np, span, wave_max_u32(span), u - cb);
         if (on) F.be[t] = e;
+        thr |= on ? (1u << ((((e.w >> 24) + 3u) >> 2) + 5u * b)) : 0u;
       }
+    }
+    // slot counts of the window's big pieces (wave-uniform)
+    const u32 thm = uniform(wave_or_u32(thr));
+    u32 nsm = 0;
+#pragma unroll
+    for (u32 b = 0; b < 4; b++) {
+      const u32 f = (thm >> (5u * b)) & 31u;
+      const u32 hb = f ? 31u - (u32)__builtin_clz(f) : 0u;  // ceil(lmax / 4)
+      nsm |= (hb <= 1u ? 2u : 1u + hb) << (4u * b);
     }
     WAVE_SYNC();
     STAMP(1);
@@ -1845,16 +1862,27 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     WAVE_SYNC();
 #endif
     STAMP(2);
+#if FX_PFM
+    // the next window's metadata, loaded under this window's rounds (the window's own
+    // metadata registers are dead from here on)
+    const u64 gnext = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
+    M = fx_meta(a, w + k);
+#endif
     // ---- rounds ----
     if (!(FX_ABL & 8))
     {
-      if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4);
-      else fx_rounds<1>(F, ring, R, fl, T, k, rw, m2, m3, m4);
+      if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4, nsm);
+      else fx_rounds<1>(F, ring, R, fl, T, k, rw, m2, m3, m4, nsm);
     }
     STAMP(3);
+#if FX_PFM
+    g = gnext;
+    w += k;
+#else
     g = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     w += k;
     M = fx_meta(a, w);
+#endif
 #if FX_SPEC
     {
       // next records: right after this window's, or the start of the next tile's region
@@ -1884,8 +1912,8 @@ __device__ __forceinline__ void expand_fast_body(const ExpArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   uint8_t* mine = smem + wv * lds_per_wave_fast();
-  u32* ring = (u32*)mine;
-  FXWin& F = *(FXWin*)(mine + FX_RING + FX_TRASH);
+  u32* ring = (u32*)(mine + FX_TRASH);  // (fx8_put: 4 writable bytes in front of the ring)
+  FXWin& F = *(FXWin*)(mine + FX_TRASH + FX_RING);
   const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
   if (chunk * a.CH >= a.cand_end) return;
   expand_chunk_fast<DIG>(F, ring, a, chunk);

@@ -54,3 +54,29 @@ __device__ __forceinline__ void fx7_put(const uint4 e, uint32_t& P, uint32_t& si
   P += l;
 }
 
+// fx8_put: fx7_put with v_alignbyte shifts and the dword count decided per window.
+// P1 = (LDS byte address of the piece) - 1, so that base = P1 & ~3 and the alignbyte
+// shift (~P1) & 3 = (4 - n) & 3 need no selector build; for n = P & 3 = 0 the five
+// slots cover [P - 4, P + 16) (slot 0 ORs zero into the dword before P: the ring
+// therefore needs 4 writable bytes in front of it).  Slot k >= 2 is written when
+// ns > k (ns: wave-uniform, from the longest entry of the piece over the window,
+// so the compare is scalar); slots past a piece's bytes receive zeros.  The entry's
+// byte 15 (its length) never reaches slots 0-3; slot 4 masks it.
+__device__ __forceinline__ void fx8_put(const uint4 e, uint32_t& P1, uint32_t ns) {
+  const uint32_t base = P1 & ~3u, s = ~P1;
+  fx7_or(base, __builtin_amdgcn_alignbyte(e.x, 0u, s));
+  fx7_or(base + 4u, __builtin_amdgcn_alignbyte(e.y, e.x, s));
+  if (ns > 2u) {
+    fx7_or(base + 8u, __builtin_amdgcn_alignbyte(e.z, e.y, s));
+    if (ns > 3u) {
+      fx7_or(base + 12u, __builtin_amdgcn_alignbyte(e.w, e.z, s));
+      if (ns > 4u) fx7_or(base + 16u, __builtin_amdgcn_alignbyte(0u, e.w & 0xFFFFFFu, s));
+    }
+  }
+  P1 += e.w >> 24;
+}
+
+// slots fx8_put needs for a piece whose longest entry has lmax bytes (n + lmax <= 4 ns
+// for every n in [1, 4]: ns = 1 + ceil(lmax / 4), at least 2)
+__device__ __forceinline__ uint32_t fx8_slots(uint32_t lmax) { return lmax <= 4u ? 2u : 1u + ((lmax + 3u) >> 2); }
+
