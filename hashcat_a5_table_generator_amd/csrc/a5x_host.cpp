@@ -121,6 +121,10 @@ struct a5x_ctx {
   DevBuf<uint64_t> loc_q, loc_r;  // range-boundary queries / results (job_locate)
 
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // side stream: the per-word kernels (k_expand_slow / k_expand_b) of a range run beside
+  // k_expand_fast (disjoint output bytes), joined back before the range completes
+  hipStream_t sstream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint64_t seg = 1024;        // candidates per per-word-path segment (a radix round there costs ~64x a FAST one)
   uint64_t chunk = 8192;      // candidates per expand wave (sweep on C3: 8192 < 16384 < 32768 ms)
   uint32_t waves_per_block = 4;
@@ -827,14 +831,27 @@ int job_launch(a5x_ctx* c, const Job& J, const Range& R, uint8_t* d_out, uint64_
   if (B.nbig)
     HIPCHK(c, a5x_launch_segments(c->big_list.p, c->d_scalars + 1, B.nbig, B.cand_off, R.cb, R.ce, c->seg,
                                   c->segs.p + sbound, c->d_scalars + 6, J.st));
-  HIPCHK(c, a5x_launch_expand(E, 0, J.st));
+  hipStream_t side = J.st;
+  if (B.nslow || B.nbig) {
+    if (!c->sstream) HIPCHK(c, hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking));
+    if (!c->ev_fork) HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    if (!c->ev_join) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_fork, J.st));
+    HIPCHK(c, hipStreamWaitEvent(c->sstream, c->ev_fork, 0));
+    side = c->sstream;
+  }
   if (B.nslow) {
     E.segs = c->segs.p; E.nsegs = c->d_scalars + 5; E.nsegs_bound = sbound;
-    HIPCHK(c, a5x_launch_expand(E, 1, J.st));
+    HIPCHK(c, a5x_launch_expand(E, 1, side));
   }
   if (B.nbig) {
     E.segs = c->segs.p + sbound; E.nsegs = c->d_scalars + 6; E.nsegs_bound = bbound;
-    HIPCHK(c, a5x_launch_expand(E, 2, J.st));
+    HIPCHK(c, a5x_launch_expand(E, 2, side));
+  }
+  HIPCHK(c, a5x_launch_expand(E, 0, J.st));
+  if (side != J.st) {
+    HIPCHK(c, hipEventRecord(c->ev_join, side));
+    HIPCHK(c, hipStreamWaitEvent(J.st, c->ev_join, 0));
   }
   return A5X_OK;
 }
@@ -959,6 +976,10 @@ void a5x_destroy(a5x_ctx* c) {
   for (auto& e : c->ev_cpy)
     if (e) (void)hipEventDestroy(e);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  if (c->sstream) (void)hipStreamSynchronize(c->sstream);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->sstream) (void)hipStreamDestroy(c->sstream);
   if (c->d_table) (void)hipFree(c->d_table);
   if (c->d_scalars) (void)hipFree(c->d_scalars);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);

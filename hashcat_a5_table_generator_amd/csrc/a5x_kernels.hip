@@ -440,6 +440,8 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
   }
 }
 
+#define KC_SLOT 48  // k_keyspace_cplx: per-lane LDS word slot (words <= KC_SLOT - 12 bytes)
+
 // The complex words of k_keyspace_thread (overlapping keys, long keys, oversize
 // tiles), one lane per listed word: the general unit walk (next_unit) on global
 // bytes; FAST records go to fixed slots after the tile regions.
@@ -450,23 +452,42 @@ __global__ void __launch_bounds__(256) k_keyspace_cplx(KsArgs a) {
   load_table(smem, a.table, a.table_bytes);
   __syncthreads();
   const Tab T = tab_view(smem);
+  uint8_t* wst = (uint8_t*)(gbuf + 2 * 256 * FW_UMAXR);  // KC_SLOT bytes per lane
   const u32 n = *a.cplx_n;
   for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const u64 w = a.cplx_list[i];
     const u64 s = a.woff[w], L64 = a.woff[w + 1] - s;
-    GWord gw;
-    gw.p = a.words + s;
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
-    u32 f = ks_classify(gw, L64, T, a, C);
-    if ((f & A5X_WF_FAST) && C.count > 0) {
-      if (i < a.cplx_cap) {
-        u64* rec = a.rec + a.cplx_base + (u64)i * FW_RMAX;
-        ks_build(gw, (u32)L64, T, a, f, rec, gbuf + threadIdx.x);
-        a.roff[w] = (u32)(a.cplx_base + (u64)i * FW_RMAX);
-      } else {
-        f = C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
+    u32 f;
+    u64* const rec = a.rec + a.cplx_base + (u64)i * FW_RMAX;
+    const bool fits = i < a.cplx_cap;
+    if (L64 + 12 <= KC_SLOT) {
+      // the word in this lane's LDS slot (all byte loads in flight together): the unit
+      // walks below re-read every byte many times
+      const uint8_t* gp = a.words + s;
+      u32* sl = (u32*)(wst + threadIdx.x * KC_SLOT);
+#pragma unroll
+      for (u32 q = 0; q < KC_SLOT / 4; q++) {
+        u32 v = 0;
+#pragma unroll
+        for (u32 b = 0; b < 4; b++)
+          if (4 * q + b < L64) v |= (u32)gp[4 * q + b] << (8 * b);
+        sl[q] = v;
       }
+      LWord lw;
+      lw.base = wst; lw.off = threadIdx.x * KC_SLOT;
+      f = ks_classify(lw, L64, T, a, C);
+      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(lw, (u32)L64, T, a, f, rec, gbuf + threadIdx.x);
+    } else {
+      GWord gw;
+      gw.p = a.words + s;
+      f = ks_classify(gw, L64, T, a, C);
+      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(gw, (u32)L64, T, a, f, rec, gbuf + threadIdx.x);
+    }
+    if ((f & A5X_WF_FAST) && C.count > 0) {
+      if (fits) a.roff[w] = (u32)(a.cplx_base + (u64)i * FW_RMAX);
+      else f = C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
     }
     if (f & A5X_WF_DEFER) a.defer_list[atomicAdd(a.defer_n, 1u)] = (u32)w;
     else if (!(f & (A5X_WF_FAST | A5X_WF_ERR_OVF))) a.slow_list[atomicAdd(a.nslow, 1u)] = (u32)w;
@@ -2067,7 +2088,8 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_keyspace_cplx, dim3(L.defer_blocks), dim3(256), ((L.table_bytes + 15u) & ~15u) + 2 * 256 * FW_UMAXR * 8, st, a);
+  hipLaunchKernelGGL(k_keyspace_cplx, dim3(L.defer_blocks), dim3(256),
+                     ((L.table_bytes + 15u) & ~15u) + 2 * 256 * FW_UMAXR * 8 + 256 * KC_SLOT, st, a);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t lds = ((L.table_bytes + 15u) & ~15u) + sizeof(LdsB);
