@@ -67,6 +67,7 @@ enum : uint32_t {
   A5X_WF_BIG = 1u << 3,     // does not fit the pass-A wave budget: pass B
   A5X_WF_DEFER = 1u << 4,   // keyspace needs the wave-level DP kernel
   A5X_WF_FAST = 1u << 5,    // radix, <= 64 B, piece plan fits (plan_word): k_expand_fast
+  A5X_WF_GLOB = 1u << 6,    // (with BIG) beyond the pass-B LDS budget: pass G, global scratch
   A5X_WF_ERR_OVF = 1u << 8, // count/bytes overflow u64
   A5X_WF_ERR_BIG = 1u << 9, // exceeds pass-B limits
 };
@@ -84,6 +85,13 @@ enum : uint32_t {
 #define A5X_DPENT_B 4096
 #define A5X_MLMAX_B 4096
 #define A5X_RING_B 16384
+// pass G: one wave per scratch slot in HBM (WaveLds + ring), for words beyond pass B --
+// any line the reference reads (bufio.Scanner stops at 64 KiB lines, main.go:72-74)
+#define A5X_LMAX_G 65535
+#define A5X_MLMAX_G 65536
+#define A5X_DPENT_G (1u << 20)
+#define A5X_RING_G (1u << 20)
+#define A5X_G_SLOTS 16
 #define A5X_CMAX 63            // max DP columns-1 (count window)
 #define A5X_TABLE_LDS_MAX 32768
 

@@ -105,6 +105,8 @@ struct a5x_ctx {
   DevBuf<uint64_t> count, bytes, cand_off, byte_off, scan_tmp, locate;
   DevBuf<uint32_t> flags, defer, chunk_w0, slow_list, big_list, roff, cplx;
   DevBuf<uint64_t> segs;  // slow / BIG segment items
+  DevBuf<uint32_t> glob;  // pass G word list (words beyond the pass-B LDS budget)
+  uint8_t* gscr = nullptr;  // pass G scratch: A5X_G_SLOTS x a5x_gslot_bytes(), allocated on first use
   DevBuf<uint64_t> rec;  // FAST plan records (keyspace tiles of FW_TILE_REC u64)
   uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] nslow, [4] cplx_n, [5] slow segs, [6] BIG segs, [16..31] guard record
   uint32_t* h_scalars = nullptr;  // pinned
@@ -353,8 +355,9 @@ int decode_dev_err(a5x_ctx* c, uint32_t e) {
   if (e & 16u) return fail(c, A5X_E_OVERFLOW, "batch keyspace overflows 64 bits");
   if (e & 4u)
     return fail(c, A5X_E_UNSUPPORTED,
-                "a word with candidates exceeds the device limits (length %d B, %d matches, DP (events+1) x "
-                "(min(max,matches)+1) <= %d)", A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B);
+                "a word with candidates exceeds the device limits (length %d B, %d matches, min(max,matches) "
+                "<= 63 substitutions unless the window is free, DP (events+1) x (min(max,matches)+1) <= %u, "
+                "candidates <= %u B)", A5X_LMAX_G, A5X_MLMAX_G, (unsigned)A5X_DPENT_G, (unsigned)A5X_RING_G - 16u);
   return fail(c, A5X_E_HIP, "device consistency error 0x%x", e);
 }
 
@@ -365,6 +368,7 @@ uint32_t ks_cplx_cap(uint64_t nw) { return (uint32_t)std::min<uint64_t>(nw / 16 
 struct Batch {  // device-side per-batch state after keyspace
   uint64_t total_cands = 0, total_bytes = 0;
   uint32_t nbig = 0, nslow = 0;
+  uint32_t nglob = 0;  // pass G words (on the BIG list, expanded by k_expand_g)
   const uint64_t* cand_off = nullptr;
   const uint64_t* byte_off = nullptr;
 };
@@ -378,7 +382,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
       (rc = grow(c, c->defer, nw + 1)) || (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)) ||
       (rc = grow(c, c->roff, nw + 1)) || (rc = grow(c, c->cplx, nw + 1)) ||
-      (rc = grow(c, c->slow_list, nw + 1)) || (rc = grow(c, c->big_list, nw + 1)) ||
+      (rc = grow(c, c->slow_list, nw + 1)) || (rc = grow(c, c->big_list, nw + 1)) || (rc = grow(c, c->glob, nw + 1)) ||
       (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC +
                                 (uint64_t)ks_cplx_cap(nw) * FW_RMAX + 2)))
     return rc;
@@ -392,8 +396,9 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   }
   if (timed) HIPCHK(c, hipEventRecord(c->ev[0], st));
   HIPCHK(c, hipMemsetAsync(c->d_scalars, 0, 128, st));  // scalars + guard debug record
+  A5xKsLaunch K;
+  memset(&K, 0, sizeof K);
   if (nw > 0) {
-    A5xKsLaunch K;
     K.table = c->d_table; K.table_bytes = c->table_bytes; K.words = d_words; K.woff = d_woff; K.nw = nw;
     K.mn = mn; K.mx = mx; K.count = c->count.p; K.bytes = c->bytes.p; K.flags = c->flags.p;
     K.defer_list = c->defer.p; K.defer_n = c->d_scalars; K.nbig = c->d_scalars + 1; K.err = c->d_scalars + 2;
@@ -403,6 +408,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
     K.cplx_list = c->cplx.p; K.cplx_n = c->d_scalars + 4; K.cplx_cap = ks_cplx_cap(nw);
     K.cplx_base = ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC;
     K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nw, (uint64_t)c->cus * 4));
+    K.glob_list = c->glob.p; K.glob_n = c->d_scalars + 7;
     HIPCHK(c, a5x_launch_keyspace(K, st));
     HIPCHK(c, a5x_launch_scan(c->count.p, c->bytes.p, nw, d_cand_off, d_byte_off, c->scan_tmp.p,
                               c->d_scalars + 2, st));
@@ -413,8 +419,25 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
     HIPCHK(c, hipMemsetAsync(d_byte_off, 0, 8, st));
     c->h_totals[0] = c->h_totals[1] = 0;
   }
-  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  if (nw > 0 && c->h_scalars[2] == 0 && c->h_scalars[7] > 0) {
+    // pass G: words beyond the pass-B LDS budget are sized in HBM scratch slots (their
+    // counts were 0 in the first scan), then the scan runs again
+    if (!c->gscr) {
+      const size_t gb = (size_t)A5X_G_SLOTS * a5x_gslot_bytes();
+      HIPCHK(c, hipMalloc((void**)&c->gscr, gb));
+      HIPCHK(c, hipMemsetAsync(c->gscr, 0, gb, st));  // the rings start (and stay) zero
+    }
+    K.gscr = c->gscr; K.gslots = A5X_G_SLOTS;
+    HIPCHK(c, a5x_launch_keyspace_g(K, st));
+    HIPCHK(c, a5x_launch_scan(c->count.p, c->bytes.p, nw, d_cand_off, d_byte_off, c->scan_tmp.p,
+                              c->d_scalars + 2, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_totals, d_cand_off + nw, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_totals + 1, d_byte_off + nw, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+  }
   if ((rc = decode_dev_err(c, c->h_scalars[2]))) {
     // name the first offending word (diagnostics)
     std::vector<uint32_t> fl(nw);
@@ -438,6 +461,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   B->total_bytes = nw ? c->h_totals[1] : 0;
   B->nbig = c->h_scalars[1];
   B->nslow = c->h_scalars[3];
+  B->nglob = nw ? c->h_scalars[7] : 0;
   B->cand_off = d_cand_off;
   B->byte_off = d_byte_off;
   return A5X_OK;
@@ -454,6 +478,7 @@ A5xExpLaunch exp_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_wo
   E.waves_per_block = c->waves_per_block;
   E.waves_per_block_fast = c->waves_per_block_fast;
   E.rec = c->rec.p; E.roff = c->roff.p; E.rec_n = c->rec.cap;
+  if (B.nglob) { E.gscr = c->gscr; E.gslots = A5X_G_SLOTS; }
   return E;
 }
 
@@ -847,6 +872,7 @@ int job_launch(a5x_ctx* c, const Job& J, const Range& R, uint8_t* d_out, uint64_
   if (B.nbig) {
     E.segs = c->segs.p + sbound; E.nsegs = c->d_scalars + 6; E.nsegs_bound = bbound;
     HIPCHK(c, a5x_launch_expand(E, 2, side));
+    if (B.nglob) HIPCHK(c, a5x_launch_expand(E, 4, side));  // pass G words of the same list
   }
   HIPCHK(c, a5x_launch_expand(E, 0, J.st));
   if (side != J.st) {
@@ -976,6 +1002,8 @@ void a5x_destroy(a5x_ctx* c) {
   for (auto& e : c->ev_cpy)
     if (e) (void)hipEventDestroy(e);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  release(c->glob);
+  if (c->gscr) (void)hipFree(c->gscr);
   if (c->sstream) (void)hipStreamSynchronize(c->sstream);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);

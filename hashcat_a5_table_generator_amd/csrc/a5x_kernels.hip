@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string.h>
+
 #include <type_traits>
 
 #include "a5x_format.h"
@@ -37,6 +39,22 @@
     __builtin_amdgcn_wave_barrier();                         \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
   } while (0)
+
+// Wave sync of the per-word path: its WaveLds / ring live in LDS, except in pass G
+// (LMAX == A5X_LMAX_G) where they are HBM scratch written and read by the wave's own
+// lanes (one CU): workgroup-scope release/acquire drains the stores and atomics (the
+// CU's L1 never holds a stale copy of its own stores; the ring is only touched by
+// L2 atomics).
+template <int LMAX>
+__device__ __forceinline__ void ws_sync() {
+  if constexpr (LMAX > A5X_LMAX_B) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    WAVE_SYNC();
+  }
+}
 
 // Diagnostic build only (-DA5X_STAMPS): per-phase s_memtime cycle sums of the
 // fast kernel, read back with a5x_debug_stamps().  Never in the shipped build.
@@ -182,6 +200,9 @@ struct KsArgs {
   u32* cplx_n;
   u32 cplx_cap;    // record slots (FW_RMAX u64 each) at rec + cplx_base
   u64 cplx_base;
+  u32* glob_list;  // pass G words (k_keyspace_wave -> k_keyspace_g)
+  u32* glob_n;
+  uint8_t* gscr;   // pass G scratch slots
 };
 
 // Append the lanes with pred to list[*ctr ...] (one atomic per wave); returns the
@@ -565,7 +586,7 @@ __device__ WordInfo wave_setup(WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, con
   if (stored) {
     for (u32 p = lane; p < L + 16 && p < LMAX + 16; p += 64) S.wbuf[p] = p < L ? wp[p] : 0;
   }
-  WAVE_SYNC();
+  ws_sync<LMAX>();
   // ---- matches: positions in chunks of 64 lanes ----
   u32 base = 0, evbase = 0, prev_end = 0;  // running matches / events / max match end
   bool conflict = false, multi = false, room = true;
@@ -635,7 +656,7 @@ __device__ WordInfo wave_setup(WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, con
   I.lo = mn <= 1 ? 1 : mn;
   if (!stored || !room) { I.fits = 0; I.why = stored ? 2 : 1; I.cls = A5X_WF_GENERAL; return I; }
   if (lane == 0) { S.evidx[L] = (uint16_t)evbase; S.evpos[evbase] = (uint16_t)L; }
-  WAVE_SYNC();
+  ws_sync<LMAX>();
   const u32 m = evbase;
 
   if (!conflict && !multi && I.freew) {
@@ -651,7 +672,7 @@ __device__ WordInfo wave_setup(WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, con
       S.slots[i] = sl;
     }
     I.nslots = m;
-    WAVE_SYNC();
+    ws_sync<LMAX>();
     // digit weights (serial; nslots is small) and P
     u64 P = 1;
     bool ovf = false, bin = true;
@@ -663,7 +684,7 @@ __device__ WordInfo wave_setup(WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, con
       if (R != 2) bin = false;
       if (S.slots[i].delta1 != ud) ud = INT32_MIN;
     }
-    WAVE_SYNC();
+    ws_sync<LMAX>();
     if (!ovf && P <= (1ull << 32)) {
       // bytes = (P-1)(L+1) + sum_slots (P/R) sum_v delta   (lanes over slots)
       i64 part = 0;
@@ -720,7 +741,7 @@ __device__ WordInfo wave_setup(WaveLds<LMAX, MLMAX, DPENT>& S, const Tab& T, con
       S.dp.G[e * W + c] = g;
       S.dp.H[e * W + c] = h;
     }
-    WAVE_SYNC();
+    ws_sync<LMAX>();
   }
   I.ovf = wave_or_u32(ovf) != 0;
   I.count = S.dp.G[0];
@@ -749,22 +770,69 @@ __global__ void __launch_bounds__(64) k_keyspace_wave(KsArgs a) {
     WordInfo I = wave_setup<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>(S, T, a.words, a.woff, w, a.mn, a.mx);
     if (lane_id() == 0) {
       u32 f = I.cls ? I.cls : (u32)(A5X_WF_RADIX | A5X_WF_FAST);
+      // beyond the LDS budget (long line, many matches, big DP or long candidates):
+      // pass G (k_keyspace_g) sizes it in HBM scratch and puts it on the BIG list
+      const bool glob = I.cls && (!I.fits || I.maxlen > A5X_RING_B - 16) && I.why != 3;
       // would pass A (smaller LDS budget) handle it?
       bool fitsA = I.L <= A5X_LMAX_A && I.nmatch <= A5X_MLMAX_A && I.maxlen <= A5X_RING_A - 16 &&
                    (I.cls != A5X_WF_GENERAL || (u64)(I.nev + 1) * I.W <= A5X_DPENT_A);
-      if (I.cls && !fitsA) { f |= A5X_WF_BIG; a.big_list[atomicAdd(a.nbig, 1u)] = w; }
-      else if (I.cls) a.slow_list[atomicAdd(a.nslow, 1u)] = w;
-      if (I.cls && (!I.fits || I.maxlen > A5X_RING_B - 16)) {
+      if (glob) {
+        f = A5X_WF_BIG | A5X_WF_GLOB;
+        a.glob_list[atomicAdd(a.glob_n, 1u)] = w;
+      } else if (I.cls && !fitsA) {
+        f |= A5X_WF_BIG;
+        a.big_list[atomicAdd(a.nbig, 1u)] = w;
+      } else if (I.cls) {
+        a.slow_list[atomicAdd(a.nslow, 1u)] = w;
+      }
+      if (!glob && I.cls && (!I.fits || I.maxlen > A5X_RING_B - 16)) {  // W > 64 count columns
         f |= A5X_WF_ERR_BIG | ((I.fits ? 5u : I.why) << 16) | (min(I.W, 255u) << 24);
         atomicOr(a.err, A5X_DERR_BIG);
       }
       if (I.ovf) { f |= A5X_WF_ERR_OVF; atomicOr(a.err, A5X_DERR_OVF); }
-      const bool bad = (f & (A5X_WF_ERR_BIG | A5X_WF_ERR_OVF)) != 0;
+      const bool bad = glob || (f & (A5X_WF_ERR_BIG | A5X_WF_ERR_OVF)) != 0;
       a.count[w] = bad ? 0 : I.count;
       a.bytes[w] = bad ? 0 : I.bytes;
       a.flags[w] = f;
     }
     WAVE_SYNC();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass G: words beyond the pass-B LDS budget (lines up to 64 KiB, more matches,
+// bigger DP tables, candidates up to A5X_RING_G - 16 bytes).  The same wave_setup /
+// expand_word code on a WaveLds and ring in HBM scratch, one slot per workgroup.
+// ---------------------------------------------------------------------------
+typedef WaveLds<A5X_LMAX_G, A5X_MLMAX_G, A5X_DPENT_G> LdsG;
+#define GSLOT_BYTES ((u64)A5X_RING_G + (((u64)sizeof(LdsG) + 255ull) & ~255ull))
+
+__global__ void __launch_bounds__(64) k_keyspace_g(KsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  LdsG& S = *(LdsG*)(a.gscr + (u64)blockIdx.x * GSLOT_BYTES + A5X_RING_G);
+  const u32 n = *a.glob_n;
+  for (u32 i = blockIdx.x; i < n; i += gridDim.x) {
+    const u32 w = a.glob_list[i];
+    WordInfo I = wave_setup<A5X_LMAX_G, A5X_MLMAX_G, A5X_DPENT_G>(S, T, a.words, a.woff, w, a.mn, a.mx);
+    if (lane_id() == 0) {
+      u32 f = (I.cls ? I.cls : (u32)A5X_WF_RADIX) | A5X_WF_BIG | A5X_WF_GLOB;
+      bool bad = false;
+      if (I.cls && (!I.fits || I.maxlen > A5X_RING_G - 16)) {
+        f |= A5X_WF_ERR_BIG | ((I.fits ? 5u : I.why) << 16) | (min(I.W, 255u) << 24);
+        atomicOr(a.err, A5X_DERR_BIG);
+        bad = true;
+      } else if (I.cls) {
+        a.big_list[atomicAdd(a.nbig, 1u)] = w;
+      }
+      if (I.ovf) { f |= A5X_WF_ERR_OVF; atomicOr(a.err, A5X_DERR_OVF); bad = true; }
+      a.count[w] = bad ? 0 : I.count;
+      a.bytes[w] = bad ? 0 : I.bytes;
+      a.flags[w] = f;
+    }
+    ws_sync<A5X_LMAX_G>();
   }
 }
 
@@ -922,6 +990,8 @@ struct ExpArgs {
   u64 dg_tmask;
   A5xHitRaw* dg_hits;    // (word, candidate in word, digest)
   u32* dg_nhits;
+  uint8_t* gscr;         // pass G scratch slots (k_expand_g, k_locate)
+  u32 gslots;
 };
 
 // Record the first tripped guard (code + context) and flag the call as failed.
@@ -1007,12 +1077,18 @@ __device__ __forceinline__ void run_flush(Run& R, u32* ring, const ExpArgs& a, u
   for (u64 b = lane; b < nb; b += 64) {
     const u64 X = R.flushed + b * 16;
     uint4* rp = (uint4*)ring + (((X - R.base) / 16) & (RING / 16 - 1));
-    const uint4 v = *rp;
-    *rp = make_uint4(0, 0, 0, 0);
+    uint4 v;
+    if constexpr (RING > A5X_RING_B) {  // pass G: the ring is HBM scratch, filled by atomics
+      u32* q = (u32*)rp;
+      v = make_uint4(atomicExch(q, 0u), atomicExch(q + 1, 0u), atomicExch(q + 2, 0u), atomicExch(q + 3, 0u));
+    } else {
+      v = *rp;
+      *rp = make_uint4(0, 0, 0, 0);
+    }
     store_block(a, X, v, R.lo, hi);
   }
   R.flushed = upto;
-  WAVE_SYNC();
+  ws_sync<(RING > A5X_RING_B ? A5X_LMAX_G : 0)>();
 }
 
 template <u32 RING>
@@ -1213,11 +1289,11 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
       }
       R.pos += tot;
     }
-    WAVE_SYNC();
+    ws_sync<LMAX>();
     const u64 full = R.pos & ~15ull;
     if (full > R.flushed) run_flush<RING>(R, ring, a, full, R.pos);
   }
-  WAVE_SYNC();
+  ws_sync<LMAX>();
   return true;
 }
 
@@ -1993,8 +2069,28 @@ __global__ void __launch_bounds__(64) k_expand_b(ExpArgs a) {
   __syncthreads();
   const Tab T = tab_view(smem);
   const u32 n = *a.nsegs;
-  for (u32 i = blockIdx.x; i < n; i += gridDim.x)
-    expand_segment<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B, A5X_RING_B>(S, ring, T, a, a.segs[i]);
+  for (u32 i = blockIdx.x; i < n; i += gridDim.x) {
+    const u64 item = a.segs[i];
+    if (a.flags[(u32)item] & A5X_WF_GLOB) continue;  // pass G (k_expand_g)
+    expand_segment<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B, A5X_RING_B>(S, ring, T, a, item);
+  }
+}
+
+// pass G: the GLOB words' segments of the BIG list, one scratch slot per workgroup
+__global__ void __launch_bounds__(64) k_expand_g(ExpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  uint8_t* slot = a.gscr + (u64)blockIdx.x * GSLOT_BYTES;
+  u32* ring = (u32*)slot;  // zero between flushes (a5x_host zeroes it once)
+  LdsG& S = *(LdsG*)(slot + A5X_RING_G);
+  const u32 n = *a.nsegs;
+  for (u32 i = blockIdx.x; i < n; i += gridDim.x) {
+    const u64 item = a.segs[i];
+    if (!(a.flags[(u32)item] & A5X_WF_GLOB)) continue;
+    expand_segment<A5X_LMAX_G, A5X_MLMAX_G, A5X_DPENT_G, A5X_RING_G>(S, ring, T, a, item);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2024,6 +2120,14 @@ __global__ void __launch_bounds__(64) k_locate(ExpArgs a, const u64* cands, u32 
       for (u32 i2 = lane_id(); i2 < rs; i2 += 64) rec[i2] = a.rec[a.roff[w] + i2];
       WAVE_SYNC();
       pos += fast_prefix_bytes(rec, r);
+    } else if (r && (a.flags[w] & A5X_WF_GLOB)) {
+      // pass G word: its setup in this workgroup's scratch slot (the host limits the grid)
+      if (blockIdx.x >= a.gslots) { if (lane_id() == 0) atomicOr(a.err, A5X_DERR_STATE); return; }
+      LdsG& SG = *(LdsG*)(a.gscr + (u64)blockIdx.x * GSLOT_BYTES + A5X_RING_G);
+      WordInfo I = wave_setup<A5X_LMAX_G, A5X_MLMAX_G, A5X_DPENT_G>(SG, T, a.words, a.woff, w, a.mn, a.mx);
+      if (!I.fits) { if (lane_id() == 0) atomicOr(a.err, A5X_DERR_STATE); return; }
+      if (I.cls & A5X_WF_RADIX) pos += radix_prefix_bytes(SG, T, I, r);
+      else pos += uniform64(dp_prefix_bytes(SG, T, I, r));
     } else if (r) {
       WordInfo I = wave_setup<A5X_LMAX_B, A5X_MLMAX_B, A5X_DPENT_B>(S, T, a.words, a.woff, w, a.mn, a.mx);
       if (!I.fits) { if (lane_id() == 0) atomicOr(a.err, A5X_DERR_STATE); return; }
@@ -2085,6 +2189,7 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   a.big_list = L.big_list; a.slow_list = L.slow_list;
   a.rec = L.rec; a.roff = L.roff;
   a.cplx_list = L.cplx_list; a.cplx_n = L.cplx_n; a.cplx_cap = L.cplx_cap; a.cplx_base = L.cplx_base;
+  a.glob_list = L.glob_list; a.glob_n = L.glob_n; a.gscr = L.gscr;
   hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -2094,6 +2199,19 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   if (e != hipSuccess) return e;
   const size_t lds = ((L.table_bytes + 15u) & ~15u) + sizeof(LdsB);
   hipLaunchKernelGGL(k_keyspace_wave, dim3(L.defer_blocks), dim3(64), lds, st, a);
+  return hipGetLastError();
+}
+
+uint64_t a5x_gslot_bytes() { return GSLOT_BYTES; }
+
+hipError_t a5x_launch_keyspace_g(const A5xKsLaunch& L, hipStream_t st) {
+  KsArgs a;
+  memset(&a, 0, sizeof a);
+  a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
+  a.mn = L.mn; a.mx = L.mx; a.count = L.count; a.bytes = L.bytes; a.flags = L.flags;
+  a.nbig = L.nbig; a.err = L.err; a.big_list = L.big_list;
+  a.glob_list = L.glob_list; a.glob_n = L.glob_n; a.gscr = L.gscr;
+  hipLaunchKernelGGL(k_keyspace_g, dim3(L.gslots), dim3(64), (L.table_bytes + 15u) & ~15u, st, a);
   return hipGetLastError();
 }
 
@@ -2152,6 +2270,7 @@ static ExpArgs exp_args(const A5xExpLaunch& L) {
   a.rec = L.rec; a.roff = L.roff; a.rec_n = L.rec_n;
   a.dg_bitmap = L.dg_bitmap; a.dg_bm_mask = L.dg_bm_mask; a.dg_has_zero = L.dg_has_zero; a.dg_hit_cap = L.dg_hit_cap;
   a.dg_table = L.dg_table; a.dg_tmask = L.dg_tmask; a.dg_hits = L.dg_hits; a.dg_nhits = L.dg_nhits;
+  a.gscr = L.gscr; a.gslots = L.gslots;
   return a;
 }
 
@@ -2178,16 +2297,19 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   else if (kind == 1)
     hipLaunchKernelGGL(k_expand_slow, dim3(blocks_for(L.nsegs_bound, waves, 65536)), dim3(64 * waves),
                        a5x_expand_lds(L.table_bytes, 1, waves), st, a);
-  else
+  else if (kind == 2)
     hipLaunchKernelGGL(k_expand_b, dim3(blocks_for(L.nsegs_bound, 1, 65536)), dim3(64), a5x_expand_lds(L.table_bytes, 2, 1),
                        st, a);
+  else if (kind == 4)
+    hipLaunchKernelGGL(k_expand_g, dim3(L.gslots), dim3(64), (L.table_bytes + 15u) & ~15u, st, a);
   return hipGetLastError();
 }
 
 hipError_t a5x_launch_locate(const A5xExpLaunch& L, const u64* cands, u32 n, u64* out_bytes, hipStream_t st) {
   ExpArgs a = exp_args(L);
-  hipLaunchKernelGGL(k_locate, dim3(n < 1024 ? (n ? n : 1) : 1024), dim3(64), a5x_keyspace_wave_lds(L.table_bytes), st, a,
-                     cands, n, out_bytes);
+  u32 grid = n < 1024 ? (n ? n : 1) : 1024;
+  if (L.gscr && L.gslots) grid = grid < L.gslots ? grid : L.gslots;  // one pass G slot per workgroup
+  hipLaunchKernelGGL(k_locate, dim3(grid), dim3(64), a5x_keyspace_wave_lds(L.table_bytes), st, a, cands, n, out_bytes);
   return hipGetLastError();
 }
 

@@ -28,6 +28,10 @@ struct A5xKsLaunch {
   uint32_t* cplx_n;
   uint32_t cplx_cap;    // record slots of FW_RMAX u64 from rec + cplx_base
   uint64_t cplx_base;
+  uint32_t* glob_list;  // words beyond the pass-B LDS budget (k_keyspace_wave appends)
+  uint32_t* glob_n;
+  uint8_t* gscr;        // pass G scratch: gslots x a5x_gslot_bytes() (ring zeroed)
+  uint32_t gslots;
 };
 
 struct A5xHitRaw;
@@ -65,9 +69,16 @@ struct A5xExpLaunch {
   uint64_t dg_tmask;
   A5xHitRaw* dg_hits;
   uint32_t* dg_nhits;
+  // pass G (words beyond the pass-B LDS budget): HBM scratch slots, one per wave
+  uint8_t* gscr;
+  uint32_t gslots;
 };
 
 hipError_t a5x_set_kernel_attrs();
+// pass G: bytes per scratch slot (ring of A5X_RING_G bytes, then the word's WaveLds)
+uint64_t a5x_gslot_bytes();
+// k_keyspace_g over the words k_keyspace_wave listed (grid = gslots)
+hipError_t a5x_launch_keyspace_g(const A5xKsLaunch& L, hipStream_t st);
 int a5x_read_stamps(unsigned long long* out16, int reset);
 hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st);
 size_t a5x_keyspace_wave_lds(uint32_t table_bytes);
@@ -81,7 +92,8 @@ hipError_t a5x_launch_segments(const uint32_t* list, const uint32_t* list_n, uin
                                const uint64_t* cand_off, uint64_t cb, uint64_t ce, uint64_t CH, uint64_t* segs,
                                uint32_t* nsegs, hipStream_t st);
 size_t a5x_expand_lds(uint32_t table_bytes, int kind, uint32_t waves);
-// kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b (pass B)
+// kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b (pass B), 3: k_expand_fast_md5,
+// 4: k_expand_g (pass G: the GLOB words of the BIG segment list)
 hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st);
 hipError_t a5x_launch_locate(const A5xExpLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out_bytes,
                              hipStream_t st);
