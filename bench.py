@@ -225,7 +225,7 @@ def cpu_baseline(tables, args):
             "cpu_model": cpu_model(), "runs": runs,
             "sample": f"{args.cpu_sample_words} words of workload {args.workload} (seed 0xC0FFEE) to /dev/null; "
                       f"C restatement of main.go (oracle/a5_oracle.c) with its goroutine pool, 1000-slot channel "
-                      f"(lock-free ring, spin-then-yield like Go's runtime) and one 4 KiB writer; best of 1 and "
+                      f"(lock-free ring; a blocked sender or receiver spins briefly, then parks on a futex like a goroutine) and one 4 KiB writer; best of 1 and "
                       f"{nmax} worker thread(s) ({cpu_model()})"}
 
 

@@ -24,7 +24,11 @@
 #define _GNU_SOURCE
 #include <errno.h>
 #include <pthread.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <sched.h>
+#include <time.h>
 #include <stdatomic.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -646,25 +650,38 @@ A5O_EXPORT int64_t a5o_expand_batch(const a5o_table *t, const uint8_t *words, co
 /* A buffered Go channel as a bounded lock-free MPMC ring (D. Vyukov's sequence-number
  * queue): a sender claims a slot with one CAS and publishes it with a release store;
  * the receiver takes slots in order.  A full (empty) channel makes the sender
- * (receiver) spin, then yield the core -- the cheap user-space park/unpark of Go's
- * runtime, not a kernel condition variable per operation (which serialised 16
- * senders on one futex and collapsed throughput). */
+ * (receiver) spin briefly and then PARK on a futex, like a goroutine parking on a
+ * channel: it stops using a core (Go's scheduler runs something else), and it is
+ * woken only when a receiver (sender) sees a parked waiter -- no syscall per message
+ * while nobody sleeps.  (Round 1 used a mutex + condition variable per operation,
+ * which serialised 16 senders on one futex; round 2's spin-then-yield kept every
+ * blocked sender runnable, starving the writer whenever the host's CPU quota was
+ * smaller than senders + 1.) */
 typedef struct { _Atomic size_t seq; bstr v; } chan_slot;
 typedef struct {
     chan_slot q[CHAN_CAP];
     _Alignas(64) _Atomic size_t tail;  /* next slot to send into */
     _Alignas(64) _Atomic size_t head;  /* next slot to receive from (one receiver) */
     _Alignas(64) _Atomic int closed;
+    _Alignas(64) _Atomic uint32_t hgen, swait;  /* receiver progress generation, parked senders */
+    _Alignas(64) _Atomic uint32_t tgen, rwait;  /* sender progress generation, parked receiver */
 } chan_t;
 
 static void chan_init(chan_t *c) {
     for (size_t i = 0; i < CHAN_CAP; i++) atomic_init(&c->q[i].seq, i);
     atomic_init(&c->tail, 0); atomic_init(&c->head, 0); atomic_init(&c->closed, 0);
+    atomic_init(&c->hgen, 0); atomic_init(&c->swait, 0); atomic_init(&c->tgen, 0); atomic_init(&c->rwait, 0);
 }
 
-static void chan_backoff(unsigned *spins) {
-    if (++*spins < 64) __builtin_ia32_pause(); else { sched_yield(); *spins = 0; }
+static void futex_wait_u32(_Atomic uint32_t *a, uint32_t v) {  /* bounded park: a missed wake costs <= 50 us */
+    struct timespec ts = {0, 50000};
+    syscall(SYS_futex, (uint32_t *)a, FUTEX_WAIT_PRIVATE, v, &ts, NULL, 0);
 }
+static void futex_wake_all(_Atomic uint32_t *a) {
+    syscall(SYS_futex, (uint32_t *)a, FUTEX_WAKE_PRIVATE, INT32_MAX, NULL, NULL, 0);
+}
+
+#define CHAN_SPIN 64
 
 static void chan_send(chan_t *c, bstr s) {
     unsigned spins = 0;
@@ -678,10 +695,25 @@ static void chan_send(chan_t *c, bstr s) {
                                                       memory_order_relaxed)) {
                 sl->v = s;
                 atomic_store_explicit(&sl->seq, pos + 1, memory_order_release);
+                if (atomic_load_explicit(&c->rwait, memory_order_relaxed)) {  /* wake the parked receiver */
+                    atomic_fetch_add_explicit(&c->tgen, 1, memory_order_relaxed);
+                    futex_wake_all(&c->tgen);
+                }
                 return;
             }
-        } else if (d < 0) {  /* full: park */
-            chan_backoff(&spins);
+        } else if (d < 0) {  /* full */
+            if (++spins < CHAN_SPIN) {
+                __builtin_ia32_pause();
+            } else if (spins < CHAN_SPIN + 64) {
+                sched_yield();
+            } else {  /* park until the receiver frees a slot */
+                const uint32_t g = atomic_load_explicit(&c->hgen, memory_order_relaxed);
+                atomic_fetch_add_explicit(&c->swait, 1, memory_order_seq_cst);
+                const size_t seq2 = atomic_load_explicit(&sl->seq, memory_order_acquire);
+                if ((intptr_t)seq2 - (intptr_t)pos < 0) futex_wait_u32(&c->hgen, g);
+                atomic_fetch_sub_explicit(&c->swait, 1, memory_order_relaxed);
+                spins = 0;
+            }
             pos = atomic_load_explicit(&c->tail, memory_order_relaxed);
         } else {
             pos = atomic_load_explicit(&c->tail, memory_order_relaxed);
@@ -699,12 +731,38 @@ static int chan_recv(chan_t *c, bstr *s) {
         if (atomic_load_explicit(&c->closed, memory_order_acquire) &&
             atomic_load_explicit(&sl->seq, memory_order_acquire) != pos + 1)
             return 0;  /* closed after every sender finished: nothing left */
-        chan_backoff(&spins);
+        if (++spins < CHAN_SPIN) {
+            __builtin_ia32_pause();
+        } else if (spins < CHAN_SPIN + 256) {
+            sched_yield();  /* the writer stays runnable a while: senders are usually mid-word */
+        } else {  /* park until a sender publishes (or the channel closes) */
+            const uint32_t g = atomic_load_explicit(&c->tgen, memory_order_relaxed);
+            atomic_store_explicit(&c->rwait, 1, memory_order_seq_cst);
+            if (atomic_load_explicit(&sl->seq, memory_order_acquire) != pos + 1 &&
+                !atomic_load_explicit(&c->closed, memory_order_acquire))
+                futex_wait_u32(&c->tgen, g);
+            atomic_store_explicit(&c->rwait, 0, memory_order_relaxed);
+            spins = 0;
+        }
     }
     *s = sl->v;
     atomic_store_explicit(&sl->seq, pos + CHAN_CAP, memory_order_release);
     atomic_store_explicit(&c->head, pos + 1, memory_order_relaxed);
+    /* parked senders are woken together once the channel is half empty (one syscall
+     * per ~CHAN_CAP/2 messages, like Go's cheap goready); parks are bounded, so no
+     * fence is needed against a sender that parks concurrently */
+    if (atomic_load_explicit(&c->swait, memory_order_relaxed) &&
+        atomic_load_explicit(&c->tail, memory_order_relaxed) - (pos + 1) <= CHAN_CAP / 2) {
+        atomic_fetch_add_explicit(&c->hgen, 1, memory_order_relaxed);
+        futex_wake_all(&c->hgen);
+    }
     return 1;
+}
+
+static void chan_close(chan_t *c) {
+    atomic_store_explicit(&c->closed, 1, memory_order_seq_cst);
+    atomic_fetch_add_explicit(&c->tgen, 1, memory_order_relaxed);
+    futex_wake_all(&c->tgen);
 }
 
 typedef struct {
@@ -765,7 +823,7 @@ A5O_EXPORT int a5o_run_pipeline(const a5o_table *t, const uint8_t *words, const 
     pthread_create(&wr, NULL, pipe_writer, j);
     for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, pipe_worker, j);
     for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
-    atomic_store_explicit(&j->ch.closed, 1, memory_order_release);  /* close(out) after wg.Wait() */
+    chan_close(&j->ch);  /* close(out) after wg.Wait() */
     pthread_join(wr, NULL);
     *out_cands = j->out_cands; *out_bytes = j->out_bytes;
     int rc = atomic_load(&j->err);
