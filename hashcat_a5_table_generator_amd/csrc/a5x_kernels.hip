@@ -217,6 +217,11 @@ __device__ __forceinline__ u32 wave_append(bool pred, u32* ctr) {
   return base + (u32)__popcll(m & ((1ull << lane) - 1ull));
 }
 
+#ifndef KS_ABL
+#define KS_ABL 0  // keyspace timing ablations (variant builds only, wrong output): 1 no build pass,
+                  // 2 no planner in the count pass, 4 no record stores
+#endif
+
 // k_keyspace_thread's open group holds KS_GCAP entries (a unit with more choices
 // makes the word complex: k_keyspace_cplx plans it with FW_UMAXR)
 #define KS_GCAP 8
@@ -232,8 +237,8 @@ struct DevRecSink {
   __device__ u32 cstride() const { return 256u; }
   __device__ u64 gld(u32 a) const { return g[a * 256u]; }
   __device__ void gst(u32 a, u64 v) { g[a * 256u] = v; }
-  __device__ void ent(u32 i, u64 v) { rec[1 + np + i] = v; }
-  __device__ void desc(u32 i, u64 v) { rec[1 + i] = v; }
+  __device__ void ent(u32 i, u64 v) { if (!(KS_ABL & 4)) rec[1 + np + i] = v; }
+  __device__ void desc(u32 i, u64 v) { if (!(KS_ABL & 4)) rec[1 + i] = v; }
 };
 
 // A word's bytes staged in LDS (the keyspace tile); 8 readable bytes past any word.
@@ -316,7 +321,7 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
           cplx = true;
         } else {
           if (COUNT) count_unit(A, U);
-          pl.unit(U);
+          if (!(KS_ABL & 2)) pl.unit(U);
           cur_end = U.e;
           if (COUNT && ulog) {
             const bool fits = *nlog < KS_ULOG && kk < 1024u && q < 64u;
@@ -421,7 +426,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       // replay the logged units (no second byte walk); words with more units re-walk
       const bool replay = nlog <= KS_ULOG;
       const u32 nrep = build && replay ? nlog : 0u;
-      for (u32 i = 0; i < wave_max_u32(nrep); i++) {
+      for (u32 i = 0; i < wave_max_u32((KS_ABL & 1) ? 0u : nrep); i++) {
         if (i < nrep) {
           const u32 e = ulog[i * 256u];
           Unit U;
@@ -430,8 +435,8 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
         }
       }
       const bool walk = build && !replay;
-      psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2);
-      if (build) {
+      if (!(KS_ABL & 1)) psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2);
+      if (build && !(KS_ABL & 1)) {
         pb.finish(L);
         const Plan& P = pb.P;
         rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
