@@ -1477,11 +1477,12 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
   if ((rc = grow(c, c->dg_cand_off, nw + 1)) || (rc = grow(c, c->dg_byte_off, nw + 1))) return rc;
   if ((rc = job_prepare(c, J, c->dg_cand_off.p, c->dg_byte_off.p, true))) return rc;
   const uint64_t tc = J.B.total_cands, tb = J.B.total_bytes;
-  // Fused path (default mode, MD5, every candidate-bearing word FAST): k_expand_fast_md5
-  // hashes each candidate in the LDS ring where it is built -- no HBM scratch, no second
-  // pass, hits already (word, candidate).  Otherwise the two-pass range loop below.
-  const bool fused = mode == A5X_MODE_DEFAULT && c->t_algo == A5X_ALGO_MD5 && J.B.nslow == 0 && J.B.nbig == 0 &&
-                     tc > 0 && !getenv("A5X_NO_FUSED_DIGEST");
+  // Fused path (default mode, every candidate-bearing word FAST): k_expand_fast_md5 /
+  // k_expand_fast_ntlm hash each candidate in the LDS ring where it is built -- no HBM
+  // scratch, no second pass, hits already (word, candidate).  Otherwise the two-pass
+  // range loop below.
+  const bool fused = mode == A5X_MODE_DEFAULT && J.B.nslow == 0 && J.B.nbig == 0 && tc > 0 &&
+                     !getenv("A5X_NO_FUSED_DIGEST");
   if (fused) {
     uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
     if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
@@ -1497,7 +1498,7 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
       E.dg_hits = c->dg_hits.p; E.dg_hit_cap = (uint32_t)dev_hits; E.dg_nhits = c->d_scalars + 8;
       HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
       HIPCHK(c, hipEventRecord(c->ev[1], J.st));
-      HIPCHK(c, a5x_launch_expand(E, 3, J.st));
+      HIPCHK(c, a5x_launch_expand(E, c->t_algo == A5X_ALGO_MD5 ? 3 : 5, J.st));
       HIPCHK(c, hipEventRecord(c->ev[2], J.st));
       HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
       HIPCHK(c, hipStreamSynchronize(J.st));

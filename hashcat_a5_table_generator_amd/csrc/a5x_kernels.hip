@@ -1342,7 +1342,7 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #define FX_PFM 1      // next window's metadata loaded before the current window's rounds
 #endif
 #ifndef FX_SPEC
-#define FX_SPEC 0     // speculative next-window records with the metadata loads (A/B: no gain)
+#define FX_SPEC 0     // speculative next-window records with the metadata loads (spills VGPRs: off)
 #endif
 #ifndef FX_SPEC_N
 #define FX_SPEC_N 2   // ... KiB of them (uint4 per lane)
@@ -1550,6 +1550,7 @@ struct FxFlush {
 // after a round's placement every lane MD5s its run's candidates straight out of the
 // LDS ring and probes the target set; nothing goes to HBM but the hits, which carry
 // (word, candidate in word) directly.  The ring is then zeroed for the next round.
+template <bool MD5>
 struct FxDigest {
   static constexpr bool DIGEST = true;
   u32* ring;
@@ -1571,7 +1572,8 @@ struct FxDigest {
       const bool on = c < lr.nc;
       if (!__builtin_amdgcn_ballot_w64(on)) break;  // runs are filled from candidate 0
       u32 d[4];
-      md_lds<true>(base, off, on ? l - 1u : 0u, d);  // the candidate without its '\n'
+      if constexpr (MD5) md_lds<true>(base, off, on ? l - 1u : 0u, d);  // the candidate without its '\n'
+      else ntlm_lds(base, off, on ? l - 1u : 0u, d);
       if (on && md_probe(a->dg_bitmap, a->dg_bm_mask, a->dg_table, a->dg_tmask, a->dg_has_zero != 0, d)) {
         const u32 h = atomicAdd(a->dg_nhits, 1u);
         if (h < a->dg_hit_cap) {
@@ -1738,7 +1740,8 @@ __device__ __forceinline__ void fx_direct_window(FXWin& F, u32* ring, const u64*
   (void)w;
 }
 
-template <bool DIG>
+// DIG: 0 = write the stream, 1 = fused MD5, 2 = fused NTLM
+template <int DIG>
 __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
   u64* const rec = (u64*)(ring + 4);  // ring bytes [16, 16 + 8 FX_WREC)
@@ -1758,7 +1761,7 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
   u64 g = g0;
   FxRun R;
   R.open = false; R.B = 0; R.lo = 0; R.pos = 0; R.carry = 0;
-  typename std::conditional<DIG, FxDigest, FxFlush>::type fl;
+  typename std::conditional<DIG != 0, FxDigest<DIG == 1>, FxFlush>::type fl;
   fl.ring = ring; fl.a = &a; fl.wbase = 0;
   FxMeta M = fx_meta(a, w);
 #if FX_SPEC
@@ -1969,6 +1972,20 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     // metadata registers are dead from here on)
     const u64 gnext = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     M = fx_meta(a, w + k);
+#if FX_SPEC
+    {
+      // the next window's records, loaded under this window's rounds too: right after
+      // this window's, or the start of the next tile's region
+      const u64 wn = w + k;
+      const u64 nx = (wn % FW_TILE == 0) ? (wn / FW_TILE) * (u64)FW_TILE_REC : src0 + ntot;
+      nsp = min((u32)FX_SPEC_N, (ntot + 2u * 128u - 1u) / 128u);  // this window's size + 1 KiB
+      spb = nx & ~1ull;
+      const uint4* src = (const uint4*)(a.rec + spb);
+#pragma unroll
+      for (u32 q = 0; q < FX_SPEC_N; q++)
+        if (q < nsp) sp[q] = spb + 2ull * (lane + 64 * q) + 2 <= a.rec_n ? src[lane + 64 * q] : make_uint4(0, 0, 0, 0);
+    }
+#endif
 #endif
     // ---- rounds ----
     if (!(FX_ABL & 8))
@@ -1985,18 +2002,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     w += k;
     M = fx_meta(a, w);
 #endif
-#if FX_SPEC
-    {
-      // next records: right after this window's, or the start of the next tile's region
-      const u64 nx = (w % FW_TILE == 0) ? (w / FW_TILE) * (u64)FW_TILE_REC : src0 + ntot;
-      nsp = min((u32)FX_SPEC_N, (ntot + 2u * 128u - 1u) / 128u);  // this window's size + 1 KiB
-      spb = nx & ~1ull;
-      const uint4* src = (const uint4*)(a.rec + spb);
-#pragma unroll
-      for (u32 q = 0; q < FX_SPEC_N; q++)
-        if (q < nsp) sp[q] = spb + 2ull * (lane + 64 * q) + 2 <= a.rec_n ? src[lane + 64 * q] : make_uint4(0, 0, 0, 0);
-    }
-#endif
     WAVE_SYNC();
   }
   if (!DIG) fx_close(R, ring, a);
@@ -2009,7 +2014,7 @@ __device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + FX_TRASH 
 #ifndef FX_WPE
 #define FX_WPE 4  // 16 waves per CU: <= 128 VGPRs, <= 10 KiB LDS per wave
 #endif
-template <bool DIG>
+template <int DIG>
 __device__ __forceinline__ void expand_fast_body(const ExpArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
@@ -2022,12 +2027,18 @@ __device__ __forceinline__ void expand_fast_body(const ExpArgs& a) {
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE))) k_expand_fast(ExpArgs a) {
-  expand_fast_body<false>(a);
+  expand_fast_body<0>(a);
 }
 
 // the same chunks, hashed (MD5) and probed in the ring instead of written (FxDigest)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE))) k_expand_fast_md5(ExpArgs a) {
-  expand_fast_body<true>(a);
+  expand_fast_body<1>(a);
+}
+
+// the same chunks, NTLM (MD4 over Go's UTF-16LE of each candidate, converted as the
+// message blocks are filled) hashed and probed in the ring
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FX_WPE))) k_expand_fast_ntlm(ExpArgs a) {
+  expand_fast_body<2>(a);
 }
 
 // k_expand_slow / k_expand_b: one k_segments item (a slow or BIG word's run of <= CH
@@ -2286,7 +2297,7 @@ size_t a5x_expand_lds(u32 table_bytes, int kind, u32 waves) {
   return waves * ((FX_RING + FX_TRASH + sizeof(FXWin) + 15u) & ~(size_t)15u);
 }
 
-// kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b, 3: k_expand_fast_md5 (fused digest)
+// kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b, 3 / 5: k_expand_fast_md5 / _ntlm (fused digest)
 hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   ExpArgs a = exp_args(L);
   const u64 c0 = L.cand_begin / L.CH, c1 = (L.cand_end + L.CH - 1) / L.CH;
@@ -2298,6 +2309,9 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
     hipLaunchKernelGGL(k_expand_fast, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);
   else if (kind == 3)
     hipLaunchKernelGGL(k_expand_fast_md5, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st,
+                       a);
+  else if (kind == 5)
+    hipLaunchKernelGGL(k_expand_fast_ntlm, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st,
                        a);
   else if (kind == 1)
     hipLaunchKernelGGL(k_expand_slow, dim3(blocks_for(L.nsegs_bound, waves, 65536)), dim3(64 * waves),

@@ -62,7 +62,7 @@ struct A5xExpLaunch {
   const uint64_t* rec;
   const uint32_t* roff;
   uint64_t rec_n;   // u64 in rec
-  // fused digest (kind 3): target set + hit buffer (see A5xDigLaunch)
+  // fused digest (kinds 3, 5): target set + hit buffer (see A5xDigLaunch)
   const uint32_t* dg_bitmap;
   uint32_t dg_bm_mask, dg_has_zero, dg_hit_cap;
   const uint4* dg_table;
@@ -93,7 +93,7 @@ hipError_t a5x_launch_segments(const uint32_t* list, const uint32_t* list_n, uin
                                uint32_t* nsegs, hipStream_t st);
 size_t a5x_expand_lds(uint32_t table_bytes, int kind, uint32_t waves);
 // kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b (pass B), 3: k_expand_fast_md5,
-// 4: k_expand_g (pass G: the GLOB words of the BIG segment list)
+// 4: k_expand_g (pass G: the GLOB words of the BIG segment list), 5: k_expand_fast_ntlm
 hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st);
 hipError_t a5x_launch_locate(const A5xExpLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out_bytes,
                              hipStream_t st);

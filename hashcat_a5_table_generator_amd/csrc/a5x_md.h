@@ -127,3 +127,83 @@ __device__ __forceinline__ void md_lds(const uint8_t* base, uint32_t off, uint32
     if (MD5) md5_block(d, M); else md4_block(d, M);
   }
 }
+
+// Next UTF-16 unit of Go's utf16.Encode([]rune(s)) over message bytes [0, len) at
+// base + off (LDS, readable 4 bytes past the message): i = byte position, pend = the
+// pending low surrogate (0: none).  Invalid UTF-8 -> U+FFFD consuming one byte, as
+// utf8.DecodeRune.  Returns false at the end of the message.
+__device__ __forceinline__ bool utf16_next(const uint8_t* base, uint32_t off, uint32_t len, uint32_t& i,
+                                           uint32_t& pend, uint32_t& u) {
+  if (pend) { u = pend; pend = 0; return true; }
+  if (i >= len) return false;
+  const uint32_t x = lds4(base, off + i);
+  const uint32_t b0 = x & 255u, b1 = (x >> 8) & 255u, b2 = (x >> 16) & 255u, b3 = x >> 24;
+  uint32_t r = b0, sz = 1;
+  if (b0 >= 0x80u) {
+    r = 0xFFFDu;
+    uint32_t size = 0, lo = 0x80u, hi = 0xBFu;
+    if (b0 >= 0xC2u && b0 <= 0xDFu) size = 2;
+    else if (b0 >= 0xE0u && b0 <= 0xEFu) { size = 3; lo = b0 == 0xE0u ? 0xA0u : 0x80u; hi = b0 == 0xEDu ? 0x9Fu : 0xBFu; }
+    else if (b0 >= 0xF0u && b0 <= 0xF4u) { size = 4; lo = b0 == 0xF0u ? 0x90u : 0x80u; hi = b0 == 0xF4u ? 0x8Fu : 0xBFu; }
+    const bool c2 = b2 >= 0x80u && b2 <= 0xBFu, c3 = b3 >= 0x80u && b3 <= 0xBFu;
+    const bool ok = size && i + size <= len && b1 >= lo && b1 <= hi && (size < 3 || c2) && (size < 4 || c3);
+    if (ok) {
+      sz = size;
+      r = size == 2 ? ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu)
+        : size == 3 ? ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu)
+                    : ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
+    }
+  }
+  i += sz;
+  if (r >= 0x10000u) {
+    const uint32_t v = r - 0x10000u;
+    u = 0xD800u + (v >> 10);
+    pend = 0xDC00u + (v & 0x3FFu);
+  } else {
+    u = r;
+  }
+  return true;
+}
+
+// NTLM = MD4 over the UTF-16LE of the candidate's runes (Go []rune + utf16.Encode), the
+// units produced while each 64-byte message block is filled (no UTF-16 buffer, any
+// length).  Wave-collective loop: lanes whose digest is done keep their state.
+__device__ __forceinline__ void ntlm_lds(const uint8_t* base, uint32_t off, uint32_t len, uint32_t* d) {
+  uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  uint32_t i = 0, pend = 0, nu = 0;
+  bool padded = false, fin = false;
+  while (__builtin_amdgcn_ballot_w64(!fin)) {
+    uint32_t M[16];
+    const bool padprev = padded;
+    uint32_t padw = 16;  // message word of this block holding the 0x80 pad
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        uint32_t u = 0;
+        if (utf16_next(base, off, len, i, pend, u)) {
+          w |= u << (16 * h);
+          nu++;
+        } else if (!padded) {
+          w |= 0x80u << (16 * h);
+          padded = true;
+          padw = (uint32_t)j;
+        }
+      }
+      M[j] = w;
+    }
+    const bool last = padprev || (padded && padw <= 13u);
+    if (last) {  // 64-bit little-endian bit length: 16 bits per unit
+      M[14] = nu << 4;
+      M[15] = nu >> 28;
+    }
+    if (!fin) {
+      uint32_t s2[4] = {st[0], st[1], st[2], st[3]};
+      md4_block(s2, M);
+      st[0] = s2[0]; st[1] = s2[1]; st[2] = s2[2]; st[3] = s2[3];
+    }
+    fin = fin || last;
+  }
+  d[0] = st[0]; d[1] = st[1]; d[2] = st[2]; d[3] = st[3];
+}

@@ -170,20 +170,24 @@ def test_c5_shape_substitute_all_modes(mode, mn):
     _check(got, want, data, offs)
 
 
-def test_fused_md5_equals_two_pass():
-    """The fused MD5 path (k_expand_fast_md5: candidates hashed in the LDS ring) and the
-    two-pass path (HBM scratch + k_digest_stream) report the same hits."""
+@pytest.mark.parametrize("algo,wl,tabs", [(0, "c3", ["czech", "german"]), (1, "c3", ["czech", "german"]),
+                                         (1, "c5", ["greek-hebrew"])])
+def test_fused_equals_two_pass(algo, wl, tabs):
+    """The fused paths (k_expand_fast_md5 / k_expand_fast_ntlm: candidates hashed in the
+    LDS ring, NTLM's UTF-16LE produced while the MD4 blocks fill) and the two-pass path
+    (HBM scratch + k_digest_stream) report the same hits."""
     from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
     from oracle import digest_oracle as dg
-    _, (data, offs) = synth.global_words("c3", 0, 50_000, seed=0xF5)
+    _, (data, offs) = synth.global_words(wl, 0, 50_000, seed=0xF5)
     n = len(offs) - 1
     rng = np.random.default_rng(3)
+    f = dg.ALGOS[algo]
     with Context(0) as ctx:
-        ctx.load_tables([table_path("czech"), table_path("german")])
+        ctx.load_tables([table_path(t) for t in tabs])
         ws = sorted(set(int(x) for x in rng.choice(n, size=300, replace=False)))
         cands = ctx.expand_words([bytes(data[int(offs[i]):int(offs[i + 1])]) for i in ws], 0, 0, 15)
-        tg = [dg.md5(cs[int(rng.integers(0, len(cs)))]) for cs in cands if cs]
-        ctx.set_targets(0, b"".join(tg) + bytes(rng.integers(0, 256, 16 * 20000, dtype=np.uint8)))
+        tg = [f(cs[int(rng.integers(0, len(cs)))]) for cs in cands if cs]
+        ctx.set_targets(algo, b"".join(tg) + bytes(rng.integers(0, 256, 16 * 20000, dtype=np.uint8)))
         dw, do = DeviceBuffer.from_array(ctx, data), DeviceBuffer.from_array(ctx, offs)
         fused, st = ctx.expand_digest_device(dw.ptr, do.ptr, n, 0, 0, 15, hit_cap=1 << 14)
         os.environ["A5X_NO_FUSED_DIGEST"] = "1"
