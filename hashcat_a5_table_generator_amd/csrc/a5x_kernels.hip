@@ -1337,7 +1337,9 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #define FX6_ZBE FX_ZBE
 // window records: ring bytes [16, FX_RING) during the setup; the last u64 is the zero slot
 #define FX_RZ ((FX_RING - 16) / 8 - 1)
+#ifndef FX_K
 #define FX_K 4        // candidates per lane run (a5x_fx6.h)
+#endif
 #ifndef FX_PFM
 #define FX_PFM 1      // next window's metadata loaded before the current window's rounds
 #endif
@@ -1369,7 +1371,10 @@ struct FXWin {
   u32 mag[FB_RMAX + 4];    // fr_magic(R), R <= FB_RMAX
 };
 static_assert(FW_RMAX < FX_RZ && FB_EMAX < FX_ZBE, "a FAST record must fit a window");
-static_assert(FX_RING + FX_TRASH + sizeof(FXWin) <= 10240, "16 waves per CU need <= 10 KiB of LDS per wave");
+#ifndef FX_WPE
+#define FX_WPE 4  // 16 waves per CU: <= 128 VGPRs, <= 10 KiB LDS per wave
+#endif
+static_assert(FX_RING + FX_TRASH + sizeof(FXWin) <= 163840 / (4 * FX_WPE), "4 FX_WPE waves per CU must fit the 160 KiB of LDS");
 
 // Closed-form bytes of candidates [0, r) of a FAST word (candidate r <-> index r + 1
 // in the piece mixed radix, piece 0 least significant).  rec = the word's record
@@ -2011,9 +2016,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
 
 __device__ __forceinline__ u32 lds_per_wave_fast() { return (FX_RING + FX_TRASH + (u32)sizeof(FXWin) + 15u) & ~15u; }
 
-#ifndef FX_WPE
-#define FX_WPE 4  // 16 waves per CU: <= 128 VGPRs, <= 10 KiB LDS per wave
-#endif
 template <int DIG>
 __device__ __forceinline__ void expand_fast_body(const ExpArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];

@@ -102,7 +102,9 @@ A5X_HD u32 fastdiv_hd(u32 n, u32 magic, u32 shift) {
 #define FB_RMAX 64
 #define FB_SPAN 4    // small pieces per big piece
 #define FB_NMAX 4    // big pieces per word
+#ifndef FB_EMAX
 #define FB_EMAX 254  // big entries per word (window budget)
+#endif
 
 #define FW_M56 0x00FFFFFFFFFFFFFFull
 A5X_HD u64 fw_meta(u32 len, u32 R) { return (u64)(len | ((R - 1u) << 3)) << 56; }
