@@ -148,3 +148,7 @@ static_assert(sizeof(A5xMVal) == 8, "mval");
 #define A5X_M_CBUF 128    // candidate buffer per lane: candidates <= 127 bytes
 #define A5X_M_NMAX 63     // sorted patterns (-s) or match positions (-r) per word
 #define A5X_M_DPMAX 1024  // DP entries (patterns/positions + 1) x (count window + 1)
+// mode pass G (HBM scratch slots, a5x_modes.hip): words longer than A5X_M_LMAX, up to a
+// ScanLines line (main.go:72-74), with candidates of up to A5X_MG_CBUF - 1 bytes
+#define A5X_MG_LMAX 65535
+#define A5X_MG_CBUF (1u << 17)

@@ -89,6 +89,8 @@ struct a5x_ctx {
   DevBuf<uint64_t> m_nseg, m_seg_off, m_seg_bytes, m_seg_boff, m_tmp;
   DevBuf<uint32_t> m_item_w;
   uint64_t m_items = 0;
+  uint64_t m_nglob = 0;       // mode pass G words of the current batch (their list: glob)
+  uint8_t* mgscr = nullptr;   // mode pass G scratch: A5X_G_SLOTS x a5x_mode_gslot_bytes(), on first use
   uint64_t mseg = 1024;  // candidates per mode-engine item
   // fused digest + lookup (a5x_digest.hip)
   int t_algo = -1;
@@ -579,6 +581,8 @@ A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_
   M.seg_bytes = c->m_seg_bytes.p; M.seg_boff = c->m_seg_boff.p;
   M.cand_begin = 0; M.cand_end = ~0ull;
   M.err = c->d_scalars + 2;
+  M.glob_list = c->glob.p; M.glob_n = c->d_scalars + 7;
+  if (c->m_nglob) { M.gscr = c->mgscr; M.gslots = A5X_G_SLOTS; }
   return M;
 }
 
@@ -599,8 +603,9 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
                 "fatal error: stack overflow (generateCombinations with k < 0, main.go:273; --table-min %d)", mn);
   if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
       (rc = grow(c, c->m_nseg, nw + 1)) || (rc = grow(c, c->m_seg_off, nw + 1)) ||
-      (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)))
+      (rc = grow(c, c->glob, nw + 1)) || (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)))
     return rc;
+  c->m_nglob = 0;
   if (!d_cand_off) {
     if ((rc = grow(c, c->cand_off, nw + 1))) return rc;
     d_cand_off = c->cand_off.p;
@@ -628,8 +633,24 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
                             c->d_scalars + 2, st));
   HIPCHK(c, hipMemcpyAsync(c->h_totals, d_cand_off + nw, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipMemcpyAsync(c->h_totals + 1, c->m_seg_off.p + nw, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  if (c->h_scalars[2] == 0 && c->h_scalars[7] > 0) {
+    // mode pass G: words longer than the LDS engines take are counted in HBM scratch
+    // slots (their counts were 0 in the first scan), then the scan runs again
+    if (!c->mgscr) {
+      HIPCHK(c, hipMalloc((void**)&c->mgscr, (size_t)A5X_G_SLOTS * a5x_mode_gslot_bytes()));
+    }
+    c->m_nglob = c->h_scalars[7];
+    M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx);
+    HIPCHK(c, a5x_launch_mode_count_g(M, st));
+    HIPCHK(c, a5x_launch_scan(c->count.p, c->m_nseg.p, nw, d_cand_off, c->m_seg_off.p, c->scan_tmp.p,
+                              c->d_scalars + 2, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_totals, d_cand_off + nw, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_totals + 1, c->m_seg_off.p + nw, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+  }
   auto name_word = [&]() {
     std::vector<uint32_t> fl(nw);
     std::vector<uint64_t> wo(nw + 1);
@@ -1003,6 +1024,7 @@ void a5x_destroy(a5x_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   release(c->glob);
+  if (c->mgscr) (void)hipFree(c->mgscr);
   if (c->gscr) (void)hipFree(c->gscr);
   if (c->sstream) (void)hipStreamSynchronize(c->sstream);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);

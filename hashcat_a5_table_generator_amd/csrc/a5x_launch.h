@@ -123,9 +123,17 @@ struct A5xModeLaunch {
   uint8_t* out;
   uint64_t out_base, out_cap;
   uint32_t* err;
+  // mode pass G: words longer than A5X_M_LMAX (flag A5X_WF_GLOB), listed by k_mode_count,
+  // run by one wave per HBM scratch slot (gslots x a5x_mode_gslot_bytes(); gscr null: none)
+  uint32_t* glob_list;
+  uint32_t* glob_n;
+  uint8_t* gscr;
+  uint32_t gslots;
 };
 size_t a5x_mode_lds(uint32_t mtab_bytes);
+uint64_t a5x_mode_gslot_bytes();
 hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st);
+hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st);
 // op 0: per-item output bytes (seg_bytes); op 1: expand items [item_begin, item_end)
 hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st);
 // out[3q..3q+2] = {item, index in item, byte offset} of global candidate cands[q]

@@ -60,17 +60,22 @@ constexpr u32 M_ERR_STATE = 1u << 3;
 constexpr u32 M_ERR_GUARD = 1u << 5;
 constexpr u32 M_ERR_LIMIT = 1u << 6;  // word beyond the mode-engine limits
 constexpr u32 M_ERR_PANIC = 1u << 7;  // -r slice-bounds panic (main.go:255)
-constexpr u32 M_ERR_CLEN = 1u << 8;   // a candidate longer than A5X_M_CBUF-1
+constexpr u32 M_ERR_CLEN = 1u << 8;   // a candidate longer than the lane buffer
+constexpr u32 M_ERR_GWORD = 1u << 30; // (not an error) word longer than A5X_M_LMAX: mode pass G
 
-constexpr u32 LSTRIDE = A5X_M_CBUF + 4;
-constexpr u32 CMAXLEN = A5X_M_CBUF - 1;
 
 // positional -s / -s -r words (m_pos_setup): entries (a5x_ring.h) and the token list
 constexpr u32 MP_NE = 256;    // entries per word: per pattern [keep, values...], then literal chunks
 constexpr u32 MP_PMAX = 16;   // patterns per word (4-bit selector per pattern)
 constexpr u32 MP_VMAX = 14;   // values per pattern (selector 1 + v <= 15)
 
-struct MLds {
+// Per-wave state of one word: LDS (MLds), or an HBM scratch slot for the words of
+// mode pass G (MLdsG: lines up to 64 KiB, candidates up to A5X_MG_CBUF - 1 bytes; the
+// positional engine, which places through LDS addresses, is not used there).
+template <u32 LMAX, u32 CBUF>
+struct MLdsT {
+  static constexpr u32 L_MAX = LMAX, STRIDE = CBUF + 4, CMAXLEN = CBUF - 1;
+  static constexpr bool G = LMAX > A5X_M_LMAX;
   u64 dp[A5X_M_DPMAX];
   uint4 ent[MP_NE];
   u32 tok[A5X_M_LMAX + 2];   // entry base | (pattern index + 1) << 16 (0: literal chunk)
@@ -81,11 +86,27 @@ struct MLds {
   uint8_t rr[MP_PMAX];       // R_r
   u32 ntok, radix, shift;
   u32 bitmap[A5X_MTAB_KEYS_MAX / 32];
-  uint8_t word[A5X_M_LMAX + 16];
+  uint8_t word[LMAX + 16];
   uint16_t pat[64];          // key index per sorted pattern (-s) / per position (-r)
-  uint8_t pst[64], pnx[64];  // -r: start byte, first later compatible position
-  uint8_t buf[2][64 * LSTRIDE];
+  uint16_t pst[64];          // -r: start byte
+  uint8_t pnx[64];           // -r: first later compatible position
+  uint8_t buf[2][64 * STRIDE];
 };
+typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF> MLds;
+typedef MLdsT<A5X_MG_LMAX, A5X_MG_CBUF> MLdsG;
+
+// wave sync over the word state: LDS, or (pass G) HBM written and read by the wave's own
+// lanes -- workgroup-scope release / acquire drains and orders those global accesses
+template <class SL>
+__device__ __forceinline__ void m_sync() {
+  if constexpr (SL::G) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    M_WAVE_SYNC();
+  }
+}
 
 struct MT {
   const A5xMHdr* h;
@@ -178,7 +199,7 @@ __device__ __forceinline__ u32 m_rune_len(const uint8_t* s, u32 n) {
 // strings.ReplaceAll(src[:n], p, v) into dst; returns the length (err |= CLEN when
 // the result does not fit the lane buffer)
 __device__ u32 m_replace_all(const uint8_t* src, u32 n, const uint8_t* p, u32 pl, const uint8_t* v, u32 vl,
-                             uint8_t* dst, u32& err) {
+                             uint8_t* dst, u32& err, const u32 CMAXLEN) {
   u32 o = 0;
   if (pl == 0) {  // "" matches before every rune and at the end
     if (vl > CMAXLEN) { err |= M_ERR_CLEN; return 0; }
@@ -212,24 +233,25 @@ __device__ u32 m_replace_all(const uint8_t* src, u32 n, const uint8_t* p, u32 pl
 
 // Per-word setup (wave-uniform result): word -> LDS, the pattern / position list,
 // the DP table and the count.
-__device__ MInfo m_setup(MLds& S, const MT& T, const A5xModeLaunch& a, u64 w) {
+template <class SL>
+__device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
   const u32 lane = m_lane();
   MInfo I;
   I.L = I.n = I.cmin = I.cmax = I.cols = 0;
   I.count = 0;
   I.bad = 0;
   const u64 w0 = a.woff[w], w1 = a.woff[w + 1];
-  if (w1 - w0 > A5X_M_LMAX) { I.bad = M_ERR_LIMIT; return I; }
+  if (w1 - w0 > SL::L_MAX) { I.bad = w1 - w0 <= A5X_MG_LMAX ? M_ERR_GWORD : M_ERR_LIMIT; return I; }
   const u32 L = (u32)(w1 - w0);
   I.L = L;
-  M_WAVE_SYNC();  // previous item's readers of S are done
+  m_sync<SL>();  // previous item's readers of S are done
   for (u32 i = lane; i < L; i += 64) S.word[i] = a.words[w0 + i];
-  M_WAVE_SYNC();
+  m_sync<SL>();
   u32 n = 0;
   if (a.mode == A5X_MODE_REVERSE) {
     // positions in (start, keyLength) order (main.go:215-226): starts q = lane, lane+64
-    for (u32 half = 0; half < 2; half++) {
-      const u32 q = half * 64 + lane;
+    for (u32 q0 = 0; q0 < L; q0 += 64) {
+      const u32 q = q0 + lane;
       u32 k0 = 0, k1 = 0, m = 0;
       if (q < L) {
         const u32 b = S.word[q];
@@ -242,11 +264,11 @@ __device__ MInfo m_setup(MLds& S, const MT& T, const A5xModeLaunch& a, u64 w) {
       u32 o = n + incl - m;
       if (n + tot <= A5X_M_NMAX && m)
         for (u32 k = k0; k < k1; k++)
-          if (m_match(T, S.word, L, q, k)) { S.pat[o] = (uint16_t)k; S.pst[o] = (uint8_t)q; o++; }
+          if (m_match(T, S.word, L, q, k)) { S.pat[o] = (uint16_t)k; S.pst[o] = (uint16_t)q; o++; }
       n += tot;
     }
     if (n > A5X_M_NMAX) { I.bad = M_ERR_LIMIT; return I; }
-    M_WAVE_SYNC();
+    m_sync<SL>();
     if (lane < n) {
       const u32 end = S.pst[lane] + T.keys[S.pat[lane]].klen;
       u32 nx = n;
@@ -258,16 +280,21 @@ __device__ MInfo m_setup(MLds& S, const MT& T, const A5xModeLaunch& a, u64 w) {
     // unique patterns present (main.go:312-319), sorted = increasing key index
     const u32 nk = T.h->nkeys, nwd = (nk + 31) / 32;
     for (u32 i = lane; i < nwd; i += 64) S.bitmap[i] = 0;
-    M_WAVE_SYNC();
+    m_sync<SL>();
     for (u32 q = lane; q < L; q += 64) {
       const u32 b = S.word[q];
       for (u32 k = T.bucket[b]; k < T.bucket[b + 1]; k++)
         if (m_match(T, S.word, L, q, k)) atomicOr(&S.bitmap[k >> 5], 1u << (k & 31));
     }
     if (T.h->has_empty && L > 0 && lane == 0) atomicOr(&S.bitmap[0], 1u);
-    M_WAVE_SYNC();
-    const u32 d0 = 2 * lane < nwd ? S.bitmap[2 * lane] : 0u;
-    const u32 d1 = 2 * lane + 1 < nwd ? S.bitmap[2 * lane + 1] : 0u;
+    m_sync<SL>();
+    // (pass G: the bitmap was built by L2 atomics; read it from L2, not a stale L1 line)
+    auto bm = [&](u32 i) -> u32 {
+      if constexpr (SL::G) return __hip_atomic_load(&S.bitmap[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else return S.bitmap[i];
+    };
+    const u32 d0 = 2 * lane < nwd ? bm(2 * lane) : 0u;
+    const u32 d1 = 2 * lane + 1 < nwd ? bm(2 * lane + 1) : 0u;
     const u32 m = (u32)__builtin_popcount(d0) + (u32)__builtin_popcount(d1);
     const u32 incl = m_incl_scan(m);
     n = (u32)__builtin_amdgcn_readlane((int)incl, 63);
@@ -284,13 +311,13 @@ __device__ MInfo m_setup(MLds& S, const MT& T, const A5xModeLaunch& a, u64 w) {
   const u32 cols = cmax + 1;
   if ((n + 1) * cols > A5X_M_DPMAX) { I.bad = M_ERR_LIMIT; return I; }
   I.cmin = cmin; I.cmax = cmax; I.cols = cols;
-  M_WAVE_SYNC();
+  m_sync<SL>();
   u64* D = S.dp;
   const u32 c = lane;
   if (c < cols) D[n * cols + c] = c == 0 ? 1ull : 0ull;
   u32 ovf = 0;
   for (int r = (int)n - 1; r >= 0; r--) {
-    M_WAVE_SYNC();
+    m_sync<SL>();
     if (c < cols) {
       u64 x = D[(r + 1) * cols + c];
       if (c > 0) {
@@ -307,7 +334,7 @@ __device__ MInfo m_setup(MLds& S, const MT& T, const A5xModeLaunch& a, u64 w) {
       D[r * cols + c] = x;
     }
   }
-  M_WAVE_SYNC();
+  m_sync<SL>();
   u64 cnt = 0;
   for (u32 k = cmin; k <= cmax; k++)
     if (__builtin_add_overflow(cnt, D[k], &cnt)) ovf = 1;
@@ -318,11 +345,13 @@ __device__ MInfo m_setup(MLds& S, const MT& T, const A5xModeLaunch& a, u64 w) {
 
 // Build candidate t (0 <= t < count) of the word set up in S into this lane's
 // buffer; returns its length and the buffer holding it.
-__device__ u32 m_build(MLds& S, const MT& T, const MInfo& I, int mode, u64 t, const uint8_t** outp, u32& err,
+template <class SL>
+__device__ u32 m_build(SL& S, const MT& T, const MInfo& I, int mode, u64 t, const uint8_t** outp, u32& err,
                        bool len_only = false) {
   const u32 lane = m_lane();
-  uint8_t* b0 = S.buf[0] + lane * LSTRIDE;
-  uint8_t* b1 = S.buf[1] + lane * LSTRIDE;
+  constexpr u32 CMAXLEN = SL::CMAXLEN;
+  uint8_t* b0 = S.buf[0] + lane * SL::STRIDE;
+  uint8_t* b1 = S.buf[1] + lane * SL::STRIDE;
   const u64* D = S.dp;
   const u32 cols = I.cols, n = I.n;
   u32 c = I.cmin;
@@ -396,7 +425,7 @@ __device__ u32 m_build(MLds& S, const MT& T, const MInfo& I, int mode, u64 t, co
       t -= (u64)v * b;
     }
     const A5xMVal V = T.vals[K.val_base + v];
-    len = m_replace_all(src, len, T.blob + K.key_off, K.klen, T.blob + V.off, V.len, dst, err);
+    len = m_replace_all(src, len, T.blob + K.key_off, K.klen, T.blob + V.off, V.len, dst, err, CMAXLEN);
     src = dst;
     dst = dst == b0 ? b1 : b0;
     c--;
@@ -448,7 +477,7 @@ __device__ __forceinline__ uint4 m_entry(const uint8_t* p, u32 n) {
 // returns the token count, or 0 when the word is not positional (byte builder path).
 __device__ u32 m_pos_setup(MLds& S, const MT& T, const MInfo& I, int mode) {
   const u32 lane = m_lane(), n = I.n, L = I.L;
-  if (n == 0 || n > MP_PMAX) return 0;
+  if (n == 0 || n > MP_PMAX || L > A5X_M_LMAX) return 0;
   u32 ok = 1, ne = 0;
   if (lane < n) {
     const A5xMKey K = T.keys[S.pat[lane]];
@@ -680,26 +709,48 @@ __device__ __forceinline__ void m_err(u32* e, u32 bits) {
 
 extern __shared__ __attribute__((aligned(16))) uint8_t m_dyn[];
 
+// per-word count, segments and flags of a set-up word
+template <class SL>
+__device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
+  const MInfo I = m_setup(S, T, a, w);
+  const bool gw = I.bad == M_ERR_GWORD;  // (LDS pass only) routed to mode pass G
+  if (m_lane() == 0) {
+    const u64 cnt = I.bad ? 0 : I.count;
+    a.count[w] = cnt;
+    a.nseg[w] = (cnt + a.SEG - 1) / a.SEG;
+    a.flags[w] = gw ? A5X_WF_GLOB : I.bad == M_ERR_OVF ? A5X_WF_ERR_OVF : (I.bad ? A5X_WF_ERR_BIG : 0u);
+    if (SL::G) a.flags[w] |= A5X_WF_GLOB;
+    if (gw) {
+      const u32 k = atomicAdd(a.glob_n, 1u);
+      a.glob_list[k] = (u32)w;
+    }
+  }
+  m_err(a.err, gw ? 0u : I.bad);
+}
+
 // one wave per word: count, segments, per-word error flags
 __global__ void __launch_bounds__(64) k_mode_count(A5xModeLaunch a) {
   MLds& S = *(MLds*)m_dyn;
   const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
-  for (u64 w = blockIdx.x; w < a.nw; w += gridDim.x) {
-    const MInfo I = m_setup(S, T, a, w);
-    if (m_lane() == 0) {
-      const u64 cnt = I.bad ? 0 : I.count;
-      a.count[w] = cnt;
-      a.nseg[w] = (cnt + a.SEG - 1) / a.SEG;
-      a.flags[w] = I.bad == M_ERR_OVF ? A5X_WF_ERR_OVF : (I.bad ? A5X_WF_ERR_BIG : 0u);
-    }
-    m_err(a.err, I.bad);
-  }
+  for (u64 w = blockIdx.x; w < a.nw; w += gridDim.x) m_count_word(S, T, a, w);
+}
+
+// mode pass G: one wave per HBM scratch slot over the listed words
+__device__ __forceinline__ MLdsG& m_gslot(const A5xModeLaunch& a) {
+  return *(MLdsG*)(a.gscr + (u64)blockIdx.x * ((sizeof(MLdsG) + 255) & ~(size_t)255));
+}
+__global__ void __launch_bounds__(64) k_mode_count_g(A5xModeLaunch a) {
+  MLdsG& S = m_gslot(a);
+  const MT T = m_table(m_dyn, a.mtab, a.mtab_bytes);
+  const u32 ng = *a.glob_n;
+  for (u32 i = blockIdx.x; i < ng; i += gridDim.x) m_count_word(S, T, a, a.glob_list[i]);
 }
 
 // Run the candidates [t0, t0 + nc) of the set-up word: op 0 = sum of (len+1),
 // op 1 = write them at out[base + prefix - out_base] when their global index
 // (g0 + t) is inside [cand_begin, cand_end).
-__device__ u64 m_run(MLds& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 t0, u32 nc, int op,
+template <class SL>
+__device__ u64 m_run(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 t0, u32 nc, int op,
                      u64 g0, u64 base, u32& err, u32 ntok = 0) {
   const u32 lane = m_lane();
   u64 run = 0;
@@ -708,11 +759,14 @@ __device__ u64 m_run(MLds& S, const MT& T, const MInfo& I, const A5xModeLaunch& 
     const bool v = k < nc;
     const uint8_t* p = nullptr;
     u32 len = 0;
-    if (v && ntok && op == 0) {  // positional word: the length formula
-      u64 sel;
-      len = m_pos_sel(S, T, I, a.mode, t0 + k, sel) + 1;
-      if (len > A5X_M_CBUF) { err |= M_ERR_CLEN; len = 0; }
-    } else if (v) {
+    if constexpr (!SL::G) {
+      if (v && ntok && op == 0) {  // positional word: the length formula
+        u64 sel;
+        len = m_pos_sel(S, T, I, a.mode, t0 + k, sel) + 1;
+        if (len > A5X_M_CBUF) { err |= M_ERR_CLEN; len = 0; }
+      }
+    }
+    if (v && !(ntok && op == 0)) {
       len = m_build(S, T, I, a.mode, t0 + k, &p, err, op == 0 && a.mode == A5X_MODE_REVERSE) + 1;
     }
     const u32 incl = m_incl_scan(len);
@@ -735,20 +789,19 @@ __device__ u64 m_run(MLds& S, const MT& T, const MInfo& I, const A5xModeLaunch& 
   return run;
 }
 
-// one wave per item (word, SEG-candidate segment): op 0 = seg_bytes, op 1 = expand
-__global__ void __launch_bounds__(64) k_mode_items(A5xModeLaunch a, int op) {
-  MLds& S = *(MLds*)m_dyn;
-  const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
-  for (u64 i = a.item_begin + blockIdx.x; i < a.item_end; i += gridDim.x) {
-    const u64 w = a.item_w[i];
-    const u64 cw0 = a.cand_off[w], cnt = a.cand_off[w + 1] - cw0;
-    const u64 t0 = (i - a.seg_off[w]) * a.SEG;
-    if (t0 >= cnt) { m_err(a.err, M_ERR_STATE); continue; }
-    const u32 nc = (u32)min(a.SEG, cnt - t0);
-    const MInfo I = m_setup(S, T, a, w);
-    if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); continue; }
-    const u32 ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
-    u32 err = 0;
+// item i (word, SEG-candidate segment): op 0 = seg_bytes, op 1 = expand
+template <class SL>
+__device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op) {
+  const u64 w = a.item_w[i];
+  const u64 cw0 = a.cand_off[w], cnt = a.cand_off[w + 1] - cw0;
+  const u64 t0 = (i - a.seg_off[w]) * a.SEG;
+  if (t0 >= cnt) { m_err(a.err, M_ERR_STATE); return; }
+  const u32 nc = (u32)min(a.SEG, cnt - t0);
+  const MInfo I = m_setup(S, T, a, w);
+  if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
+  u32 err = 0, ntok = 0;
+  if constexpr (!SL::G) {
+    ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
     if (ntok && op == 1) {
       // the leaves of this item inside [cand_begin, cand_end); the first one's bytes start
       // at seg_boff[i] (or at out_base itself when the range starts inside the item)
@@ -757,50 +810,90 @@ __global__ void __launch_bounds__(64) k_mode_items(A5xModeLaunch a, int op) {
       const u64 tb = rb > t0 ? rb : t0;
       if (a.cand_end > cw0 && tb < re)
         m_pos_expand(S, T, I, a, tb, re, tb == t0 ? a.seg_boff[i] - a.out_base : 0, ntok, err);
-    } else if (ntok && S.radix) {  // op 0, radix mode: closed form, no candidate is visited
+      m_err(a.err, m_wave_or(err));
+      return;
+    }
+    if (ntok && S.radix) {  // op 0, radix mode: closed form, no candidate is visited
       const u64 run = m_pos_prefix(S, I, t0 + nc) - m_pos_prefix(S, I, t0);
       if (m_lane() == 0) a.seg_bytes[i] = run;
-    } else {
-      const u64 base = op == 1 ? a.seg_boff[i] : 0;
-      const u64 run = m_run(S, T, I, a, t0, nc, op, cw0, base, err, ntok);
-      if (op == 0 && m_lane() == 0) a.seg_bytes[i] = run;
+      return;
     }
-    m_err(a.err, m_wave_or(err));
+  }
+  const u64 base = op == 1 ? a.seg_boff[i] : 0;
+  const u64 run = m_run(S, T, I, a, t0, nc, op, cw0, base, err, ntok);
+  if (op == 0 && m_lane() == 0) a.seg_bytes[i] = run;
+  m_err(a.err, m_wave_or(err));
+}
+
+// one wave per item; the items of pass-G words are left to k_mode_items_g
+__global__ void __launch_bounds__(64) k_mode_items(A5xModeLaunch a, int op) {
+  MLds& S = *(MLds*)m_dyn;
+  const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
+  for (u64 i = a.item_begin + blockIdx.x; i < a.item_end; i += gridDim.x) {
+    if (a.flags[a.item_w[i]] & A5X_WF_GLOB) continue;
+    m_item(S, T, a, i, op);
   }
 }
 
-// one wave per query g: {item containing g, index inside the item, byte offset of g}
+// the items of the listed pass-G words inside [item_begin, item_end), dealt to the slots
+__global__ void __launch_bounds__(64) k_mode_items_g(A5xModeLaunch a, int op) {
+  MLdsG& S = m_gslot(a);
+  const MT T = m_table(m_dyn, a.mtab, a.mtab_bytes);
+  const u32 ng = *a.glob_n;
+  for (u32 k = 0; k < ng; k++) {
+    const u64 w = a.glob_list[k];
+    const u64 i0 = max(a.seg_off[w], a.item_begin), i1 = min(a.seg_off[w + 1], a.item_end);
+    for (u64 i = i0; i < i1; i++)
+      if ((i + k) % gridDim.x == blockIdx.x) m_item(S, T, a, i, op);
+  }
+}
+
+// query q: {item containing g, index inside the item, byte offset of g}; G: only the
+// queries inside pass-G words (the LDS pass skips those)
+template <class SL>
+__device__ void m_locate(SL& S, const MT& T, const A5xModeLaunch& a, const u64* cands, u32 q, u64* out) {
+  const u64 g = cands[q];
+  const u64 total = a.cand_off[a.nw];
+  if (g >= total) {
+    if (!SL::G && m_lane() == 0) { out[3 * q] = a.nitems; out[3 * q + 1] = 0; out[3 * q + 2] = a.seg_boff[a.nitems]; }
+    return;
+  }
+  u64 lo = 0, hi = a.nw;  // largest w with cand_off[w] <= g
+  while (hi - lo > 1) {
+    const u64 mid = (lo + hi) / 2;
+    if (a.cand_off[mid] <= g) lo = mid; else hi = mid;
+  }
+  const u64 w = lo, local = g - a.cand_off[w];
+  if (((a.flags[w] & A5X_WF_GLOB) != 0) != SL::G) return;
+  const u64 item = a.seg_off[w] + local / a.SEG;
+  const u64 t0 = (local / a.SEG) * a.SEG;
+  const u32 r = (u32)(local - t0);
+  u64 pre = 0;
+  if (r) {
+    const MInfo I = m_setup(S, T, a, w);
+    if (I.bad || I.count != a.cand_off[w + 1] - a.cand_off[w]) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
+    u32 err = 0, ntok = 0;
+    if constexpr (!SL::G) {
+      ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
+      if (ntok && S.radix) pre = m_pos_prefix(S, I, t0 + r) - m_pos_prefix(S, I, t0);
+    }
+    if (!(ntok && S.radix)) pre = m_run(S, T, I, a, t0, r, 0, 0, 0, err, ntok);
+    m_err(a.err, m_wave_or(err));
+  }
+  if (m_lane() == 0) { out[3 * q] = item; out[3 * q + 1] = r; out[3 * q + 2] = a.seg_boff[item] + pre; }
+}
+
+// one wave per query g
 __global__ void __launch_bounds__(64) k_mode_locate(A5xModeLaunch a, const u64* cands, u32 nq, u64* out) {
   MLds& S = *(MLds*)m_dyn;
   const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
-  for (u32 q = blockIdx.x; q < nq; q += gridDim.x) {
-    const u64 g = cands[q];
-    const u64 total = a.cand_off[a.nw];
-    if (g >= total) {
-      if (m_lane() == 0) { out[3 * q] = a.nitems; out[3 * q + 1] = 0; out[3 * q + 2] = a.seg_boff[a.nitems]; }
-      continue;
-    }
-    u64 lo = 0, hi = a.nw;  // largest w with cand_off[w] <= g
-    while (hi - lo > 1) {
-      const u64 mid = (lo + hi) / 2;
-      if (a.cand_off[mid] <= g) lo = mid; else hi = mid;
-    }
-    const u64 w = lo, local = g - a.cand_off[w];
-    const u64 item = a.seg_off[w] + local / a.SEG;
-    const u64 t0 = (local / a.SEG) * a.SEG;
-    const u32 r = (u32)(local - t0);
-    u64 pre = 0;
-    if (r) {
-      const MInfo I = m_setup(S, T, a, w);
-      if (I.bad || I.count != a.cand_off[w + 1] - a.cand_off[w]) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); continue; }
-      u32 err = 0;
-      const u32 ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
-      if (ntok && S.radix) pre = m_pos_prefix(S, I, t0 + r) - m_pos_prefix(S, I, t0);
-      else pre = m_run(S, T, I, a, t0, r, 0, 0, 0, err, ntok);
-      m_err(a.err, m_wave_or(err));
-    }
-    if (m_lane() == 0) { out[3 * q] = item; out[3 * q + 1] = r; out[3 * q + 2] = a.seg_boff[item] + pre; }
-  }
+  for (u32 q = blockIdx.x; q < nq; q += gridDim.x) m_locate(S, T, a, cands, q, out);
+}
+
+__global__ void __launch_bounds__(64) k_mode_locate_g(A5xModeLaunch a, const u64* cands, u32 nq, u64* out) {
+  MLdsG& S = m_gslot(a);
+  const MT T = m_table(m_dyn, a.mtab, a.mtab_bytes);
+  for (u32 q = blockIdx.x; q < nq; q += gridDim.x) m_locate(S, T, a, cands, q, out);
 }
 
 // per-word byte offsets / bytes from the per-item byte offsets
@@ -820,8 +913,15 @@ inline u32 m_grid(u64 n, u32 cap) { return (u32)(n < 1 ? 1 : (n < cap ? n : cap)
 
 size_t a5x_mode_lds(uint32_t mtab_bytes) { return sizeof(MLds) + ((mtab_bytes + 15u) & ~15u); }
 
+uint64_t a5x_mode_gslot_bytes() { return (sizeof(MLdsG) + 255) & ~(size_t)255; }
+
 hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st) {
   hipLaunchKernelGGL(k_mode_count, dim3(m_grid(L.nw, 1u << 18)), dim3(64), a5x_mode_lds(L.mtab_bytes), st, L);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st) {
+  hipLaunchKernelGGL(k_mode_count_g, dim3(L.gslots), dim3(64), (L.mtab_bytes + 15u) & ~15u, st, L);
   return hipGetLastError();
 }
 
@@ -829,12 +929,17 @@ hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st)
   if (L.item_end <= L.item_begin) return hipSuccess;
   hipLaunchKernelGGL(k_mode_items, dim3(m_grid(L.item_end - L.item_begin, 1u << 18)), dim3(64),
                      a5x_mode_lds(L.mtab_bytes), st, L, op);
+  if (L.gscr && L.gslots)
+    hipLaunchKernelGGL(k_mode_items_g, dim3(L.gslots), dim3(64), (L.mtab_bytes + 15u) & ~15u, st, L, op);
   return hipGetLastError();
 }
 
 hipError_t a5x_launch_mode_locate(const A5xModeLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out,
                                   hipStream_t st) {
   hipLaunchKernelGGL(k_mode_locate, dim3(m_grid(n, 64)), dim3(64), a5x_mode_lds(L.mtab_bytes), st, L, cands, n, out);
+  if (L.gscr && L.gslots)
+    hipLaunchKernelGGL(k_mode_locate_g, dim3(L.gslots < n ? L.gslots : (n ? n : 1)), dim3(64),
+                       (L.mtab_bytes + 15u) & ~15u, st, L, cands, n, out);
   return hipGetLastError();
 }
 

@@ -119,3 +119,50 @@ def test_pass_g_mixed_batch_ranges(gpu_ctx):
         pos += s2["bytes"]
     assert pos == tb
     assert bytes(np.concatenate(parts)) == bytes(ref)
+
+
+def _c_oracle_words_mode(tabs, words, mode, mn, mx):
+    from oracle import c_oracle as co
+    t = co.CTable([table_path(x) for x in tabs])
+    data, offs = co.pack_words(words)
+    out, wb = t.expand_batch(data, offs, mode, mn, mx)
+    res, pos = [], 0
+    for b in wb:
+        seg = out[pos:pos + int(b)]
+        pos += int(b)
+        res.append(sorted(seg.split(b"\n")[:-1]) if seg else [])
+    return res
+
+
+def _mode_long_words():
+    rng = np.random.default_rng(129)
+    words = [_word(rng, L, k, keys=b"aesz") for L, k in ((129, 8), (200, 11), (1000, 6), (5000, 4), (65535, 3),
+                                                          (3000, 0))]
+    words.append(b"x" * 40000 + b"strasse" + b"w" * 100)  # "s" / "ss" patterns far into a long line
+    words += [b"strasse", b"abc", b"", b"zebra"]           # short words in the same batch (LDS engines)
+    return words
+
+
+@pytest.mark.parametrize("mode,mn,mx", [(1, 0, 15), (2, 0, 15), (3, 0, 15), (1, 2, 2), (2, 1, 1), (3, 2, 3)])
+def test_mode_long_lines_vs_c_oracle(mode, mn, mx):
+    """-r / -s / -s -r on lines longer than the LDS engines' 128 B (mode pass G: word state
+    and lane buffers in HBM scratch slots) == the C oracle per word, with small items
+    (A5X_MSEG=64: a G word spans many items over all slots) and small host ranges (range
+    starts located inside G words)."""
+    import os
+    from hashcat_a5_table_generator_amd import Context
+    words = _mode_long_words()
+    os.environ["A5X_MSEG"] = "64"
+    os.environ["A5X_HOST_CHUNK_BYTES"] = "200000"
+    try:
+        c = Context(0)
+    finally:
+        os.environ.pop("A5X_MSEG")
+        os.environ.pop("A5X_HOST_CHUNK_BYTES")
+    c.load_tables([table_path("czech"), table_path("german")])
+    got = [sorted(x) for x in c.expand_words(words, mode, mn, mx)]
+    c.close()
+    want = _c_oracle_words_mode(["czech", "german"], words, mode, mn, mx)
+    assert sum(len(x) for x in want[:7]) > 0
+    for w, g, e in zip(words, got, want):
+        assert len(g) == len(e) and g == e, (len(w), mode, mn, mx, len(g), len(e))
