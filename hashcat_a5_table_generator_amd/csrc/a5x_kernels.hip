@@ -284,7 +284,9 @@ __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const
 // at q, make the word "complex": k_keyspace_cplx walks it with next_unit.
 // ulog (count pass only): the lane's lone units as (q << 10 | key) at ulog[i * 256];
 // nlog = their number, KS_ULOG + 1 when they do not fit (the build pass re-walks).
+#ifndef KS_ULOG
 #define KS_ULOG 16
+#endif
 template <bool COUNT, class PL>
 __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 Lmax, u32 bmax, const Tab& T,
                                          PL& pl, CountAcc& A, bool& cplx, uint16_t* ulog = nullptr,

@@ -151,3 +151,29 @@ def test_lookup_with_a_full_32_bit_prefilter(gpu_ctx, monkeypatch):
     hits, _ = gpu_ctx.expand_digest(*pack_words(words), 0, 0, 15)
     got = {(w, c) for w, c, _ in hits}
     assert set(pl) <= got
+
+
+def test_fused_ntlm_multi_block_candidates(gpu_ctx):
+    """Fused NTLM (k_expand_fast_ntlm) on candidates of 20-64 UTF-16 units: MD4 message
+    blocks past the first (the 0x80 pad and the bit length in a second / third block),
+    2-byte and 4-byte UTF-8 (surrogate pairs) and invalid bytes (U+FFFD), bit-exact vs the
+    RFC 1320 restatement over Go's UTF-16LE."""
+    from hashcat_a5_table_generator_amd import pack_words
+    from oracle import digest_oracle as dg
+    gpu_ctx.clear_table()
+    gpu_ctx.load_tables([table_path("czech")])
+    # FAST words (the fused path needs every candidate-bearing word FAST: <= 8 pieces)
+    words = [b"x" * n + b"a" for n in range(19, 48)]                 # 20-48 units: pads in block 1 / 2
+    words += [("β" * n + "a").encode() for n in range(10, 24)]       # 2-byte UTF-8
+    words += [("😀" * n + "ea").encode() for n in range(5, 12)]      # surrogate pairs, 12-24 units
+    words += [b"\xff\xfe" * 10 + b"ae", b"\xce" + b"q" * 30 + b"e"]  # invalid UTF-8 -> U+FFFD
+    per_word = gpu_ctx.expand_words(words, 0, 0, 15)
+    assert all(per_word)
+    targets = {dg.ntlm(c): (w, i) for w, cs in enumerate(per_word) for i, c in enumerate(cs)}
+    gpu_ctx.set_targets(1, b"".join(targets))
+    hits, st = gpu_ctx.expand_digest(*pack_words(words), 0, 0, 15)
+    assert st["ms_total"] - st["ms_keyspace"] - st["ms_expand"] < 1e-3  # the fused path ran
+    got = {(w, c) for w, c, _ in hits}
+    assert got == {(w, i) for w, cs in enumerate(per_word) for i in range(len(cs))}
+    for w, c, d in hits:
+        assert dg.ntlm(per_word[w][c]) == d
