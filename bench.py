@@ -159,6 +159,7 @@ def digest_profile(algo: str, words: int, kernel: str):
             continue
         if (d.get("algo") == algo and d.get("words") == words and d.get("kernel_src_sha") == sha
                 and d.get("kernel") == kernel):
+            d["_file"] = os.path.relpath(f, ROOT)
             return d
     return None
 
@@ -257,10 +258,10 @@ def digest_roofline(args, tc, ms_dig, ms_exp):
     ops per candidate from the committed PMC profile of these sources x candidates /
     stage time); peak = 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz 32-bit VALU ops (a
     wave64 VALU instruction issues over 2 cycles: MI355X_MICROARCH.md; = the 157.3 TF f32
-    FMA peak / 2).  Fused path (MD5, all-FAST batch): k_expand_fast_md5 expands, hashes
-    and probes in one kernel, so the stage time is the expansion time."""
+    FMA peak / 2).  Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm
+    expand, hash and probe in one kernel, so the stage time is the expansion time."""
     fused = ms_dig < 1e-3
-    kernel = "k_expand_fast_md5" if fused else "k_digest_stream"
+    kernel = f"k_expand_fast_{args.digest}" if fused else "k_digest_stream"
     ms_stage = ms_exp if fused else ms_dig
     prof = digest_profile(args.digest, args.words, kernel)
     peak = 256 * 4 * 32 * 2.4e9 / 1e12  # Tops/s
@@ -272,7 +273,7 @@ def digest_roofline(args, tc, ms_dig, ms_exp):
         ach = prof["int_ops_per_cand"] * tc / (ms_stage * 1e-3) / 1e12
         r.update(achieved=ach, frac=ach / peak, int_ops_per_cand=prof["int_ops_per_cand"],
                  valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"),
-                 profile=f"profiles/pmc_digest_{args.digest}_c5.json (kernel_src_sha {prof['kernel_src_sha'][:12]})")
+                 profile=f"{prof['_file']} (kernel_src_sha {prof['kernel_src_sha'][:12]})")
     return r
 
 

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "a5x.h"
+#include "a5x_format.h"
 #include "a5x_launch.h"
 #include "a5x_md.h"
 
@@ -280,7 +281,48 @@ __global__ void __launch_bounds__(64) k_hits_resolve(A5xHitRaw* hits, u32 n, con
   }
 }
 
+// Hybrid fused digest: the candidate-bearing words the fused kernel leaves out (not
+// FAST: slow / BIG / pass-G words) are listed, then gathered into a compact sub-batch
+// that the two-pass path digests.
+__global__ void __launch_bounds__(256) k_nonfast_list(const u32* flags, const u64* cand_off, u64 nw, u32* list,
+                                                       u32* n) {
+  for (u64 w = (u64)blockIdx.x * 256 + threadIdx.x; w < nw; w += (u64)gridDim.x * 256)
+    if (cand_off[w + 1] > cand_off[w] && !(flags[w] & A5X_WF_FAST)) list[atomicAdd(n, 1u)] = (u32)w;
+}
+
+__global__ void __launch_bounds__(256) k_gather_lens(const u64* woff, const u32* idx, u32 m, u64* lens) {
+  for (u32 k = blockIdx.x * 256 + threadIdx.x; k < m; k += gridDim.x * 256) lens[k] = woff[idx[k] + 1] - woff[idx[k]];
+}
+
+__global__ void __launch_bounds__(64) k_gather_words(const uint8_t* words, const u64* woff, const u32* idx, u32 m,
+                                                      const u64* sub_off, uint8_t* out) {
+  for (u32 k = blockIdx.x; k < m; k += gridDim.x) {
+    const u64 s = woff[idx[k]], L = woff[idx[k] + 1] - s, d = sub_off[k];
+    for (u64 i = threadIdx.x; i < L; i += 64) out[d + i] = words[s + i];
+  }
+}
+
 }  // namespace
+
+hipError_t a5x_launch_nonfast_list(const uint32_t* flags, const uint64_t* cand_off, uint64_t nw, uint32_t* list,
+                                   uint32_t* n, hipStream_t st) {
+  if (!nw) return hipSuccess;
+  const u64 b = (nw + 255) / 256;
+  hipLaunchKernelGGL(k_nonfast_list, dim3((u32)(b < 16384 ? b : 16384)), dim3(256), 0, st, flags, cand_off, nw, list, n);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_gather_words(const uint8_t* words, const uint64_t* woff, const uint32_t* idx, uint32_t m,
+                                   uint64_t* lens, const uint64_t* sub_off, uint8_t* out, hipStream_t st) {
+  if (!m) return hipSuccess;
+  if (lens) {  // pass 1: the lengths
+    hipLaunchKernelGGL(k_gather_lens, dim3((m + 255) / 256 < 4096 ? (m + 255) / 256 : 4096), dim3(256), 0, st, woff, idx,
+                       m, lens);
+  } else {     // pass 2: the bytes at the scanned offsets
+    hipLaunchKernelGGL(k_gather_words, dim3(m < 65536 ? m : 65536), dim3(64), 0, st, words, woff, idx, m, sub_off, out);
+  }
+  return hipGetLastError();
+}
 
 size_t a5x_digest_lds(int algo) {
   const u32 per = algo == A5X_ALGO_MD5 ? (u32)sizeof(DWave<DCfg<true>::BLK>)

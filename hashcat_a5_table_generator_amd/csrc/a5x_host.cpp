@@ -89,7 +89,8 @@ struct a5x_ctx {
   DevBuf<uint64_t> m_nseg, m_seg_off, m_seg_bytes, m_seg_boff, m_tmp;
   DevBuf<uint32_t> m_item_w;
   uint64_t m_items = 0;
-  uint64_t m_nglob = 0;       // mode pass G words of the current batch (their list: glob)
+  uint64_t m_nglob = 0;
+  bool dg_two_pass = false;   // a5x_expand_digest_device: the hybrid's sub-batch call (no fused path)       // mode pass G words of the current batch (their list: glob)
   uint8_t* mgscr = nullptr;   // mode pass G scratch: A5X_G_SLOTS x a5x_mode_gslot_bytes(), on first use
   uint64_t mseg = 1024;  // candidates per mode-engine item
   // fused digest + lookup (a5x_digest.hip)
@@ -1499,12 +1500,13 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
   if ((rc = grow(c, c->dg_cand_off, nw + 1)) || (rc = grow(c, c->dg_byte_off, nw + 1))) return rc;
   if ((rc = job_prepare(c, J, c->dg_cand_off.p, c->dg_byte_off.p, true))) return rc;
   const uint64_t tc = J.B.total_cands, tb = J.B.total_bytes;
-  // Fused path (default mode, every candidate-bearing word FAST): k_expand_fast_md5 /
-  // k_expand_fast_ntlm hash each candidate in the LDS ring where it is built -- no HBM
-  // scratch, no second pass, hits already (word, candidate).  Otherwise the two-pass
-  // range loop below.
-  const bool fused = mode == A5X_MODE_DEFAULT && J.B.nslow == 0 && J.B.nbig == 0 && tc > 0 &&
-                     !getenv("A5X_NO_FUSED_DIGEST");
+  // Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm hash each FAST
+  // word's candidates in the LDS ring where they are built -- no HBM scratch, no second
+  // pass, hits already (word, candidate).  The other candidate-bearing words (slow / BIG
+  // / pass G) are gathered into a sub-batch for the two-pass path (hybrid).  Modes
+  // -r / -s / -s -r: the two-pass range loop below.
+  const bool fused = mode == A5X_MODE_DEFAULT && tc > 0 && !c->dg_two_pass && !getenv("A5X_NO_FUSED_DIGEST");
+  const bool hybrid = fused && (J.B.nslow || J.B.nbig || J.B.nglob);
   if (fused) {
     uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
     if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
@@ -1531,10 +1533,63 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
       dev_hits = std::min<uint64_t>(nh, hit_cap);  // run again with room for every hit the caller takes
       if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
     }
-    const uint64_t take = std::min(std::min(nh, dev_hits), hit_cap);
+    uint64_t take = std::min(std::min(nh, dev_hits), hit_cap);
     if (take) {
       HIPCHK(c, hipMemcpyAsync(hits, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, J.st));
       HIPCHK(c, hipStreamSynchronize(J.st));
+    }
+    float a = 0;  // this batch's keyspace (before the sub-batch reuses the events)
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    float ms_sub = 0;
+    if (hybrid) {
+      // the words the fused kernel skipped, in batch order, as a compact sub-batch
+      struct DTmp {
+        void* p = nullptr;
+        ~DTmp() { if (p) (void)hipFree(p); }
+      } d_list, d_n, d_lens, d_off, d_sw;
+      HIPCHK(c, hipMalloc(&d_list.p, std::max<uint64_t>(1, nw) * 4));
+      HIPCHK(c, hipMalloc(&d_n.p, 4));
+      HIPCHK(c, hipMemsetAsync(d_n.p, 0, 4, J.st));
+      HIPCHK(c, a5x_launch_nonfast_list(c->flags.p, J.B.cand_off, nw, (uint32_t*)d_list.p, (uint32_t*)d_n.p, J.st));
+      uint32_t m = 0;
+      HIPCHK(c, hipMemcpyAsync(&m, d_n.p, 4, hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      std::vector<uint32_t> idx(m);
+      if (m) HIPCHK(c, hipMemcpy(idx.data(), d_list.p, (size_t)m * 4, hipMemcpyDeviceToHost));
+      std::sort(idx.begin(), idx.end());
+      std::vector<uint64_t> off((size_t)m + 1, 0);
+      if (m) {
+        HIPCHK(c, hipMemcpy(d_list.p, idx.data(), (size_t)m * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMalloc(&d_lens.p, (size_t)m * 8));
+        HIPCHK(c, a5x_launch_gather_words(J.w, J.wo, (const uint32_t*)d_list.p, m, (uint64_t*)d_lens.p, nullptr, nullptr,
+                                          J.st));
+        HIPCHK(c, hipMemcpyAsync(off.data() + 1, d_lens.p, (size_t)m * 8, hipMemcpyDeviceToHost, J.st));
+        HIPCHK(c, hipStreamSynchronize(J.st));
+        for (uint32_t k = 0; k < m; k++) off[k + 1] += off[k];
+      }
+      HIPCHK(c, hipMalloc(&d_off.p, ((size_t)m + 1) * 8));
+      HIPCHK(c, hipMemcpy(d_off.p, off.data(), ((size_t)m + 1) * 8, hipMemcpyHostToDevice));
+      HIPCHK(c, hipMalloc(&d_sw.p, off[m] + 16));
+      HIPCHK(c, hipMemsetAsync(d_sw.p, 0, off[m] + 16, J.st));
+      HIPCHK(c, a5x_launch_gather_words(J.w, J.wo, (const uint32_t*)d_list.p, m, nullptr, (const uint64_t*)d_off.p,
+                                        (uint8_t*)d_sw.p, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      // their candidates through the two-pass path (the recursion sees no FAST word, or
+      // fewer words); hit word indices mapped back to the batch
+      const uint64_t room = hit_cap > take ? hit_cap - take : 0;
+      uint64_t nh2 = 0;
+      a5x_stats st2;
+      memset(&st2, 0, sizeof st2);
+      c->dg_two_pass = true;  // (the sub-batch's words are the ones the fused kernel skips)
+      rc = a5x_expand_digest_device(c, (const uint8_t*)d_sw.p, (const uint64_t*)d_off.p, m, mode, mn, mx,
+                                    scratch_bytes, room ? hits + take : nullptr, room, &nh2, &st2, stream);
+      c->dg_two_pass = false;
+      if (rc && rc != A5X_E_CAPACITY) return rc;
+      const uint64_t got = std::min(nh2, room);
+      for (uint64_t i = take; i < take + got; i++) hits[i].word = idx[hits[i].word];
+      take += got;
+      nh += nh2;
+      ms_sub = st2.ms_total;
     }
     a5x_stats total;
     memset(&total, 0, sizeof total);
@@ -1542,11 +1597,9 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
     total.candidates = tc;
     total.bytes = tb;
     total.expand_launches = 1;
-    float a = 0;
-    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
     total.ms_keyspace = a;
-    total.ms_expand = ms;  // expansion + digest + lookup, fused
-    total.ms_total = a + ms;
+    total.ms_expand = ms + ms_sub;  // expansion + digest + lookup: fused (+ the two-pass sub-batch)
+    total.ms_total = a + ms + ms_sub;
     if (n_hits) *n_hits = nh;
     if (stats) *stats = total;
     if (nh > hit_cap)

@@ -198,3 +198,54 @@ def test_fused_equals_two_pass(algo, wl, tabs):
     assert st["candidates"] == st2["candidates"]
     assert st["ms_total"] - st["ms_keyspace"] - st["ms_expand"] < 1e-3 < st2["ms_total"] - st2["ms_keyspace"] - st2["ms_expand"]
     assert sorted(fused) == sorted(two) and len(fused) >= len(tg)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_hybrid_fused_digest_mixed_batch(algo):
+    """A batch with non-FAST words (more than 8 pieces, BIG and pass-G lines for MD5)
+    among FAST ones: the fused kernel hashes the FAST words and the others go through the
+    two-pass path as a gathered sub-batch; the hits equal the all-two-pass run's and
+    include every planted (word, candidate)."""
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, pack_words, synth
+    from oracle import digest_oracle as dg
+    _, (data, offs) = synth.global_words("c3", 0, 20_000, seed=0xB7)
+    words = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in range(len(offs) - 1)]
+    rng = np.random.default_rng(17 + algo)
+    digits = list(b"0123456789")
+
+    def spread(L, keys):
+        w = bytearray(np.asarray(rng.choice(digits, size=L), dtype=np.uint8).tobytes())
+        for p in rng.choice(L, size=len(keys), replace=False):
+            w[p] = keys[int(rng.integers(0, len(keys)))]
+        return bytes(w)
+
+    extra = [spread(int(rng.integers(57, 62)), b"aeu") for _ in range(300)]   # > 8 pieces: not FAST
+    if algo == 0:                                                              # BIG and pass-G lines
+        extra += [spread(L, b"ae") for L in (100, 700, 2100, 5000)]
+    pos = sorted(rng.choice(len(words) + len(extra), size=len(extra), replace=False))
+    for p, w in zip(pos, extra):
+        words.insert(int(p), w)
+    f = dg.ALGOS[algo]
+    with Context(0) as ctx:
+        ctx.load_tables([table_path("czech"), table_path("german")])
+        pick = sorted(set(int(x) for x in rng.choice(len(words), size=200, replace=False)) | set(int(p) for p in pos))
+        cands = ctx.expand_words([words[i] for i in pick], 0, 0, 15)
+        planted = {}
+        for i, cs in zip(pick, cands):
+            if cs:
+                c = int(rng.integers(0, len(cs)))
+                planted[(i, c)] = f(cs[c])
+        ctx.set_targets(algo, b"".join(planted.values()) + bytes(rng.integers(0, 256, 16 * 5000, dtype=np.uint8)))
+        d, o = pack_words(words)
+        dw, do = DeviceBuffer.from_array(ctx, d), DeviceBuffer.from_array(ctx, o)
+        fused, st = ctx.expand_digest_device(dw.ptr, do.ptr, len(words), 0, 0, 15, hit_cap=1 << 14)
+        os.environ["A5X_NO_FUSED_DIGEST"] = "1"
+        try:
+            two, st2 = ctx.expand_digest_device(dw.ptr, do.ptr, len(words), 0, 0, 15, hit_cap=1 << 14)
+        finally:
+            os.environ.pop("A5X_NO_FUSED_DIGEST")
+    assert st["candidates"] == st2["candidates"]
+    assert sorted(fused) == sorted(two)
+    got = {(w, c) for w, c, _ in fused}
+    assert set(planted) <= got
+    assert any(w in set(int(p) for p in pos) for w, _ in got)  # hits in the non-FAST words too
