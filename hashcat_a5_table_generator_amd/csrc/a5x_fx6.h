@@ -193,9 +193,12 @@ __device__ __forceinline__ u32 fx6_word(u32 rw, u32 k, u32 rr, u32 nl, u32& jcur
 // fx6_round with OR placement (same run / fit / scan logic; ring zero past R.pos)
 // A lane's run of the last round, for the fused digest (FLUSH::DIGEST): ring byte
 // offset of its first candidate, candidate lengths ('\n' included), window word, rank.
+#ifndef FX6_KMAX
+#define FX6_KMAX 4       // candidates per lane run (FX_K of the includer)
+#endif
 struct FxLaneRun {
   u32 off, nc, j, st;
-  u32 clen[4];
+  u32 clen[FX6_KMAX];
 };
 
 // nsm: fx8_put slot counts of big pieces 0-3 (4 bits each, wave-uniform)
@@ -203,7 +206,7 @@ template <int NB, int K, bool NOOR = false, class FLUSH>
 __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
                                          u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush, FxLaneRun& lr,
                                          u32 nsm) {
-  static_assert(K <= 4, "FxLaneRun holds 4 candidates");
+  static_assert(K <= FX6_KMAX, "FxLaneRun holds FX6_KMAX candidates");
   const u32 lane = lane_id();
   const uint4 q0 = wq[j][0], q1 = wq[j][1];
   const u32 st = act ? (rr + lane - q1.w) * K + rb[j] : 0u;  // first rank of the run
@@ -281,7 +284,7 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
     lr.j = j;
     lr.st = st;
 #pragma unroll
-    for (int c = 0; c < 4; c++) lr.clen[c] = c < K ? clen[c] : 0u;
+    for (int c = 0; c < FX6_KMAX; c++) lr.clen[c] = c < K ? clen[c] : 0u;
   } else {
     flush(R);
   }

@@ -1425,7 +1425,7 @@ struct FxRun {
 #ifndef FX_FLB
 #define FX_FLB 0 // flush: batch the ring block reads before the stores
 #endif
-static_assert(FX_RING / 16 <= 256, "fx_flush: at most 4 ring blocks per lane");
+static_assert(!FX_FLB || FX_RING / 16 <= 256, "fx_flush (FX_FLB): at most 4 ring blocks per lane");
 __device__ __forceinline__ void fx_store16(uint8_t* p, const uint4 v) {
 #if FX_NT
   typedef u32 v4u __attribute__((ext_vector_type(4)));
@@ -1520,6 +1520,7 @@ __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) 
   R.open = false;
 }
 
+#define FX6_KMAX FX_K
 #include "a5x_fx6.h"
 #include "a5x_md.h"
 
@@ -1574,8 +1575,10 @@ struct FxDigest {
     const uint8_t* base = (const uint8_t*)ring;
     u32 off = lr.off;
 #pragma unroll 1
-    for (u32 c = 0; c < 4; c++) {
-      const u32 l = c == 0 ? lr.clen[0] : c == 1 ? lr.clen[1] : c == 2 ? lr.clen[2] : lr.clen[3];
+    for (u32 c = 0; c < FX6_KMAX; c++) {
+      u32 l = lr.clen[0];
+#pragma unroll
+      for (u32 q = 1; q < FX6_KMAX; q++) l = c == q ? lr.clen[q] : l;
       const bool on = c < lr.nc;
       if (!__builtin_amdgcn_ballot_w64(on)) break;  // runs are filled from candidate 0
       u32 d[4];
