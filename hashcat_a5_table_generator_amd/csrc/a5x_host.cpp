@@ -87,6 +87,7 @@ struct a5x_ctx {
   size_t d_mtab_cap = 0;
   uint32_t mtab_bytes = 0;
   DevBuf<uint64_t> m_nseg, m_seg_off, m_seg_bytes, m_seg_boff, m_tmp;
+  DevBuf<uint8_t> m_item_fl;  // per item: the layout that expands it (a5x_modes.hip m_item)
   DevBuf<uint32_t> m_item_w;
   uint64_t m_items = 0;
   uint64_t m_nglob = 0;
@@ -579,7 +580,7 @@ A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_
   M.mode = mode; M.mn = mn; M.mx = mx; M.SEG = c->mseg;
   M.count = c->count.p; M.nseg = c->m_nseg.p; M.flags = c->flags.p;
   M.seg_off = c->m_seg_off.p; M.item_w = c->m_item_w.p; M.nitems = c->m_items;
-  M.seg_bytes = c->m_seg_bytes.p; M.seg_boff = c->m_seg_boff.p;
+  M.seg_bytes = c->m_seg_bytes.p; M.seg_boff = c->m_seg_boff.p; M.item_fl = c->m_item_fl.p;
   M.cand_begin = 0; M.cand_end = ~0ull;
   M.err = c->d_scalars + 2;
   M.glob_list = c->glob.p; M.glob_n = c->d_scalars + 7;
@@ -676,6 +677,7 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   const uint64_t items = c->h_totals[1];
   c->m_items = items;
   if ((rc = grow(c, c->m_item_w, items + 1)) || (rc = grow(c, c->m_seg_bytes, items + 1)) ||
+      (rc = grow(c, c->m_item_fl, items + 1)) ||
       (rc = grow(c, c->m_seg_boff, items + 1)) || (rc = grow(c, c->m_tmp, items + 1)) ||
       (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(items + 1) + 16)))
     return rc;
@@ -1010,7 +1012,7 @@ void a5x_destroy(a5x_ctx* c) {
   release(c->count); release(c->bytes); release(c->cand_off); release(c->byte_off); release(c->scan_tmp);
   release(c->locate); release(c->flags); release(c->defer); release(c->chunk_w0); release(c->slow_list); release(c->big_list);
   release(c->segs);
-  release(c->m_nseg); release(c->m_seg_off); release(c->m_seg_bytes); release(c->m_seg_boff); release(c->m_tmp);
+  release(c->m_nseg); release(c->m_seg_off); release(c->m_seg_bytes); release(c->m_item_fl); release(c->m_seg_boff); release(c->m_tmp);
   release(c->m_item_w);
   release(c->t_bitmap); release(c->t_table); release(c->dg_scratch); release(c->dg_blk_cnt); release(c->dg_blk_pre);
   release(c->dg_cand_off); release(c->dg_byte_off); release(c->dg_hits);

@@ -118,6 +118,7 @@ struct A5xModeLaunch {
   uint64_t nitems;
   uint64_t item_begin, item_end;
   uint64_t* seg_bytes;       // length pass output (per item)
+  uint8_t* item_fl;          // per item: which layout expands it (set by the length pass)
   const uint64_t* seg_boff;  // exclusive scan of seg_bytes (nitems+1)
   uint64_t cand_begin, cand_end;
   uint8_t* out;

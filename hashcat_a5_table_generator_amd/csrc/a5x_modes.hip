@@ -72,10 +72,15 @@ constexpr u32 MP_VMAX = 14;   // values per pattern (selector 1 + v <= 15)
 // Per-wave state of one word: LDS (MLds), or an HBM scratch slot for the words of
 // mode pass G (MLdsG: lines up to 64 KiB, candidates up to A5X_MG_CBUF - 1 bytes; the
 // positional engine, which places through LDS addresses, is not used there).
-template <u32 LMAX, u32 CBUF>
+// NBUF: bytes of the candidate buffers -- the byte builder's two per-lane buffers
+// (2 x 64 x STRIDE), the positional engine's ring only (MP_RING), or none (counting
+// and closed-form lengths): the smaller layouts run more waves per CU.
+constexpr u32 MP_RING = 16 + 64 * A5X_M_CBUF + 48;
+template <u32 LMAX, u32 CBUF, u32 NBUF = 2 * 64 * (CBUF + 4)>
 struct MLdsT {
   static constexpr u32 L_MAX = LMAX, STRIDE = CBUF + 4, CMAXLEN = CBUF - 1;
   static constexpr bool G = LMAX > A5X_M_LMAX;
+  static constexpr bool BUILDER = NBUF >= 2 * 64 * STRIDE, RING = NBUF >= MP_RING;
   u64 dp[A5X_M_DPMAX];
   uint4 ent[MP_NE];
   u32 tok[A5X_M_LMAX + 2];   // entry base | (pattern index + 1) << 16 (0: literal chunk)
@@ -90,10 +95,12 @@ struct MLdsT {
   uint16_t pat[64];          // key index per sorted pattern (-s) / per position (-r)
   uint16_t pst[64];          // -r: start byte
   uint8_t pnx[64];           // -r: first later compatible position
-  uint8_t buf[2][64 * STRIDE];
+  alignas(16) uint8_t buf[NBUF];
 };
-typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF> MLds;
-typedef MLdsT<A5X_MG_LMAX, A5X_MG_CBUF> MLdsG;
+typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF> MLds;                // byte builder (general words)
+typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MP_RING> MLdsR;      // positional expansion
+typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, 16> MLdsC;           // counts, closed-form lengths
+typedef MLdsT<A5X_MG_LMAX, A5X_MG_CBUF> MLdsG;             // mode pass G (HBM)
 
 // wave sync over the word state: LDS, or (pass G) HBM written and read by the wave's own
 // lanes -- workgroup-scope release / acquire drains and orders those global accesses
@@ -343,6 +350,39 @@ __device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
   return I;
 }
 
+// -r: leaf t -> the chosen non-overlapping positions (bit j = position j)
+template <class SL>
+__device__ __forceinline__ u64 m_rsel(const SL& S, const MInfo& I, u64 t, u32& err) {
+  const u64* D = S.dp;
+  const u32 cols = I.cols, n = I.n;
+  u32 c = I.cmin;
+  while (c < I.cmax && t >= D[c]) { t -= D[c]; c++; }
+  u64 sel = 0;
+  u32 r = 0;
+  while (c > 0) {
+    if (r >= n) { err |= M_ERR_STATE; break; }
+    const u64 a0 = D[(r + 1) * cols + c];
+    if (t < a0) { r++; continue; }
+    t -= a0;
+    sel |= 1ull << r;
+    r = S.pnx[r];
+    c--;
+  }
+  return sel;
+}
+
+// -r: the candidate's length does not depend on where (or how wrongly) the replacements
+// land: L + sum (|subs[0]| - |key|); panics surface in the expansion pass, which builds it
+template <class SL>
+__device__ __forceinline__ u32 m_rlen(const SL& S, const MT& T, const MInfo& I, u64 sel) {
+  int l = (int)I.L;
+  for (u64 m = sel; m; m &= m - 1) {
+    const A5xMKey K = T.keys[S.pat[__builtin_ctzll(m)]];
+    if (K.nvals) l += (int)T.vals[K.val_base].len - (int)K.klen;
+  }
+  return (u32)l;
+}
+
 // Build candidate t (0 <= t < count) of the word set up in S into this lane's
 // buffer; returns its length and the buffer holding it.
 template <class SL>
@@ -350,36 +390,17 @@ __device__ u32 m_build(SL& S, const MT& T, const MInfo& I, int mode, u64 t, cons
                        bool len_only = false) {
   const u32 lane = m_lane();
   constexpr u32 CMAXLEN = SL::CMAXLEN;
-  uint8_t* b0 = S.buf[0] + lane * SL::STRIDE;
-  uint8_t* b1 = S.buf[1] + lane * SL::STRIDE;
+  static_assert(SL::BUILDER, "m_build needs the builder layout");
+  uint8_t* b0 = S.buf + lane * SL::STRIDE;
+  uint8_t* b1 = S.buf + (64 + lane) * SL::STRIDE;
   const u64* D = S.dp;
   const u32 cols = I.cols, n = I.n;
-  u32 c = I.cmin;
-  while (c < I.cmax && t >= D[c]) { t -= D[c]; c++; }
   if (mode == A5X_MODE_REVERSE) {
-    // unrank the non-overlapping subset (bit j = position j chosen)
-    u64 sel = 0;
-    u32 r = 0;
-    while (c > 0) {
-      if (r >= n) { err |= M_ERR_STATE; break; }
-      const u64 a0 = D[(r + 1) * cols + c];
-      if (t < a0) { r++; continue; }
-      t -= a0;
-      sel |= 1ull << r;
-      r = S.pnx[r];
-      c--;
-    }
+    u64 sel = m_rsel(S, I, t, err);
     u32 len = I.L;
-    if (len_only) {  // the result's length does not depend on where (or how wrongly) the
-                     // replacements land: L + sum (|subs[0]| - |key|); panics surface in the
-                     // expansion pass, which builds the candidate
-      int l = (int)len;
-      for (u64 m = sel; m; m &= m - 1) {
-        const A5xMKey K = T.keys[S.pat[__builtin_ctzll(m)]];
-        if (K.nvals) l += (int)T.vals[K.val_base].len - (int)K.klen;
-      }
+    if (len_only) {
       *outp = nullptr;
-      return (u32)l;
+      return m_rlen(S, T, I, sel);
     }
     for (u32 i = 0; i < len; i++) b0[i] = S.word[i];
     // combo indices descending, running offset (main.go:249-257)
@@ -410,6 +431,8 @@ __device__ u32 m_build(SL& S, const MT& T, const MInfo& I, int mode, u64 t, cons
     return len;
   }
   // -s / -s -r: chosen patterns in sorted order, ReplaceAll each (main.go:339-341)
+  u32 c = I.cmin;
+  while (c < I.cmax && t >= D[c]) { t -= D[c]; c++; }
   const uint8_t* src = S.word;
   uint8_t* dst = b0;
   u32 len = I.L;
@@ -475,7 +498,8 @@ __device__ __forceinline__ uint4 m_entry(const uint8_t* p, u32 n) {
 
 // Tokens and entries of the word set up in S (after m_setup, modes -s / -s -r):
 // returns the token count, or 0 when the word is not positional (byte builder path).
-__device__ u32 m_pos_setup(MLds& S, const MT& T, const MInfo& I, int mode) {
+template <class SL>
+__device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode) {
   const u32 lane = m_lane(), n = I.n, L = I.L;
   if (n == 0 || n > MP_PMAX || L > A5X_M_LMAX) return 0;
   u32 ok = 1, ne = 0;
@@ -564,7 +588,8 @@ __device__ u32 m_pos_setup(MLds& S, const MT& T, const MInfo& I, int mode) {
 
 // Sum over leaves t in [0, x) of (len + 1) in radix mode (closed form; lanes over
 // patterns): x (L + 1) + sum_r occ_r sum_{t'} delta_r(digit_r(t')), t' = t + shift.
-__device__ u64 m_pos_prefix(const MLds& S, const MInfo& I, u64 x) {
+template <class SL>
+__device__ u64 m_pos_prefix(const SL& S, const MInfo& I, u64 x) {
   const u32 lane = m_lane(), n = I.n;
   auto G = [&](u64 y) -> i64 {  // this lane's pattern: sum_{t' < y} delta(digit(t'))
     if (lane >= n) return 0;
@@ -588,7 +613,8 @@ __device__ u64 m_pos_prefix(const MLds& S, const MInfo& I, u64 x) {
 
 // Leaf t of a positional word: per-pattern selectors (4 bits each: 0 keep, 1 + v value
 // v) by walking the DP table as m_build does; returns the candidate length.
-__device__ u32 m_pos_sel(const MLds& S, const MT& T, const MInfo& I, int mode, u64 t, u64& sel) {
+template <class SL>
+__device__ u32 m_pos_sel(const SL& S, const MT& T, const MInfo& I, int mode, u64 t, u64& sel) {
   if (S.radix) {  // mixed-radix digits by magic division (pattern 0 least significant)
     u32 x = (u32)t + S.shift, len = I.L;
     u64 sv = 0;
@@ -646,12 +672,13 @@ __device__ __forceinline__ void m_store16_nt(uint8_t* p, const uint4 x) {
 // start at a.out + pos0.  64 leaves per round: lengths (formula) -> wave scan ->
 // every token's entry OR-placed into the zeroed ring (S.buf) -> complete 16-B blocks
 // streamed with dwordx4 stores (the item's first and last blocks byte-exact).
-__device__ void m_pos_expand(MLds& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 tb, u64 te, u64 pos0,
+template <class SL>
+__device__ void m_pos_expand(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 tb, u64 te, u64 pos0,
                              u32 ntok, u32& err) {
   const u32 lane = m_lane();
-  uint4* r4 = (uint4*)&S.buf[0][0];
+  uint4* r4 = (uint4*)&S.buf[0];
   constexpr u32 RB = sizeof(S.buf) / 16;
-  static_assert(sizeof(S.buf) >= 16 + 64 * A5X_M_CBUF + 32, "ring: one round of 64 candidates");
+  static_assert(SL::RING && sizeof(S.buf) >= 16 + 64 * A5X_M_CBUF + 32, "ring: one round of 64 candidates");
   const u32 ringa = fx6_addr(r4);
   for (u32 i = lane; i < RB; i += 64) r4[i] = make_uint4(0, 0, 0, 0);
   M_WAVE_SYNC();
@@ -730,8 +757,8 @@ __device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLa
 
 // one wave per word: count, segments, per-word error flags
 __global__ void __launch_bounds__(64) k_mode_count(A5xModeLaunch a) {
-  MLds& S = *(MLds*)m_dyn;
-  const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
+  MLdsC& S = *(MLdsC*)m_dyn;
+  const MT T = m_table(m_dyn + sizeof(MLdsC), a.mtab, a.mtab_bytes);
   for (u64 w = blockIdx.x; w < a.nw; w += gridDim.x) m_count_word(S, T, a, w);
 }
 
@@ -767,7 +794,12 @@ __device__ u64 m_run(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a,
       }
     }
     if (v && !(ntok && op == 0)) {
-      len = m_build(S, T, I, a.mode, t0 + k, &p, err, op == 0 && a.mode == A5X_MODE_REVERSE) + 1;
+      if (op == 0 && a.mode == A5X_MODE_REVERSE) {
+        len = m_rlen(S, T, I, m_rsel(S, I, t0 + k, err)) + 1;
+      } else {
+        if constexpr (SL::BUILDER) len = m_build(S, T, I, a.mode, t0 + k, &p, err) + 1;
+        else err |= M_ERR_STATE;  // (item routed to the wrong layout)
+      }
     }
     const u32 incl = m_incl_scan(len);
     const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
@@ -789,7 +821,15 @@ __device__ u64 m_run(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a,
   return run;
 }
 
-// item i (word, SEG-candidate segment): op 0 = seg_bytes, op 1 = expand
+// item i (word, SEG-candidate segment): op 0 = seg_bytes, op 1 = expand.  The LDS
+// items run in two layouts, routed by item_fl (written by the op-0 closed-form pass):
+//   MLdsC / MLdsR (small: more waves per CU): op 0 of every item -- closed-form or
+//     formula lengths of positional words, -r lengths; op 1 of positional items (ring);
+//   MLds (byte builder): op 0 of non-positional -s / -s -r items, op 1 of every
+//     non-positional item.
+constexpr uint8_t MI_POS = 1;       // positional: lengths done, ring expansion
+constexpr uint8_t MI_BUILD = 2;     // byte builder for the expansion, lengths done
+constexpr uint8_t MI_BUILD_LEN = 3; // byte builder for the lengths too
 template <class SL>
 __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op) {
   const u64 w = a.item_w[i];
@@ -800,40 +840,54 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
   const MInfo I = m_setup(S, T, a, w);
   if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
   u32 err = 0, ntok = 0;
-  if constexpr (!SL::G) {
+  if constexpr (!SL::G && !SL::BUILDER) {
     ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
-    if (ntok && op == 1) {
-      // the leaves of this item inside [cand_begin, cand_end); the first one's bytes start
-      // at seg_boff[i] (or at out_base itself when the range starts inside the item)
-      const u64 rb = a.cand_begin > cw0 ? a.cand_begin - cw0 : 0;
-      const u64 re = a.cand_end - cw0 < t0 + nc ? a.cand_end - cw0 : t0 + nc;  // (cand_end > cw0 here)
-      const u64 tb = rb > t0 ? rb : t0;
-      if (a.cand_end > cw0 && tb < re)
-        m_pos_expand(S, T, I, a, tb, re, tb == t0 ? a.seg_boff[i] - a.out_base : 0, ntok, err);
+    if (op == 1) {
+      if constexpr (SL::RING) {
+        // the leaves of this item inside [cand_begin, cand_end); the first one's bytes start
+        // at seg_boff[i] (or at out_base itself when the range starts inside the item)
+        const u64 rb = a.cand_begin > cw0 ? a.cand_begin - cw0 : 0;
+        const u64 re = a.cand_end - cw0 < t0 + nc ? a.cand_end - cw0 : t0 + nc;  // (cand_end > cw0 here)
+        const u64 tb = rb > t0 ? rb : t0;
+        if (!ntok) err |= M_ERR_STATE;
+        else if (a.cand_end > cw0 && tb < re)
+          m_pos_expand(S, T, I, a, tb, re, tb == t0 ? a.seg_boff[i] - a.out_base : 0, ntok, err);
+      }
       m_err(a.err, m_wave_or(err));
       return;
     }
+    if (m_lane() == 0) a.item_fl[i] = ntok ? MI_POS : a.mode == A5X_MODE_REVERSE ? MI_BUILD : MI_BUILD_LEN;
+    if (!ntok && a.mode != A5X_MODE_REVERSE) return;  // lengths need the byte builder
     if (ntok && S.radix) {  // op 0, radix mode: closed form, no candidate is visited
       const u64 run = m_pos_prefix(S, I, t0 + nc) - m_pos_prefix(S, I, t0);
       if (m_lane() == 0) a.seg_bytes[i] = run;
       return;
     }
   }
+  if constexpr (!SL::G && SL::BUILDER)
+    if (op == 0 && m_lane() == 0) a.item_fl[i] = MI_BUILD;
   const u64 base = op == 1 ? a.seg_boff[i] : 0;
   const u64 run = m_run(S, T, I, a, t0, nc, op, cw0, base, err, ntok);
   if (op == 0 && m_lane() == 0) a.seg_bytes[i] = run;
   m_err(a.err, m_wave_or(err));
 }
 
-// one wave per item; the items of pass-G words are left to k_mode_items_g
-__global__ void __launch_bounds__(64) k_mode_items(A5xModeLaunch a, int op) {
-  MLds& S = *(MLds*)m_dyn;
-  const MT T = m_table(m_dyn + sizeof(MLds), a.mtab, a.mtab_bytes);
+// one wave per item of layout SL (route: which item_fl values it takes; 0 = all); the
+// items of pass-G words are left to k_mode_items_g
+template <class SL>
+__device__ __forceinline__ void m_items(const A5xModeLaunch& a, int op, uint8_t route) {
+  SL& S = *(SL*)m_dyn;
+  const MT T = m_table(m_dyn + sizeof(SL), a.mtab, a.mtab_bytes);
   for (u64 i = a.item_begin + blockIdx.x; i < a.item_end; i += gridDim.x) {
     if (a.flags[a.item_w[i]] & A5X_WF_GLOB) continue;
+    if (route && a.item_fl[i] != route) continue;
     m_item(S, T, a, i, op);
   }
 }
+__global__ void __launch_bounds__(64) k_mode_items_len(A5xModeLaunch a) { m_items<MLdsC>(a, 0, 0); }
+__global__ void __launch_bounds__(64) k_mode_items_len_b(A5xModeLaunch a) { m_items<MLds>(a, 0, MI_BUILD_LEN); }
+__global__ void __launch_bounds__(64) k_mode_items_pos(A5xModeLaunch a) { m_items<MLdsR>(a, 1, MI_POS); }
+__global__ void __launch_bounds__(64) k_mode_items_b(A5xModeLaunch a) { m_items<MLds>(a, 1, MI_BUILD); }
 
 // the items of the listed pass-G words inside [item_begin, item_end), dealt to the slots
 __global__ void __launch_bounds__(64) k_mode_items_g(A5xModeLaunch a, int op) {
@@ -912,11 +966,13 @@ inline u32 m_grid(u64 n, u32 cap) { return (u32)(n < 1 ? 1 : (n < cap ? n : cap)
 }  // namespace
 
 size_t a5x_mode_lds(uint32_t mtab_bytes) { return sizeof(MLds) + ((mtab_bytes + 15u) & ~15u); }
+template <class SL>
+static size_t m_lds(uint32_t mtab_bytes) { return sizeof(SL) + ((mtab_bytes + 15u) & ~15u); }
 
 uint64_t a5x_mode_gslot_bytes() { return (sizeof(MLdsG) + 255) & ~(size_t)255; }
 
 hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st) {
-  hipLaunchKernelGGL(k_mode_count, dim3(m_grid(L.nw, 1u << 18)), dim3(64), a5x_mode_lds(L.mtab_bytes), st, L);
+  hipLaunchKernelGGL(k_mode_count, dim3(m_grid(L.nw, 1u << 18)), dim3(64), m_lds<MLdsC>(L.mtab_bytes), st, L);
   return hipGetLastError();
 }
 
@@ -927,8 +983,16 @@ hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st) {
 
 hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st) {
   if (L.item_end <= L.item_begin) return hipSuccess;
-  hipLaunchKernelGGL(k_mode_items, dim3(m_grid(L.item_end - L.item_begin, 1u << 18)), dim3(64),
-                     a5x_mode_lds(L.mtab_bytes), st, L, op);
+  const dim3 g(m_grid(L.item_end - L.item_begin, 1u << 18));
+  if (op == 0) {
+    hipLaunchKernelGGL(k_mode_items_len, g, dim3(64), m_lds<MLdsC>(L.mtab_bytes), st, L);
+    if (L.mode != A5X_MODE_REVERSE)
+      hipLaunchKernelGGL(k_mode_items_len_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
+  } else {
+    if (L.mode != A5X_MODE_REVERSE)
+      hipLaunchKernelGGL(k_mode_items_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
+    hipLaunchKernelGGL(k_mode_items_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
+  }
   if (L.gscr && L.gslots)
     hipLaunchKernelGGL(k_mode_items_g, dim3(L.gslots), dim3(64), (L.mtab_bytes + 15u) & ~15u, st, L, op);
   return hipGetLastError();
