@@ -496,10 +496,64 @@ __device__ __forceinline__ uint4 m_entry(const uint8_t* p, u32 n) {
   return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32) | (n << 24));
 }
 
-// Tokens and entries of the word set up in S (after m_setup, modes -s / -s -r):
-// returns the token count, or 0 when the word is not positional (byte builder path).
+// -r positional words: every position's key and subs[0] have the same length (so the
+// running-offset bug of main.go:249-257 moves nothing), positions do not overlap, and
+// each key has a value (no panic).  A leaf is then the word with each chosen position's
+// bytes replaced in place: tokens = literal chunks and positions (entries [key, subs[0]],
+// selected by bit j of the leaf's position set), every candidate L + 1 bytes long.
+template <class SL>
+__device__ u32 m_rpos_setup(SL& S, const MT& T, const MInfo& I) {
+  const u32 lane = m_lane(), n = I.n, L = I.L;
+  if (n == 0 || L > A5X_M_LMAX) return 0;
+  u32 ok = 1;
+  if (lane < n) {
+    const A5xMKey K = T.keys[S.pat[lane]];
+    ok = K.nvals >= 1 && K.klen >= 1 && K.klen <= 15 && T.vals[K.val_base].len == K.klen &&
+         (lane + 1 >= n || (u32)S.pst[lane] + K.klen <= (u32)S.pst[lane + 1]);
+  }
+  if (__ballot(!ok)) return 0;
+  m_sync<SL>();
+  if (lane < n) {  // position entries: [key, subs[0]] at 2 j
+    const A5xMKey K = T.keys[S.pat[lane]];
+    S.ent[2 * lane] = m_entry(T.blob + K.key_off, K.klen);
+    S.ent[2 * lane + 1] = m_entry(T.blob + T.vals[K.val_base].off, K.klen);
+  }
+  m_sync<SL>();
+  if (lane == 0) {  // tokens in byte order: literal chunks of <= 15 bytes and positions
+    u32 nt = 0, e = 2 * n, q = 0, j = 0;
+    bool over = false;
+    while (q < L) {
+      if (j < n && S.pst[j] == q) {
+        S.tok[nt++] = (2 * j) | ((j + 1) << 16);
+        q += T.keys[S.pat[j]].klen;
+        j++;
+      } else {
+        if (e >= MP_NE) { over = true; break; }
+        const u32 qe = j < n ? (u32)S.pst[j] : L;
+        u32 k = 0;
+        u64 lo = 0, hi = 0;
+        while (q < qe && k < 15) {
+          const u64 b = S.word[q];
+          if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
+          k++;
+          q++;
+        }
+        S.ent[e] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32) | (k << 24));
+        S.tok[nt++] = e++;
+      }
+    }
+    S.ntok = over ? 0u : nt;
+    S.radix = 0;
+  }
+  m_sync<SL>();
+  return (u32)__builtin_amdgcn_readfirstlane((int)S.ntok);
+}
+
+// Tokens and entries of the word set up in S (after m_setup): returns the token count,
+// or 0 when the word is not positional (byte builder path).
 template <class SL>
 __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode) {
+  if (mode == A5X_MODE_REVERSE) return m_rpos_setup(S, T, I);
   const u32 lane = m_lane(), n = I.n, L = I.L;
   if (n == 0 || n > MP_PMAX || L > A5X_M_LMAX) return 0;
   u32 ok = 1, ne = 0;
@@ -615,6 +669,11 @@ __device__ u64 m_pos_prefix(const SL& S, const MInfo& I, u64 x) {
 // v) by walking the DP table as m_build does; returns the candidate length.
 template <class SL>
 __device__ u32 m_pos_sel(const SL& S, const MT& T, const MInfo& I, int mode, u64 t, u64& sel) {
+  if (mode == A5X_MODE_REVERSE) {  // positional -r: the position set; length L
+    u32 err = 0;
+    sel = m_rsel(S, I, t, err);
+    return I.L;
+  }
   if (S.radix) {  // mixed-radix digits by magic division (pattern 0 least significant)
     u32 x = (u32)t + S.shift, len = I.L;
     u64 sv = 0;
@@ -685,6 +744,7 @@ __device__ void m_pos_expand(SL& S, const MT& T, const MInfo& I, const A5xModeLa
   u64 B = pos0 & ~15ull, pos = pos0;
   const u64 lo = pos0;
   const uint4 nl = make_uint4(0x0Au, 0u, 0u, 1u << 24);
+  const bool rev = a.mode == A5X_MODE_REVERSE;  // token selector: bit j of the position set
   for (u64 t0 = tb; t0 < te; t0 += 64) {
     const u64 t = t0 + lane;
     u64 sel = 0;
@@ -699,7 +759,7 @@ __device__ void m_pos_expand(SL& S, const MT& T, const MInfo& I, const A5xModeLa
     if (len) {
       for (u32 k = 0; k < ntok; k++) {
         const u32 d = S.tok[k], pi = d >> 16;
-        const u32 ix = (d & 0xFFFFu) + (pi ? (u32)(sel >> (4 * (pi - 1))) & 15u : 0u);
+        const u32 ix = (d & 0xFFFFu) + (pi ? (rev ? (u32)(sel >> (pi - 1)) & 1u : (u32)(sel >> (4 * (pi - 1))) & 15u) : 0u);
         fx7_put(S.ent[ix], P, sink);
       }
       fx7_put(nl, P, sink);
@@ -841,7 +901,7 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
   if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
   u32 err = 0, ntok = 0;
   if constexpr (!SL::G && !SL::BUILDER) {
-    ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
+    ntok = a.mode != A5X_MODE_DEFAULT ? m_pos_setup(S, T, I, a.mode) : 0u;
     if (op == 1) {
       if constexpr (SL::RING) {
         // the leaves of this item inside [cand_begin, cand_end); the first one's bytes start
@@ -928,7 +988,7 @@ __device__ void m_locate(SL& S, const MT& T, const A5xModeLaunch& a, const u64* 
     if (I.bad || I.count != a.cand_off[w + 1] - a.cand_off[w]) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
     u32 err = 0, ntok = 0;
     if constexpr (!SL::G) {
-      ntok = a.mode >= A5X_MODE_SUBALL ? m_pos_setup(S, T, I, a.mode) : 0u;
+      ntok = a.mode != A5X_MODE_DEFAULT ? m_pos_setup(S, T, I, a.mode) : 0u;
       if (ntok && S.radix) pre = m_pos_prefix(S, I, t0 + r) - m_pos_prefix(S, I, t0);
     }
     if (!(ntok && S.radix)) pre = m_run(S, T, I, a, t0, r, 0, 0, 0, err, ntok);
@@ -989,8 +1049,7 @@ hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st)
     if (L.mode != A5X_MODE_REVERSE)
       hipLaunchKernelGGL(k_mode_items_len_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   } else {
-    if (L.mode != A5X_MODE_REVERSE)
-      hipLaunchKernelGGL(k_mode_items_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
+    hipLaunchKernelGGL(k_mode_items_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_items_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   }
   if (L.gscr && L.gslots)

@@ -154,11 +154,11 @@ def test_c5_shape_lookup_one_million_targets(algo):
         assert all(hc[w][c] in plains for w, c in set(got) - set(planted))
 
 
-@pytest.mark.parametrize("mode,mn", [(2, 0), (3, 0), (3, 1), (2, 2)])
+@pytest.mark.parametrize("mode,mn", [(2, 0), (3, 0), (3, 1), (2, 2), (1, 0), (1, 2)])
 def test_c5_shape_substitute_all_modes(mode, mn):
-    """-s / -s -r at the C5 shape (README.MD:159,163: greek-hebrew -s, -s -r -m 1):
-    100k Greek words (positional fast path: single-codepoint patterns, repeated
-    letters tie their occurrences) == C oracle per-word digests."""
+    """-s / -s -r / -r at the C5 shape (README.MD:159,163: greek-hebrew -s, -s -r -m 1):
+    100k Greek words (positional fast paths: single-codepoint patterns, repeated letters
+    tie their occurrences; -r with length-preserving subs[0]) == C oracle per-word digests."""
     from hashcat_a5_table_generator_amd import Context, synth
     from oracle import c_oracle as co
     _, (data, offs) = synth.global_words("c5", 0, 100_000, seed=0x55 + mode)
