@@ -579,6 +579,7 @@ A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_
   M.mtab = c->d_mtab; M.mtab_bytes = c->mtab_bytes; M.words = d_words; M.woff = d_woff; M.nw = nw;
   M.mode = mode; M.mn = mn; M.mx = mx; M.SEG = c->mseg;
   M.count = c->count.p; M.nseg = c->m_nseg.p; M.flags = c->flags.p;
+  M.wbytes = c->bytes.p;  // (scratch until k_mode_wordbytes writes the per-word bytes)
   M.seg_off = c->m_seg_off.p; M.item_w = c->m_item_w.p; M.nitems = c->m_items;
   M.seg_bytes = c->m_seg_bytes.p; M.seg_boff = c->m_seg_boff.p; M.item_fl = c->m_item_fl.p;
   M.cand_begin = 0; M.cand_end = ~0ull;

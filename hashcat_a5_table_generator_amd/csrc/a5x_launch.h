@@ -119,6 +119,7 @@ struct A5xModeLaunch {
   uint64_t item_begin, item_end;
   uint64_t* seg_bytes;       // length pass output (per item)
   uint8_t* item_fl;          // per item: which layout expands it (set by the length pass)
+  uint64_t* wbytes;          // per word: closed-form output bytes of single-item positional words (~0: none)
   const uint64_t* seg_boff;  // exclusive scan of seg_bytes (nitems+1)
   uint64_t cand_begin, cand_end;
   uint8_t* out;

@@ -812,6 +812,17 @@ __device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLa
       a.glob_list[k] = (u32)w;
     }
   }
+  if constexpr (!SL::G) {
+    // single-item positional words: their output bytes in closed form here, so the length
+    // pass takes them without another setup (wbytes = ~0: the length pass computes them)
+    u64 wb = ~0ull;
+    if (!I.bad && I.count > 0 && I.count <= a.SEG && a.mode != A5X_MODE_DEFAULT) {
+      const u32 ntok = m_pos_setup(S, T, I, a.mode);
+      if (ntok && a.mode == A5X_MODE_REVERSE) wb = I.count * (u64)(I.L + 1);
+      else if (ntok && S.radix) wb = m_pos_prefix(S, I, I.count) - m_pos_prefix(S, I, 0);
+    }
+    if (m_lane() == 0) a.wbytes[w] = wb;
+  }
   m_err(a.err, gw ? 0u : I.bad);
 }
 
@@ -939,8 +950,13 @@ __device__ __forceinline__ void m_items(const A5xModeLaunch& a, int op, uint8_t 
   SL& S = *(SL*)m_dyn;
   const MT T = m_table(m_dyn + sizeof(SL), a.mtab, a.mtab_bytes);
   for (u64 i = a.item_begin + blockIdx.x; i < a.item_end; i += gridDim.x) {
-    if (a.flags[a.item_w[i]] & A5X_WF_GLOB) continue;
+    const u64 w = a.item_w[i];
+    if (a.flags[w] & A5X_WF_GLOB) continue;
     if (route && a.item_fl[i] != route) continue;
+    if (op == 0 && !route && a.wbytes[w] != ~0ull) {  // sized by k_mode_count (one item)
+      if (m_lane() == 0) { a.seg_bytes[i] = a.wbytes[w]; a.item_fl[i] = MI_POS; }
+      continue;
+    }
     m_item(S, T, a, i, op);
   }
 }
