@@ -18,5 +18,7 @@ ALGOS="ntlm" KRE=k_expand_fast_ntlm bash tools/gpu_digest_prof.sh || exit 17
 for alg in md5 ntlm; do
   timeout -k 10 300 python bench.py --digest $alg --workload c5 --words 2000000 --targets 1000000 --steps 3 --warmup 1 > gpurun_out/bench_${T}_digest_$alg.json 2> gpurun_out/bench_${T}_digest_$alg.err || { tail -5 gpurun_out/bench_${T}_digest_$alg.err; exit 18; }
 done
-timeout -k 10 300 python bench.py --mode 2 --workload c5 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_${T}_c5_mode2.json 2> gpurun_out/bench_${T}_c5_mode2.err || { tail -5 gpurun_out/bench_${T}_c5_mode2.err; exit 19; }
+for m in 1 2 3; do
+  timeout -k 10 300 python bench.py --mode $m --workload c5 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_${T}_c5_mode$m.json 2> gpurun_out/bench_${T}_c5_mode$m.err || { tail -5 gpurun_out/bench_${T}_c5_mode$m.err; exit 19; }
+done
 echo done
