@@ -91,7 +91,7 @@ struct MLdsT {
   uint8_t rr[MP_PMAX];       // R_r
   u32 ntok, radix, shift;
   u32 bitmap[A5X_MTAB_KEYS_MAX / 32];
-  uint8_t word[LMAX + 16];
+  alignas(16) uint8_t word[LMAX + 16];
   uint16_t pat[64];          // key index per sorted pattern (-s) / per position (-r)
   uint16_t pst[64];          // -r: start byte
   uint8_t pnx[64];           // -r: first later compatible position
@@ -130,6 +130,12 @@ struct MInfo {
 };
 
 __device__ __forceinline__ u32 m_lane() { return __lane_id(); }
+
+// 4 bytes at byte offset off of a 4-aligned LDS byte array (two dword reads + funnel shift)
+__device__ __forceinline__ u32 m_lds4(const uint8_t* base, u32 off) {
+  const u32* p = (const u32*)(base + (off & ~3u));
+  return __builtin_amdgcn_alignbyte(p[1], p[0], off & 3u);
+}
 
 __device__ __forceinline__ u32 m_incl_scan(u32 x) {
   const u32 lane = m_lane();
@@ -590,36 +596,98 @@ __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode) {
       S.ent[b + 1 + v] = m_entry(T.blob + V.off, V.len);
     }
   }
-  for (u32 q = lane; q < L; q += 64) {  // occurrences (distinct codepoints: at most one per byte)
+  // Occurrences and the token list, lane-parallel over bytes (L <= 128: two passes of
+  // 64).  Patterns are single codepoints (<= 4 bytes, compared as one masked dword), so at
+  // most one starts at a byte and occurrences never overlap; literal bytes form runs cut
+  // into <= 15-byte chunks.  Tokens in byte order: occurrences, literal chunks.
+  u32 pkey = 0, pmask = 0, plen = 0;
+  if (lane < n) {
+    const A5xMKey K = T.keys[S.pat[lane]];
+    const uint8_t* kp = T.blob + K.key_off;
+    for (u32 i = 0; i < K.klen; i++) pkey |= (u32)kp[i] << (8 * i);
+    plen = K.klen;
+    pmask = plen >= 4 ? 0xffffffffu : ((1u << (8 * plen)) - 1u);
+  }
+  for (u32 q0 = 0; q0 < L; q0 += 64) {
+    const u32 q = q0 + lane;
     u32 m = 0;
-    for (u32 i = 0; i < n && !m; i++)
-      if (m_match(T, S.word, L, q, S.pat[i])) m = i + 1;
-    S.mpi[q] = (uint8_t)m;
+    if (q < L) {
+      const u32 w4 = m_lds4(S.word, q);
+      for (u32 i = 0; i < n; i++) {
+        const u32 ki = (u32)__builtin_amdgcn_readlane((int)pkey, (int)i);
+        const u32 mi = (u32)__builtin_amdgcn_readlane((int)pmask, (int)i);
+        const u32 li = (u32)__builtin_amdgcn_readlane((int)plen, (int)i);
+        if (!m && (w4 & mi) == ki && q + li <= L) m = i + 1;
+      }
+      S.mpi[q] = (uint8_t)m;
+    }
   }
   M_WAVE_SYNC();
-  if (lane == 0) {  // token list: occurrences and <= 15-byte literal chunks, in byte order
-    u32 nt = 0, e = npe, q = 0;
-    bool over = false;
-    while (q < L) {
-      const u32 pi = S.mpi[q];
-      if (pi) {
-        S.tok[nt++] = S.pb[pi - 1] | (pi << 16);
-        S.occ[pi - 1]++;
-        q += T.keys[S.pat[pi - 1]].klen;
-      } else {
-        if (e >= MP_NE) { over = true; break; }
-        u32 k = 0;
-        u64 lo = 0, hi = 0;
-        while (q < L && !S.mpi[q] && k < 15) {
-          const u64 b = S.word[q];
-          if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
-          k++;
-          q++;
-        }
-        S.ent[e] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32) | (k << 24));
-        S.tok[nt++] = e++;
-      }
+  u32 nt = 0, nlit = 0, rs_carry = 0, occ = 0;
+  for (u32 q0 = 0; q0 < L; q0 += 64) {  // token starts, in order; positions -> S.elen (free here)
+    const u32 q = q0 + lane;
+    const bool in = q < L;
+    const u32 m = in ? S.mpi[q] : 0u;
+    bool cov = false;  // inside an occurrence that starts at q - 1 .. q - 3
+    for (u32 d = 1; d <= 3; d++) {
+      const u32 md = (in && q >= d) ? S.mpi[q - d] : 0u;
+      const u32 ld = (u32)__shfl((int)plen, (int)(md ? md - 1 : 0));
+      cov = cov || (md && ld > d);
     }
+    const bool lit = in && !m && !cov;
+    bool litp = false;  // byte q - 1 literal (lane 0: from the previous pass)
+    {
+      const u32 mp = (in && q >= 1) ? S.mpi[q - 1] : 1u;
+      bool covp = false;
+      for (u32 d = 2; d <= 4; d++) {
+        const u32 md = (in && q >= d) ? S.mpi[q - d] : 0u;
+        const u32 ld = (u32)__shfl((int)plen, (int)(md ? md - 1 : 0));
+        covp = covp || (md && ld > d - 1);
+      }
+      litp = q >= 1 && !mp && !covp;
+    }
+    // start of this byte's literal run (segmented max scan over lanes)
+    u32 rs = lit && !litp ? q + 1 : 0u;  // (q + 1: 0 = none)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const u32 y = (u32)__shfl_up((int)rs, d, 64);
+      if ((int)lane >= d) rs = max(rs, y);
+    }
+    rs = max(rs, rs_carry);
+    const u32 runq = rs ? rs - 1 : 0u;
+    const bool lstart = lit && ((q - runq) % 15u == 0u);
+    const bool tstart = (in && m) || lstart;
+    const u64 tb = __ballot(tstart), lb = __ballot(lstart);
+    const u32 ti = nt + (u32)__popcll(tb & ((1ull << lane) - 1ull));
+    const u32 li = nlit + (u32)__popcll(lb & ((1ull << lane) - 1ull));
+    if (tstart) {
+      S.elen[ti] = (uint8_t)q;
+      S.tok[ti] = m ? (S.pb[m - 1] | (m << 16)) : (npe + li);
+    }
+    for (u32 i = 0; i < n; i++) {
+      const u32 c = (u32)__popcll(__ballot(in && m == i + 1));
+      if (lane == i) occ += c;
+    }
+    nt += (u32)__popcll(tb);
+    nlit += (u32)__popcll(lb);
+    rs_carry = (u32)__builtin_amdgcn_readlane((int)rs, 63);
+  }
+  const bool over = npe + nlit > MP_NE;
+  if (lane < n) S.occ[lane] = (uint8_t)occ;
+  M_WAVE_SYNC();
+  if (!over) {  // literal chunk entries: bytes [q, next token start)
+    for (u32 k = lane; k < nt; k += 64) {
+      const u32 d = S.tok[k];
+      if (d >> 16) continue;
+      const u32 q = S.elen[k], qe = k + 1 < nt ? (u32)S.elen[k + 1] : L, len = qe - q;
+      const u32 x0 = m_lds4(S.word, q), x1 = m_lds4(S.word, q + 4), x2 = m_lds4(S.word, q + 8), x3 = m_lds4(S.word, q + 12);
+      u64 lo = (u64)x0 | ((u64)x1 << 32), hi = (u64)x2 | ((u64)x3 << 32);
+      lo = len >= 8 ? lo : (lo & ((1ull << (8 * len)) - 1ull));
+      hi = len >= 16 ? hi : len > 8 ? (hi & ((1ull << (8 * (len - 8))) - 1ull)) : 0ull;
+      S.ent[d] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, ((u32)(hi >> 32) & 0xFFFFFFu) | (len << 24));
+    }
+  }
+  if (lane == 0) {
     S.ntok = over ? 0u : nt;
     // radix mode: no effective size window (min <= 1, max >= #patterns) -- the leaves are
     // every per-pattern choice vector (minus the all-keep one when min = 1), enumerated
