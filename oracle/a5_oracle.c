@@ -657,7 +657,9 @@ A5O_EXPORT int64_t a5o_expand_batch(const a5o_table *t, const uint8_t *words, co
  * which serialised 16 senders on one futex; round 2's spin-then-yield kept every
  * blocked sender runnable, starving the writer whenever the host's CPU quota was
  * smaller than senders + 1.) */
-typedef struct { _Atomic size_t seq; bstr v; } chan_slot;
+/* A channel message: the candidate string and the worker whose pool it came from. */
+typedef struct { bstr v; int owner; } chan_msg;
+typedef struct { _Atomic size_t seq; chan_msg v; } chan_slot;
 typedef struct {
     chan_slot q[CHAN_CAP];
     _Alignas(64) _Atomic size_t tail;  /* next slot to send into */
@@ -683,7 +685,7 @@ static void futex_wake_all(_Atomic uint32_t *a) {
 
 #define CHAN_SPIN 64
 
-static void chan_send(chan_t *c, bstr s) {
+static void chan_send(chan_t *c, chan_msg s) {
     unsigned spins = 0;
     size_t pos = atomic_load_explicit(&c->tail, memory_order_relaxed);
     for (;;) {
@@ -721,7 +723,7 @@ static void chan_send(chan_t *c, bstr s) {
     }
 }
 
-static int chan_recv(chan_t *c, bstr *s) {
+static int chan_recv(chan_t *c, chan_msg *s) {
     unsigned spins = 0;
     const size_t pos = atomic_load_explicit(&c->head, memory_order_relaxed);
     chan_slot *sl = &c->q[pos & (CHAN_CAP - 1)];
@@ -765,24 +767,81 @@ static void chan_close(chan_t *c) {
     futex_wake_all(&c->tgen);
 }
 
+/* Candidate strings come from per-worker pools of 128-B slots that the writer hands
+ * back through a single-producer / single-consumer ring, like Go's per-P allocation
+ * caches with the garbage collector reclaiming the writer's consumed strings: no
+ * cross-thread malloc/free per candidate (glibc's arena locks made 16 workers slower
+ * than one).  Longer strings use malloc. */
+#define POOL_SLOT 128
+#define POOL_RET 8192   /* return ring per worker (power of two) */
+#define POOL_BLOCK (POOL_SLOT * 512)
+typedef struct {
+    uint8_t **ret;                      /* slots returned by the writer */
+    _Alignas(64) _Atomic size_t rhead;  /* consumed by the worker */
+    _Alignas(64) _Atomic size_t rtail;  /* produced by the writer */
+    _Alignas(64) uint8_t *blk; size_t blk_used;
+    uint8_t **blocks; size_t nblocks, cblocks;
+} str_pool;
+
+static uint8_t *pool_get(str_pool *P) {
+    const size_t h = atomic_load_explicit(&P->rhead, memory_order_relaxed);
+    if (h != atomic_load_explicit(&P->rtail, memory_order_acquire)) {
+        uint8_t *x = P->ret[h & (POOL_RET - 1)];
+        atomic_store_explicit(&P->rhead, h + 1, memory_order_release);
+        return x;
+    }
+    if (!P->blk || P->blk_used == POOL_BLOCK) {
+        if (P->nblocks == P->cblocks) {
+            P->cblocks = P->cblocks ? 2 * P->cblocks : 64;
+            P->blocks = (uint8_t **)xrealloc(P->blocks, P->cblocks * sizeof(uint8_t *));
+        }
+        P->blk = (uint8_t *)xrealloc(NULL, POOL_BLOCK);
+        P->blocks[P->nblocks++] = P->blk;
+        P->blk_used = 0;
+    }
+    uint8_t *x = P->blk + P->blk_used;
+    P->blk_used += POOL_SLOT;
+    return x;
+}
+
+static void pool_put(str_pool *P, uint8_t *x) {  /* writer side; a full ring keeps the slot */
+    const size_t t = atomic_load_explicit(&P->rtail, memory_order_relaxed);
+    if (t - atomic_load_explicit(&P->rhead, memory_order_acquire) >= POOL_RET) return;
+    P->ret[t & (POOL_RET - 1)] = x;
+    atomic_store_explicit(&P->rtail, t + 1, memory_order_release);
+}
+
 typedef struct {
     const a5o_table *t; const uint8_t *words; const uint64_t *off; size_t nw;
     int mode, mn, mx; chan_t ch; atomic_size_t next; atomic_int err; int fd;
     uint64_t out_cands, out_bytes;
+    str_pool *pools;
 } pipe_job;
 
+typedef struct { pipe_job *j; int id; } pipe_worker_arg;
+
 static void emit_chan(void *u, const uint8_t *s, size_t n) {
-    pipe_job *j = (pipe_job *)u;
-    chan_send(&j->ch, bdup(s, n));   /* Go: newWord is a fresh string; out <- newWord */
+    pipe_worker_arg *w = (pipe_worker_arg *)u;
+    chan_msg m;
+    m.owner = n + 1 <= POOL_SLOT ? w->id : -1;
+    if (m.owner >= 0) {
+        m.v.p = pool_get(&w->j->pools[w->id]);
+        if (n) memcpy(m.v.p, s, n);
+        m.v.p[n] = 0; m.v.n = n;
+    } else {
+        m.v = bdup(s, n);
+    }
+    chan_send(&w->j->ch, m);   /* Go: newWord is a fresh string; out <- newWord */
 }
 
 static void *pipe_worker(void *arg) {
-    pipe_job *j = (pipe_job *)arg;
+    pipe_worker_arg *w = (pipe_worker_arg *)arg;
+    pipe_job *j = w->j;
     for (;;) {
         size_t i = atomic_fetch_add(&j->next, 1);
         if (i >= j->nw) break;
         int rc = a5o_expand_word(j->t, j->words + j->off[i], (size_t)(j->off[i + 1] - j->off[i]),
-                                 j->mode, j->mn, j->mx, emit_chan, j);
+                                 j->mode, j->mn, j->mx, emit_chan, w);
         if (rc) atomic_store(&j->err, rc);
     }
     return NULL;
@@ -790,11 +849,13 @@ static void *pipe_worker(void *arg) {
 
 static void *pipe_writer(void *arg) {
     pipe_job *j = (pipe_job *)arg;
-    uint8_t wb[4096]; size_t wn = 0; bstr s;
-    while (chan_recv(&j->ch, &s)) {
+    uint8_t wb[4096]; size_t wn = 0; chan_msg m;
+    while (chan_recv(&j->ch, &m)) {
         /* writer.WriteString(s + "\n"): the concat allocates a new string */
+        bstr s = m.v;
         bstr line = bdup(s.p, s.n + 1); line.p[s.n] = '\n';
-        free(s.p);
+        if (m.owner >= 0) pool_put(&j->pools[m.owner], s.p);
+        else free(s.p);
         size_t n = line.n, o = 0;
         while (o < n) {
             size_t k = sizeof(wb) - wn; if (k > n - o) k = n - o;
@@ -820,13 +881,26 @@ A5O_EXPORT int a5o_run_pipeline(const a5o_table *t, const uint8_t *words, const 
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t wr, th[256];
+    pipe_worker_arg wa[256];
+    j->pools = NULL;
+    if (posix_memalign((void **)&j->pools, 64, (size_t)nthreads * sizeof(str_pool))) { free(j); return -1; }
+    memset(j->pools, 0, (size_t)nthreads * sizeof(str_pool));
+    for (int i = 0; i < nthreads; i++) {
+        j->pools[i].ret = (uint8_t **)xrealloc(NULL, POOL_RET * sizeof(uint8_t *));
+        atomic_init(&j->pools[i].rhead, 0); atomic_init(&j->pools[i].rtail, 0);
+    }
     pthread_create(&wr, NULL, pipe_writer, j);
-    for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, pipe_worker, j);
+    for (int i = 0; i < nthreads; i++) { wa[i].j = j; wa[i].id = i; pthread_create(&th[i], NULL, pipe_worker, &wa[i]); }
     for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
     chan_close(&j->ch);  /* close(out) after wg.Wait() */
     pthread_join(wr, NULL);
     *out_cands = j->out_cands; *out_bytes = j->out_bytes;
     int rc = atomic_load(&j->err);
+    for (int i = 0; i < nthreads; i++) {
+        for (size_t b = 0; b < j->pools[i].nblocks; b++) free(j->pools[i].blocks[b]);
+        free(j->pools[i].blocks); free(j->pools[i].ret);
+    }
+    free(j->pools);
     free(j);
     return rc;
 }
