@@ -1589,7 +1589,10 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
       c->dg_two_pass = false;
       if (rc && rc != A5X_E_CAPACITY) return rc;
       const uint64_t got = std::min(nh2, room);
-      for (uint64_t i = take; i < take + got; i++) hits[i].word = idx[hits[i].word];
+      for (uint64_t i = take; i < take + got; i++) {
+        if (hits[i].word >= m) return fail(c, A5X_E_HIP, "sub-batch hit word %llu of %u", (unsigned long long)hits[i].word, m);
+        hits[i].word = idx[hits[i].word];
+      }
       take += got;
       nh += nh2;
       ms_sub = st2.ms_total;

@@ -525,29 +525,34 @@ __device__ u32 m_rpos_setup(SL& S, const MT& T, const MInfo& I) {
     S.ent[2 * lane + 1] = m_entry(T.blob + T.vals[K.val_base].off, K.klen);
   }
   m_sync<SL>();
-  if (lane == 0) {  // tokens in byte order: literal chunks of <= 15 bytes and positions
-    u32 nt = 0, e = 2 * n, q = 0, j = 0;
-    bool over = false;
-    while (q < L) {
-      if (j < n && S.pst[j] == q) {
-        S.tok[nt++] = (2 * j) | ((j + 1) << 16);
-        q += T.keys[S.pat[j]].klen;
-        j++;
-      } else {
-        if (e >= MP_NE) { over = true; break; }
-        const u32 qe = j < n ? (u32)S.pst[j] : L;
-        u32 k = 0;
-        u64 lo = 0, hi = 0;
-        while (q < qe && k < 15) {
-          const u64 b = S.word[q];
-          if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
-          k++;
-          q++;
-        }
-        S.ent[e] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32) | (k << 24));
-        S.tok[nt++] = e++;
+  // tokens in byte order, lane-parallel: lane j <= n takes the literal gap before
+  // position j (j == n: after the last one), cut into <= 15-byte chunks, then position j
+  u32 gs = 0, ge = 0;
+  if (lane <= n) {
+    gs = lane == 0 ? 0u : (u32)S.pst[lane - 1] + T.keys[S.pat[lane - 1]].klen;
+    ge = lane < n ? (u32)S.pst[lane] : L;
+  }
+  const u32 nch = (lane <= n && ge > gs) ? (ge - gs + 14u) / 15u : 0u;
+  const u32 ntk = nch + (lane < n ? 1u : 0u);
+  const u32 tinc = m_incl_scan(ntk), cinc = m_incl_scan(nch);
+  const u32 nt = (u32)__builtin_amdgcn_readlane((int)tinc, 63);
+  const u32 nlit = (u32)__builtin_amdgcn_readlane((int)cinc, 63);
+  const bool over = 2 * n + nlit > MP_NE;
+  if (!over && lane <= n) {
+    const u32 t = tinc - ntk, e = 2 * n + cinc - nch;
+    for (u32 c = 0; c < nch; c++) {
+      const u32 q = gs + 15u * c, len = min(15u, ge - q);
+      u64 lo = 0, hi = 0;
+      for (u32 k = 0; k < len; k++) {
+        const u64 x = S.word[q + k];
+        if (k < 8) lo |= x << (8 * k); else hi |= x << (8 * (k - 8));
       }
+      S.ent[e + c] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32) | (len << 24));
+      S.tok[t + c] = e + c;
     }
+    if (lane < n) S.tok[t + nch] = (2 * lane) | ((lane + 1) << 16);
+  }
+  if (lane == 0) {
     S.ntok = over ? 0u : nt;
     S.radix = 0;
   }
