@@ -64,20 +64,41 @@ def parse():
                     help="fused expansion + digest + lookup (SURVEY 8(a) a8, configs[4]); use with --workload c5")
     ap.add_argument("--targets", type=int, default=1_000_000, help="target digests for --digest (planted + random)")
     ap.add_argument("--scratch-gb", type=float, default=8.0, help="device scratch for the --digest range loop")
+    ap.add_argument("--backend", default=os.environ.get("A5X_DIST_BACKEND", "nccl"), choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU collectives)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on device 0 (multi-rank tests on a one-GPU box)")
+    ap.add_argument("--steady-batches", type=int, default=4,
+                    help="also time this many batches through two contexts on two host threads (batch k+1's "
+                         "keyspace under batch k's expansion): the steady-state line; 0 = off")
+    ap.add_argument("--stdout", action="store_true",
+                    help="the reference's own output path (main.go:58-68): the CLI replica's stdout to /dev/null "
+                         "and to a pipe, and a5x_expand into a host sink (PCIe-inclusive rates, never `value` of "
+                         "the headline line)")
+    ap.add_argument("--dump", default=None,
+                    help="directory: per-rank per-word digests (expansion) / gathered hits (--digest) for tests")
     return ap.parse_args()
 
 
 class Dist:
-    def __init__(self, n_gpus: int):
+    """One process per GPU (torchrun env).  backend "nccl" is RCCL over xGMI on ROCm;
+    "gloo" runs the same collectives on the host (CPU tests, several ranks on one GPU)."""
+
+    def __init__(self, n_gpus: int, backend: str = "nccl", same_device: bool = False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.device = 0 if same_device else self.local  # the GPU this rank drives
+        self.backend = backend
         self.dist = None
         if self.world > 1:
             import torch
             import torch.distributed as dist
-            torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            if backend == "nccl":
+                torch.cuda.set_device(self.device)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.device))
+            else:
+                dist.init_process_group(backend)
             self.dist, self.torch = dist, torch
         if n_gpus != self.world and self.rank == 0:
             log(f"note: --gpus {n_gpus} but WORLD_SIZE={self.world}; using WORLD_SIZE")
@@ -90,7 +111,7 @@ class Dist:
     def reduce(self, x: float, op: str) -> float:
         if not self.dist:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda" if self.backend == "nccl" else "cpu")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
         return float(t.item())
 
@@ -123,7 +144,7 @@ def shard_for_rank(args, D, ctx):
     dw, do = DeviceBuffer.from_array(ctx, bd), DeviceBuffer.from_array(ctx, bo)
     lp = DeviceBuffer(ctx, (b1 - b0 + 1) * 8)
     ctx.keyspace_device(dw.ptr, do.ptr, b1 - b0, args.mode, args.min, args.max, d_byte_off=lp.ptr)
-    split = hd.distributed_split(D.dist, lp.to_array(np.uint64, count=b1 - b0 + 1), b0, n_total, D.world, "nccl")
+    split = hd.distributed_split(D.dist, lp.to_array(np.uint64, count=b1 - b0 + 1), b0, n_total, D.world, D.backend)
     for b in (dw, do, lp):
         b.free()
     ctx.clear_table()
@@ -149,19 +170,24 @@ digest_src_sha = kernel_src_sha
 
 
 def digest_profile(algo: str, words: int, kernel: str):
-    """VALU evidence of the digest kernel for THESE sources (tools/gpu_digest_prof.sh), else None."""
+    """VALU evidence of the digest kernel (tools/gpu.sh digestprof): the profile of THESE
+    sources when committed, else the newest one for the same kernel and size, flagged
+    (its int ops per candidate are those of the profiled sources)."""
     sha = digest_src_sha()
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_digest_*.json")), reverse=True):
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_digest_*.json")), key=os.path.getmtime, reverse=True):
         try:
             with open(f) as fh:
                 d = json.load(fh)
         except Exception:
             continue
-        if (d.get("algo") == algo and d.get("words") == words and d.get("kernel_src_sha") == sha
-                and d.get("kernel") == kernel):
+        if d.get("algo") == algo and d.get("words") == words and d.get("kernel") == kernel:
             d["_file"] = os.path.relpath(f, ROOT)
-            return d
-    return None
+            d["_sha_match"] = d.get("kernel_src_sha") == sha
+            if d["_sha_match"]:
+                return d
+            best = best or d
+    return best
 
 
 def latest_profile_traffic(workload: str, words: int):
@@ -253,57 +279,97 @@ def digest_cpu_baseline(tables, args):
                       f" per candidate, 1 thread"}
 
 
-def digest_roofline(args, tc, ms_dig, ms_exp):
+def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
     """Digest stage: VALU-bound.  achieved = integer lane-ops/s of the digest kernel (int
-    ops per candidate from the committed PMC profile of these sources x candidates /
-    stage time); peak = 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz 32-bit VALU ops (a
+    ops per candidate from the PMC profile (tools/gpu.sh digestprof) x candidates / stage
+    time); peak = 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz 32-bit VALU ops (a
     wave64 VALU instruction issues over 2 cycles: MI355X_MICROARCH.md; = the 157.3 TF f32
     FMA peak / 2).  Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm
-    expand, hash and probe in one kernel, so the stage time is the expansion time."""
+    expand, hash and probe in one kernel, so the stage time is the expansion time.  The
+    step's time is accounted as keyspace + stage (+ two-pass digest) + the rest (host)."""
     fused = ms_dig < 1e-3
-    kernel = f"k_expand_fast_{args.digest}" if fused else "k_digest_stream"
+    kernel = (f"k_expand_fast_{args.digest}" if args.mode == 0 else "k_mode_digest_pos") if fused else "k_digest_stream"
     ms_stage = ms_exp if fused else ms_dig
     prof = digest_profile(args.digest, args.words, kernel)
     peak = 256 * 4 * 32 * 2.4e9 / 1e12  # Tops/s
     r = {"bound": "valu", "kernel": kernel + ("" if fused else f"<{args.digest}>"), "fused": fused,
          "unit": "Tops/s (int32 lane ops)", "peak": peak, "ms_digest_per_step": ms_stage if not fused else 0.0,
-         "ms_expand_per_step": ms_exp, "digest_cand_per_s": tc / (ms_stage * 1e-3), "achieved": None, "frac": None,
-         "profile": None}
+         "ms_expand_per_step": ms_exp, "ms_keyspace_per_step": ms_ks, "ms_step": ms_step,
+         "ms_step_unaccounted": ms_step - ms_ks - ms_exp - (0.0 if fused else ms_dig),
+         "digest_cand_per_s": tc / (ms_stage * 1e-3), "achieved": None, "frac": None, "profile": None}
     if prof:
         ach = prof["int_ops_per_cand"] * tc / (ms_stage * 1e-3) / 1e12
         r.update(achieved=ach, frac=ach / peak, int_ops_per_cand=prof["int_ops_per_cand"],
                  valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"),
-                 profile=f"{prof['_file']} (kernel_src_sha {prof['kernel_src_sha'][:12]})")
+                 profile=f"{prof['_file']} (kernel_src_sha {prof['kernel_src_sha'][:12]}"
+                         f"{'' if prof['_sha_match'] else ', an earlier source revision'})")
     return r
 
 
+def plant_targets(args, D, ctx, data, offs, w0, algo):
+    """Targets of the C5 lookup: one candidate of each sampled word of the GLOBAL list
+    (every stride-th global word index, candidate chosen by a generator seeded with that
+    index, so the planted set does not depend on how the list is sharded), digested on
+    the device; each rank plants the sampled words of its shard and one all-gather
+    (dist.gather_rows_u64 to every rank via all-gather) gives every rank the same
+    target set, plus the same random digests.  Returns (planted [(global word, cand)],
+    target digests (n, 16) u8)."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer, dist as hd
+    n = len(offs) - 1
+    stride = max(1, (args.words * D.world) // 1000)
+    first = (w0 + stride - 1) // stride * stride
+    sample = list(range(first - w0, n, stride))
+    sw = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in sample]
+    cands = ctx.expand_words(sw, args.mode, args.min, args.max)
+    mine = [(w0 + w, int(np.random.default_rng(w0 + w).integers(0, len(c)))) for w, c in zip(sample, cands) if c]
+    lines = b"".join(cands[sample.index(g - w0)][k] + b"\n" for g, k in mine)
+    rows = np.zeros((len(mine), 4), dtype=np.uint64)
+    if mine:
+        lb = DeviceBuffer.from_array(ctx, np.frombuffer(lines, dtype=np.uint8))
+        db = DeviceBuffer(ctx, 16 * len(mine) + 16)
+        ctx.digest_lines_device(algo, lb.ptr, len(lines), db.ptr, len(mine))
+        dig = db.to_array(count=16 * len(mine)).reshape(-1, 16)
+        rows = hd.hits_to_rows([(g, k, bytes(dig[i])) for i, (g, k) in enumerate(mine)])
+    allrows = rows
+    if D.world > 1:  # every rank gets every rank's planted rows (an all-gather)
+        allrows = _allgather_rows(D, rows, hd.allgather_u64(D.dist, [len(rows)], D.backend)[:, 0])
+    planted = hd.rows_to_hits(allrows)
+    pd = np.frombuffer(b"".join(d for _, _, d in planted), dtype=np.uint8).reshape(-1, 16)
+    rng = np.random.default_rng(0xD16E57)  # the same random digests on every rank
+    rand = rng.integers(0, 256, size=(max(0, args.targets - len(planted)), 16), dtype=np.uint8)
+    return [(w, c) for w, c, _ in planted], np.concatenate([pd, rand])
+
+
+def _allgather_rows(D, rows, counts):
+    """Every rank's (n_r, 4) u64 rows on every rank (all-gather, padded to the largest n_r)."""
+    from hashcat_a5_table_generator_amd import dist as hd
+    m = int(counts.max())
+    pad = np.zeros((max(m, 1), 4), dtype=np.uint64)
+    pad[: len(rows)] = rows
+    flat = hd.allgather_u64(D.dist, pad.reshape(-1), D.backend)
+    return np.concatenate([flat[r].reshape(-1, 4)[: int(counts[r])] for r in range(D.world)])
+
+
 def run_digest(args, D):
-    """Fused expansion + MD5/NTLM + target lookup over a resident batch (configs[4] shape)."""
-    from hashcat_a5_table_generator_amd import ALGO_MD5, ALGO_NTLM, Context, DeviceBuffer, pack_words, synth
+    """Fused expansion + MD5/NTLM + target lookup over a resident batch (configs[4]
+    shape).  Multi-GPU (north_star (e)): every rank looks up its shard against the same
+    target set; the hit counts are all-reduced and the hit records -- word indices
+    rebased from the shard to the global list -- are gathered on rank 0, which checks
+    that every planted (global word, candidate) was found."""
+    from hashcat_a5_table_generator_amd import ALGO_MD5, ALGO_NTLM, Context, DeviceBuffer, dist as hd, synth
     algo = ALGO_MD5 if args.digest == "md5" else ALGO_NTLM
-    ctx = Context(D.local)
+    ctx = Context(D.device)
     tables, data, offs, (w0, w1) = shard_for_rank(args, D, ctx)
     n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)
     do = DeviceBuffer.from_array(ctx, offs)
     tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max)
-    # planted targets: one candidate of each of 1000 sampled words, digested by the device
-    rng = np.random.default_rng(0xD16E57 + D.rank)
-    sample = sorted(set(int(x) for x in rng.integers(0, n, size=1000)))
-    sw = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in sample]
-    cands = ctx.expand_words(sw, args.mode, args.min, args.max)
-    planted = [(w, int(rng.integers(0, len(c)))) for w, c in zip(sample, cands) if c]
-    lines = b"".join(cands[sample.index(w)][k] + b"\n" for w, k in planted)
-    lb = DeviceBuffer.from_array(ctx, np.frombuffer(lines, dtype=np.uint8))
-    db = DeviceBuffer(ctx, 16 * len(planted) + 16)
-    ctx.digest_lines_device(algo, lb.ptr, len(lines), db.ptr, len(planted))
-    pd = db.to_array(count=16 * len(planted)).reshape(-1, 16)
-    rand = rng.integers(0, 256, size=(max(0, args.targets - len(planted)), 16), dtype=np.uint8)
-    ctx.set_targets(algo, np.concatenate([pd, rand]))
+    planted, targets = plant_targets(args, D, ctx, data, offs, w0, algo)
+    ctx.set_targets(algo, targets)
     scratch = int(args.scratch_gb * (1 << 30))
-    log(f"rank {D.rank}: {n} words -> {tc} candidates, {tb / 1e9:.2f} GB; {args.targets} targets "
-        f"({len(planted)} planted)")
+    log(f"rank {D.rank}: words [{w0}, {w1}) -> {tc} candidates, {tb / 1e9:.2f} GB; {len(targets)} targets "
+        f"({len(planted)} planted over all ranks)")
 
     def step():
         return ctx.expand_digest_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max, scratch_bytes=scratch,
@@ -317,16 +383,23 @@ def run_digest(args, D):
     D.barrier()
     dt = time.perf_counter() - t0
     hits, st = res[-1]
-    got = {(w, c) for w, c, _ in hits}
-    missing = [p for p in planted if p not in got]
-    if missing:
-        raise SystemExit(f"digest lookup lost {len(missing)} planted hits, e.g. {missing[:3]}")
+    gathered = hd.gather_rows_u64(D.dist, hd.hits_to_rows(hits, word_base=w0), D.backend)  # rank 0: all ranks' hits
     dt_max = D.reduce(dt, "max")
     cands_all = D.reduce(float(tc) * args.steps, "sum")
     hits_all = D.reduce(float(len(hits)), "sum")
     ms_dig = float(np.mean([s["ms_total"] - s["ms_keyspace"] - s["ms_expand"] for _, s in res]))
     ms_exp = float(np.mean([s["ms_expand"] for _, s in res]))
+    ms_ks = float(np.mean([s["ms_keyspace"] for _, s in res]))
     if D.rank == 0:
+        got = {(w, c) for w, c, _ in hd.rows_to_hits(gathered)}
+        missing = [p for p in planted if p not in got]
+        if missing:
+            raise SystemExit(f"digest lookup lost {len(missing)} planted hits, e.g. {missing[:3]}")
+        if len(gathered) != int(hits_all):
+            raise SystemExit(f"gathered {len(gathered)} hit records, ranks report {int(hits_all)}")
+        if args.dump:
+            os.makedirs(args.dump, exist_ok=True)
+            np.save(os.path.join(args.dump, "hits.npy"), gathered)
         desc = synth.CONFIGS[args.workload][3]
         res_line = {
             "metric": "candidates/sec (whole node) at 1/2/4/8 MI355X + % HBM write roofline",
@@ -335,11 +408,14 @@ def run_digest(args, D):
             "scaling": "weak", "vs_baseline": None, "dtype": "u8/u32", "data": "synthetic",
             "config": {"workload": f"{args.workload}: {desc} + fused {args.digest.upper()} lookup (configs[4])",
                        "tables": tables, "words_per_gpu": n, "candidates_per_gpu_step": tc, "bytes_per_gpu_step": tb,
-                       "targets": args.targets, "planted": len(planted), "hits_all_ranks": hits_all,
+                       "targets": len(targets), "planted": len(planted), "hits_all_ranks": hits_all,
+                       "hits_gathered_on_rank0": len(gathered),
                        "mode": MODE_NAMES[args.mode], "table_min": args.min, "table_max": args.max,
                        "scratch_bytes": scratch,
-                       "parallelism": PARALLELISM.format(world=D.world) + "; hit counts all-reduced"},
-            "roofline": digest_roofline(args, tc, ms_dig, ms_exp),
+                       "parallelism": PARALLELISM.format(world=D.world) + "; one target set on every rank (planted "
+                                      "digests all-gathered); hit counts all-reduced, hit records gathered on rank 0 "
+                                      "with global word indices"},
+            "roofline": digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, dt_max / args.steps * 1e3),
             "cpu_baseline": None if args.no_cpu_baseline else digest_cpu_baseline(tables, args),
         }
         print(json.dumps(res_line), flush=True)
@@ -348,14 +424,164 @@ def run_digest(args, D):
     D.close()
 
 
+def steady_state(args, D, tables, tb1, n1):
+    """Whole-job throughput over a stream of batches: ``--steady-batches`` batches (words
+    disjoint from the headline batch and across ranks) already resident in HBM, run
+    through two contexts on two host threads, so batch k + 1's keyspace overlaps batch
+    k's expansion on the device (the CLI's pipeline, csrc/a5x_cli.cpp).  Batches are
+    sized so the two output buffers stay <= 100 GB.  Returns the steady-state record."""
+    import threading
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
+    nb = args.steady_batches
+    wpb = max(1, min(n1, int(n1 * 50e9 / max(tb1, 1))))
+    base = (D.world + D.rank * nb) * args.words  # past every rank's headline words
+    batches = []
+    ctxs = [Context(D.device) for _ in range(2)]
+    paths = [os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables]
+    for c in ctxs:
+        c.load_tables(paths)
+    for i in range(nb):
+        _, (bd, bo) = synth.global_words(args.workload, base + i * wpb, base + (i + 1) * wpb, seed=SEED)
+        batches.append((DeviceBuffer.from_array(ctxs[i & 1], bd), DeviceBuffer.from_array(ctxs[i & 1], bo)))
+    sizes = [ctxs[i & 1].keyspace_device(batches[i][0].ptr, batches[i][1].ptr, wpb, 0, args.min, args.max)
+             for i in range(nb)]
+    outs = [DeviceBuffer(ctxs[t], max(16, max(sz[1] for i, sz in enumerate(sizes) if (i & 1) == t)))
+            for t in range(min(2, nb))]
+    errs = []
+
+    def run(t):
+        try:
+            for i in range(t, nb, 2):
+                dw, do = batches[i]
+                ctxs[t].expand_device(dw.ptr, do.ptr, wpb, outs[t].ptr, sizes[i][1], 0, args.min, args.max)
+        except Exception as e:  # noqa: BLE001 -- reported after the join
+            errs.append(e)
+
+    def all_batches():
+        th = [threading.Thread(target=run, args=(t,)) for t in range(min(2, nb))]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if errs:
+            raise errs[0]
+
+    all_batches()  # warmup
+    D.barrier()
+    t0 = time.perf_counter()
+    all_batches()
+    D.barrier()
+    dt = D.reduce(time.perf_counter() - t0, "max")
+    cands = D.reduce(float(sum(c for c, _ in sizes)), "sum")
+    nbytes = D.reduce(float(sum(b for _, b in sizes)), "sum")
+    for dw, do in batches:
+        dw.free()
+        do.free()
+    for o in outs:
+        o.free()
+    for c in ctxs:
+        c.close()
+    log(f"steady state: {nb} batches x {wpb} words, {dt * 1e3 / nb:.2f} ms/batch, "
+        f"{nbytes / dt / 1e9:.0f} GB/s all ranks")
+    return {"batches": nb, "words_per_batch": wpb, "contexts": 2, "value": cands / dt, "unit": "candidates/s",
+            "ms_per_batch": dt * 1e3 / nb, "bytes_per_s": nbytes / dt,
+            "frac": nbytes / dt / D.world / (HBM_PEAK_GBS * 1e9),
+            "note": "whole job (keyspace + scan + plan + expansion) per batch, two contexts on two host threads: "
+                    "batch k+1's keyspace overlaps batch k's expansion; frac = algorithmic bytes / wall / GPUs / 8 TB/s"}
+
+
+PCIE_GBS = 64.0  # PCIe 5.0 x16, one direction, theoretical (MI355X host link)
+
+
+def run_stdout(args, D):
+    """Throughput of the drop-in's stdout path at the C3 shape: the CLI replica
+    (a5x_generator: streamed dictionary, two-context batch pipeline, 4 MiB stdio
+    buffer) writing "cand\n" to /dev/null and into a pipe drained by ``wc -c``, and
+    a5x_expand (double-buffered pinned D2H) handing every span to a no-op host sink.
+    Every byte crosses PCIe; the fraction is against 64 GB/s.  The CLI runs first, as
+    a child process, before this process touches the GPU."""
+    import ctypes
+    import subprocess
+    import tempfile
+    from hashcat_a5_table_generator_amd import synth
+    from hashcat_a5_table_generator_amd.build import CLI
+    tables, (data, offs) = synth.config_words(args.workload, args.words, seed=SEED)
+    n = len(offs) - 1
+    tpaths = [os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables]
+    body = bytes(data[: int(offs[-1])])
+    lens = np.diff(offs.astype(np.int64))
+    # the dictionary file: the words, one per line
+    ends = np.cumsum(lens)
+    text = bytearray(len(body) + n)
+    src = np.frombuffer(body, dtype=np.uint8)
+    dst = np.frombuffer(text, dtype=np.uint8)
+    pos = np.arange(len(body)) + np.repeat(np.arange(n), lens)
+    dst[pos] = src
+    dst[ends + np.arange(n)] = 10
+    runs = {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        dpath = os.path.join(td, "dict.txt")
+        with open(dpath, "wb") as f:
+            f.write(text)
+        cmd = [CLI, dpath] + sum((["-t", t] for t in tpaths), []) + ["-m", str(args.min), "-x", str(args.max)]
+        for name, shell in (("cli_devnull", None), ("cli_pipe_wc", " | wc -c")):
+            best = None
+            for _ in range(2):
+                t0 = time.perf_counter()
+                if shell is None:
+                    r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+                else:
+                    r = subprocess.run(["bash", "-o", "pipefail", "-c", " ".join(cmd) + shell], stdout=subprocess.PIPE,
+                                       stderr=subprocess.PIPE)
+                dt = time.perf_counter() - t0
+                if r.returncode:
+                    raise SystemExit(f"{name}: {r.stderr.decode(errors='replace')[-500:]}")
+                best = dt if best is None else min(best, dt)
+            runs[name] = best
+            if shell:
+                runs["pipe_bytes"] = int(r.stdout.split()[0])
+    from hashcat_a5_table_generator_amd import Context, _lib
+    ctx = Context(D.device)
+    ctx.load_tables(tpaths)
+    tc, tb = ctx.keyspace(data, offs, args.mode, args.min, args.max)
+    tc, tb = int(tc.sum()), int(tb.sum())
+    cb = _lib.SINK(lambda u, p, k: 0)
+    st = _lib.Stats()
+    lib_t = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ctx._chk(ctx._L.a5x_expand(ctx.h, data.ctypes.data, offs.ctypes.data, n, args.mode, args.min, args.max, cb,
+                                   None, ctypes.byref(st)))
+        dt = time.perf_counter() - t0
+        lib_t = dt if lib_t is None else min(lib_t, dt)
+    ctx.close()
+    if "pipe_bytes" in runs and runs["pipe_bytes"] != tb:
+        raise SystemExit(f"CLI wrote {runs['pipe_bytes']} bytes, keyspace says {tb}")
+
+    def rec(t):
+        return {"seconds": t, "candidates_per_s": tc / t, "GB_per_s": tb / t / 1e9, "pcie_frac": tb / t / 1e9 / PCIE_GBS}
+    desc = synth.CONFIGS[args.workload][3]
+    line = {"metric": "candidates/sec through the stdout path (main.go:58-68), PCIe-inclusive", "value": tc / runs["cli_devnull"],
+            "unit": "candidates/s", "n_gpus": 1, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"{args.workload}: {desc}", "words": n, "candidates": tc, "bytes": tb,
+                       "dict_bytes": len(text), "pcie_peak_GBps": PCIE_GBS},
+            "cli_devnull": rec(runs["cli_devnull"]), "cli_pipe_wc": rec(runs["cli_pipe_wc"]),
+            "a5x_expand_host_sink": rec(lib_t),
+            "note": "a5x_generator <dict> -t ... > /dev/null (and | wc -c): file read, batches of 4M words through "
+                    "two contexts, pinned double-buffered D2H, fwrite; a5x_expand: the same D2H into a no-op C sink"}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
-    D = Dist(args.gpus)
+    D = Dist(args.gpus, args.backend, args.same_device)
+    if args.stdout:
+        return run_stdout(args, D)
     if args.digest != "none":
         return run_digest(args, D)
     from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
 
-    ctx = Context(D.local)
+    ctx = Context(D.device)
     tables, data, offs, (w0, w1) = shard_for_rank(args, D, ctx)
     n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
@@ -385,17 +611,24 @@ def main():
     launches = stats[-1]["expand_launches"]
     ms_exp_max = D.reduce(ms_exp, "max")
 
-    if args.verify:
-        from oracle import c_oracle as co
+    if args.verify or args.dump:
         dig = DeviceBuffer(ctx, n * 32)
         ctx.digest_device(out.ptr, boff.ptr, 0, n, dig.ptr)
         got = dig.to_array(np.uint64).reshape(n, 4)
+        if args.dump:  # this rank's shard: per-word digests of words [w0, w1) of the global list
+            os.makedirs(args.dump, exist_ok=True)
+            np.save(os.path.join(args.dump, f"digest_{w0}_{w1}.npy"), got)
+    if args.verify:
+        from oracle import c_oracle as co
         want = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables]
                          ).digest_batch(data, offs, args.mode, args.min, args.max)
         bad = int((got != want).any(axis=1).sum())
         log(f"verify: {bad} mismatching words of {n}")
         if bad:
             raise SystemExit(f"verification failed on {bad} words")
+
+    out.free()
+    steady = steady_state(args, D, tables, tb, n) if args.steady_batches > 0 and args.mode == 0 else None
 
     if D.rank == 0:
         achieved = tb / (ms_exp * 1e-3) / 1e9  # GB/s, algorithmic bytes per launch / launch time
@@ -445,12 +678,13 @@ def main():
                 "algorithmic_bytes_per_launch": tb,
             },
             "cpu_baseline": None,
+            "steady_state": steady,
         }
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(tables, args)
         print(json.dumps(res), flush=True)
     D.barrier()
-    for b in (out, boff, dw, do):
+    for b in (boff, dw, do):
         b.free()
     ctx.close()
     D.close()

@@ -73,8 +73,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         subprocess.run(cmd, check=True)
         os.replace(LIB + ".tmp", LIB)
     cli_src = os.path.join(CSRC, "a5x_cli.cpp")
-    if os.path.exists(cli_src) and (force or _stale(CLI, [cli_src, LIB])):
-        cmd = [hipcc, "-O2", "-std=c++17", *inc, cli_src, "-o", CLI, "-L", OUT, "-la5x",
+    if os.path.exists(cli_src) and (force or _stale(CLI, [cli_src, LIB, os.path.join(CSRC, "a5x_gosem.h")])):
+        cmd = [hipcc, "-O2", "-std=c++17", "-pthread", *inc, cli_src, "-o", CLI, "-L", OUT, "-la5x",
                "-Wl,-rpath,$ORIGIN"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

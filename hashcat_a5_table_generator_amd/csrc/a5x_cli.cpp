@@ -18,11 +18,17 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
 #include "a5x.h"
+#include "a5x_gosem.h"
 
 static void usage(FILE* f) {
   fprintf(f,
@@ -42,6 +48,87 @@ static void usage(FILE* f) {
           "      --algo=md5                    Digest of --hashes: md5 (hashcat -m 0) or ntlm (-m 1000)\n");
 }
 
+// ---------------------------------------------------------------------------
+// Dictionary stream (main.go:52-56, 72-74): bufio.Scanner + ScanLines over the file in
+// bounded chunks -- LF split, one trailing CR dropped, a final unterminated line kept,
+// and the first line with no '\n' in 64 KiB (bufio.ErrTooLong) silently ends the input,
+// as the reference never checks scanner.Err().  At most one chunk of file bytes plus one
+// batch per pipeline slot is resident, whatever the dictionary size.
+// ---------------------------------------------------------------------------
+struct DictStream {
+  FILE* f = nullptr;
+  std::vector<uint8_t> buf;
+  size_t pos = 0, end = 0;
+  bool eof = false, stop = false;
+  explicit DictStream(FILE* fp, size_t chunk = (size_t)64 << 20) : f(fp), buf(chunk + a5x::gosem::kMaxScanToken) {}
+  // keep >= 64 KiB (or the rest of the file) past pos, so a line is cut exactly where
+  // the whole-file scanner would cut it
+  void fill() {
+    if (eof || end - pos >= a5x::gosem::kMaxScanToken) return;
+    memmove(buf.data(), buf.data() + pos, end - pos);
+    end -= pos;
+    pos = 0;
+    while (!eof && end < buf.size()) {
+      const size_t r = fread(buf.data() + end, 1, buf.size() - end, f);
+      if (r == 0) eof = true;
+      end += r;
+    }
+  }
+  // the next batch: up to max_words words / about max_bytes bytes (+16 B pad)
+  bool next(std::vector<uint8_t>& words, std::vector<uint64_t>& off, uint64_t max_words, size_t max_bytes) {
+    words.clear();
+    off.assign(1, 0);
+    while (!stop && off.size() - 1 < max_words && words.size() < max_bytes) {
+      fill();
+      const uint8_t* line;
+      size_t len;
+      const int r = a5x::gosem::scan_line(buf.data(), end, &pos, &line, &len);
+      if (r <= 0) { stop = true; break; }  // EOF, or ErrTooLong (silently the end, main.go:73)
+      words.insert(words.end(), line, line + len);
+      off.push_back(words.size());
+    }
+    words.resize(words.size() + 16, 0);
+    return off.size() > 1;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Batch pipeline: two liba5x contexts on the device, each driven by its own thread,
+// take alternate batches; batch k + 1's upload, keyspace and first range run while
+// batch k's output is still streaming to stdout.  Output stays in batch order: a
+// batch's sink waits for its turn (the reference's order across words is arbitrary,
+// main.go:77, but a deterministic stream is easier to check).
+// ---------------------------------------------------------------------------
+struct Turn {
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t turn = 0;
+  void wait(uint64_t k) {
+    std::unique_lock<std::mutex> l(mu);
+    cv.wait(l, [&] { return turn == k; });
+  }
+  void done(uint64_t k) {
+    std::lock_guard<std::mutex> l(mu);
+    turn = k + 1;
+    cv.notify_all();
+  }
+};
+
+struct SinkCtx {
+  Turn* t;
+  uint64_t k;
+  bool waited;
+};
+
+static int sink_ordered(void* user, const uint8_t* data, size_t len) {
+  SinkCtx* s = (SinkCtx*)user;
+  if (!s->waited) {
+    s->t->wait(s->k);
+    s->waited = true;
+  }
+  return fwrite(data, 1, len, stdout) == len ? 0 : 1;
+}
+
 static int sink_stdout(void* user, const uint8_t* data, size_t len) {
   (void)user;
   return fwrite(data, 1, len, stdout) == len ? 0 : 1;
@@ -52,25 +139,30 @@ static int hexv(int c) {
 }
 
 // target digests: one hex digest per line (32 hex digits; anything after them, e.g. a
-// ":plain" of a potfile line, is ignored); other lines are counted and skipped
+// ":plain" of a potfile line, is ignored); other lines are counted and skipped.  Whole
+// lines of any length (getline): a long potfile plain is one line, never a continuation
+// piece read as a target.
 static int load_targets(a5x_ctx* ctx, const char* path, int algo) {
   FILE* f = fopen(path, "rb");
   if (!f) return A5X_E_IO;
   std::vector<uint8_t> dig;
-  char line[4096];
+  char* line = nullptr;
+  size_t cap = 0;
+  ssize_t n;
   uint64_t bad = 0;
-  while (fgets(line, sizeof line, f)) {
+  while ((n = getline(&line, &cap, f)) >= 0) {
     size_t k = 0;
     uint8_t d[16];
-    for (; k < 32; k++) {
+    for (; k < 32 && k < (size_t)n; k++) {
       const int v = hexv((unsigned char)line[k]);
       if (v < 0) break;
       if (k & 1) d[k / 2] |= (uint8_t)v; else d[k / 2] = (uint8_t)(v << 4);
     }
-    const char t = line[32];
+    const char t = (size_t)n > 32 ? line[32] : 0;
     if (k == 32 && (t == 0 || t == '\n' || t == '\r' || t == ':')) dig.insert(dig.end(), d, d + 16);
-    else if (line[0] != '\n' && line[0] != '\r') bad++;
+    else if (n > 0 && line[0] != '\n' && line[0] != '\r') bad++;
   }
+  free(line);
   fclose(f);
   if (bad) fprintf(stderr, "a5_generator: %llu line(s) of %s are not 32-hex-digit hashes (skipped)\n",
                    (unsigned long long)bad, path);
@@ -165,44 +257,103 @@ int main(int argc, char** argv) {
   }
   FILE* f = fopen(dict.c_str(), "rb");
   if (!f) { perror(dict.c_str()); a5x_destroy(ctx); return 1; }
-  std::vector<uint8_t> data;
-  {
-    uint8_t buf[1 << 16];
-    size_t r;
-    while ((r = fread(buf, 1, sizeof buf, f)) > 0) data.insert(data.end(), buf, buf + r);
-    fclose(f);
-  }
-  uint64_t n = 0;
-  a5x_split_words(data.data(), data.size(), nullptr, nullptr, 0, &n);
-  std::vector<uint8_t> words(data.size() + 16);
-  std::vector<uint64_t> off(n + 2);
-  a5x_split_words(data.data(), data.size(), words.data(), off.data(), off.size(), &n);
   static char obuf[1 << 22];
   setvbuf(stdout, obuf, _IOFBF, sizeof obuf);
   const int mode = (suball ? A5X_MODE_SUBALL : A5X_MODE_DEFAULT) + (rev ? 1 : 0);
   if (!hashes.empty() && (rc = load_targets(ctx, hashes.c_str(), algo))) {
     fprintf(stderr, "a5_generator: %s\n", rc == A5X_E_IO ? "cannot read --hashes file" : a5x_last_error(ctx));
     a5x_destroy(ctx);
+    fclose(f);
     return 1;
   }
-  const uint64_t B = 1u << 22;
+  uint64_t B = 1u << 22;           // words per batch
+  size_t BB = (size_t)64 << 20;    // word bytes per batch
+  size_t chunk = (size_t)64 << 20; // dictionary bytes read at a time
+  // (test hooks: small batches / chunks exercise the pipeline and the chunk edges)
+  if (const char* e = getenv("A5X_CLI_BATCH")) B = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+  if (const char* e = getenv("A5X_CLI_CHUNK")) chunk = std::max<size_t>(1, strtoull(e, nullptr, 10));
+  DictStream ds(f, chunk);
+  if (hashes.empty()) {
+    // two contexts, two threads, alternate batches, ordered output
+    a5x_ctx* ctx2 = nullptr;
+    rc = a5x_create(device, &ctx2);
+    for (size_t t = 0; rc == 0 && t < tables.size(); t++) rc = a5x_load_table_file(ctx2, tables[t].c_str());
+    if (rc) {
+      fprintf(stderr, "a5_generator: %s\n", ctx2 ? a5x_last_error(ctx2) : "second context");
+      a5x_destroy(ctx2);
+      a5x_destroy(ctx);
+      fclose(f);
+      return 1;
+    }
+    a5x_ctx* cx[2] = {ctx, ctx2};
+    Turn turn;
+    std::mutex qmu;
+    std::condition_variable qcv;
+    std::deque<std::pair<uint64_t, std::pair<std::vector<uint8_t>, std::vector<uint64_t>>>> q[2];
+    bool done_reading = false;
+    std::atomic<int> failed{0};  // first error code (later batches are skipped)
+    std::string emsg;
+    auto worker = [&](int w) {
+      for (;;) {
+        std::pair<uint64_t, std::pair<std::vector<uint8_t>, std::vector<uint64_t>>> job;
+        {
+          std::unique_lock<std::mutex> l(qmu);
+          qcv.wait(l, [&] { return !q[w].empty() || done_reading; });
+          if (q[w].empty()) return;
+          job = std::move(q[w].front());
+          q[w].pop_front();
+          qcv.notify_all();
+        }
+        const uint64_t k = job.first;
+        auto& words = job.second.first;
+        auto& off = job.second.second;
+        SinkCtx sc{&turn, k, false};
+        const int r = failed.load() ? 0 : a5x_expand(cx[w], words.data(), off.data(), off.size() - 1, mode, tmin,
+                                                     tmax, sink_ordered, &sc, nullptr);
+        if (!sc.waited) turn.wait(k);  // (a batch with no output still takes its turn)
+        int zero = 0;
+        if (r && failed.compare_exchange_strong(zero, r)) emsg = a5x_last_error(cx[w]);
+        turn.done(k);
+      }
+    };
+    std::thread th0(worker, 0), th1(worker, 1);
+    for (uint64_t k = 0;; k++) {
+      std::vector<uint8_t> words;
+      std::vector<uint64_t> off;
+      if (!ds.next(words, off, B, BB)) break;
+      std::unique_lock<std::mutex> l(qmu);
+      qcv.wait(l, [&] { return q[k & 1].empty() || failed.load(); });  // one batch ahead per context
+      if (failed.load()) break;
+      q[k & 1].emplace_back(k, std::make_pair(std::move(words), std::move(off)));
+      qcv.notify_all();
+    }
+    {
+      std::lock_guard<std::mutex> l(qmu);
+      done_reading = true;
+      qcv.notify_all();
+    }
+    th0.join();
+    th1.join();
+    rc = failed.load();
+    fclose(f);
+    fflush(stdout);
+    if (rc) fprintf(stderr, "a5_generator: %s\n", emsg.c_str());
+    a5x_destroy(ctx2);
+    a5x_destroy(ctx);
+    return rc ? 2 : 0;
+  }
+  std::vector<uint8_t> words;
   std::vector<uint64_t> sub;
   std::vector<a5x_hit> hits(1 << 16);
   std::unordered_set<std::string> cracked;  // each target reported once (hashcat potfile)
-  for (uint64_t b0 = 0; b0 < n && rc == 0; b0 += B) {
-    const uint64_t b1 = b0 + B < n ? b0 + B : n;
-    sub.resize(b1 - b0 + 1);
-    for (uint64_t i = b0; i <= b1; i++) sub[i - b0] = off[i] - off[b0];
-    const uint8_t* wb = words.data() + off[b0];
-    if (hashes.empty()) {
-      rc = a5x_expand(ctx, wb, sub.data(), b1 - b0, mode, tmin, tmax, sink_stdout, nullptr, nullptr);
-      continue;
-    }
+  while (rc == 0 && ds.next(words, sub, B, BB)) {
+    const uint64_t nb = sub.size() - 1;
+    const uint8_t* wb = words.data();
     uint64_t nh = 0;
-    rc = a5x_expand_digest(ctx, wb, sub.data(), b1 - b0, mode, tmin, tmax, hits.data(), hits.size(), &nh, nullptr);
+    rc = a5x_expand_digest(ctx, wb, sub.data(), nb, mode, tmin, tmax, hits.data(), hits.size(), &nh, nullptr);
     if (rc == A5X_E_CAPACITY && nh > hits.size()) {
       hits.resize(nh);
-      rc = a5x_expand_digest(ctx, wb, sub.data(), b1 - b0, mode, tmin, tmax, hits.data(), hits.size(), &nh, nullptr);
+      rc = a5x_expand_digest(ctx, wb, sub.data(), nb, mode, tmin, tmax, hits.data(), hits.size(), &nh, nullptr);
     }
     if (rc) break;
     // stream order, then the first candidate of each digest
@@ -212,9 +363,10 @@ int main(int argc, char** argv) {
     std::vector<a5x_hit> first;
     for (uint64_t h = 0; h < nh; h++)
       if (cracked.insert(std::string((const char*)hits[h].digest, 16)).second) first.push_back(hits[h]);
-    rc = a5x_format_hits(ctx, wb, sub.data(), b1 - b0, mode, tmin, tmax, first.data(), first.size(), sink_stdout,
+    rc = a5x_format_hits(ctx, wb, sub.data(), nb, mode, tmin, tmax, first.data(), first.size(), sink_stdout,
                          nullptr);
   }
+  fclose(f);
   fflush(stdout);
   if (rc) fprintf(stderr, "a5_generator: %s\n", a5x_last_error(ctx));
   a5x_destroy(ctx);

@@ -31,12 +31,9 @@ typedef uint64_t u64;
 typedef uint32_t u32;
 
 // stream bytes per wave: 4 KiB for MD5 (lanes stay busy over ~3 rounds of candidates),
-// 2 KiB for NTLM (its per-lane UTF-16 buffers also live in LDS)
+// 2 KiB for NTLM (the MD4 of UTF-16LE costs about twice per candidate byte)
 template <bool MD5> struct DCfg { static constexpr u32 BLK = MD5 ? 4096u : 2048u; };
 constexpr u32 DMARGIN = 256;               // next-block bytes staged for straddling lines
-constexpr u32 USTRIDE = 132;               // NTLM UTF-16 buffer per lane (64 units + pad)
-constexpr u32 UMAX = 128;                  // UTF-16LE bytes per candidate (64 units)
-constexpr u32 D_ERR_LONG = 1u << 9;        // an NTLM candidate beyond 64 UTF-16 units
 constexpr u32 D_ERR_HITCAP = 1u << 10;     // more hits than the caller's buffer
 
 __device__ __forceinline__ u32 d_lane() { return __lane_id(); }
@@ -57,6 +54,14 @@ __device__ __forceinline__ u32 glob4(const uint8_t* base, u64 off, u64 lim) {
     if (off + k < lim) v |= (u32)base[off + k] << (8 * k);
   return v;
 }
+
+// message bytes in HBM (lines that run past the staged bytes): 4 bytes at message
+// offset i, zero past the stream end
+struct MdGlob {
+  const uint8_t* g;
+  u64 off, lim;
+  __device__ __forceinline__ u32 at4(u32 i) const { return glob4(g, off + i, lim); }
+};
 
 // Merkle-Damgard over message bytes [0, len) of src (LDS, or global when lds == false):
 // RFC 1321/1320 padding (0x80, zeros, 64-bit little-endian bit length).
@@ -85,49 +90,6 @@ __device__ __forceinline__ void md_digest(const uint8_t* lbase, u32 loff, const 
   }
 }
 
-// Go []rune(string) + utf16.Encode of candidate bytes into UTF-16LE bytes at dst;
-// returns the byte length, or UMAX + 2 when it does not fit.
-__device__ u32 utf16le(const uint8_t* lbase, u32 loff, const uint8_t* gbase, u64 goff, bool lds, u32 len,
-                       uint8_t* dst) {
-  auto at = [&](u32 i) -> u32 { return lds ? (u32)lbase[loff + i] : (u32)gbase[goff + i]; };
-  u32 o = 0, i = 0;
-  while (i < len) {
-    const u32 b0 = at(i);
-    u32 r = 0xFFFDu, sz = 1;
-    if (b0 < 0x80u) {
-      r = b0;
-    } else {
-      u32 size = 0, lo = 0x80u, hi = 0xBFu;
-      if (b0 >= 0xC2u && b0 <= 0xDFu) size = 2;
-      else if (b0 >= 0xE0u && b0 <= 0xEFu) { size = 3; if (b0 == 0xE0u) lo = 0xA0u; else if (b0 == 0xEDu) hi = 0x9Fu; }
-      else if (b0 >= 0xF0u && b0 <= 0xF4u) { size = 4; if (b0 == 0xF0u) lo = 0x90u; else if (b0 == 0xF4u) hi = 0x8Fu; }
-      if (size && i + size <= len) {
-        const u32 b1 = at(i + 1);
-        bool ok = b1 >= lo && b1 <= hi;
-        for (u32 k = 2; ok && k < size; k++) { const u32 bk = at(i + k); ok = bk >= 0x80u && bk <= 0xBFu; }
-        if (ok) {
-          sz = size;
-          if (size == 2) r = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
-          else if (size == 3) r = ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (at(i + 2) & 0x3Fu);
-          else r = ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((at(i + 2) & 0x3Fu) << 6) | (at(i + 3) & 0x3Fu);
-        }
-      }
-    }
-    i += sz;
-    if (r >= 0x10000u) {
-      if (o + 4 > UMAX) return UMAX + 2;
-      const u32 v = r - 0x10000u, h = 0xD800u + (v >> 10), l = 0xDC00u + (v & 0x3FFu);
-      dst[o] = (uint8_t)h; dst[o + 1] = (uint8_t)(h >> 8); dst[o + 2] = (uint8_t)l; dst[o + 3] = (uint8_t)(l >> 8);
-      o += 4;
-    } else {
-      if (o + 2 > UMAX) return UMAX + 2;
-      dst[o] = (uint8_t)r; dst[o + 1] = (uint8_t)(r >> 8);
-      o += 2;
-    }
-  }
-  return o;
-}
-
 __device__ __forceinline__ bool probe(const A5xDigLaunch& a, const u32* d) {
   return md_probe(a.bitmap, a.bm_mask, a.table, a.tmask, a.has_zero_target != 0, d);
 }
@@ -150,9 +112,8 @@ __global__ void __launch_bounds__(256) k_digest_stream(A5xDigLaunch a, int op) {
   typedef DWave<DBLK> WT;
   constexpr u32 DBUF = WT::BUF;
   constexpr u32 NM = DBLK / 2048u;  // 32-bit newline masks per lane (32 B each)
-  const u32 per = (u32)sizeof(WT) + (MD5 ? 0u : 64u * USTRIDE);
+  const u32 per = (u32)sizeof(WT);
   WT& W = *(WT*)(d_dyn + wv * ((per + 15u) & ~15u));
-  uint8_t* ubuf = (uint8_t*)&W + sizeof(WT) + lane * USTRIDE;
   const u64 nblk = (a.nbytes + DBLK - 1) / DBLK;
   u32 err = 0;
   for (u64 blk = (u64)blockIdx.x * nwv + wv; blk < nblk; blk += (u64)gridDim.x * nwv) {
@@ -241,10 +202,17 @@ __global__ void __launch_bounds__(256) k_digest_stream(A5xDigLaunch a, int op) {
       u32 d[4];
       if (MD5) {
         md_digest<true>(W.data, s, a.out, bs + s, a.nbytes, in_lds, len, d);
+      } else if (in_lds) {  // any length: the UTF-16LE units are made as MD4 blocks fill
+        MdLds src;
+        src.base = W.data;
+        src.off = s;
+        ntlm_stream(src, len, d);
       } else {
-        const u32 ul = utf16le(W.data, s, a.out, bs + s, in_lds, len, ubuf);
-        if (ul > UMAX) { err |= D_ERR_LONG; continue; }
-        md_digest<false>(ubuf, 0, nullptr, 0, 0, true, ul, d);
+        MdGlob src;
+        src.g = a.out;
+        src.off = bs + s;
+        src.lim = a.nbytes;
+        ntlm_stream(src, len, d);
       }
       if (op == 2) {
         uint4* o4 = (uint4*)(a.dig_out + 16 * (a.blk_pre[blk] + i));
@@ -325,8 +293,7 @@ hipError_t a5x_launch_gather_words(const uint8_t* words, const uint64_t* woff, c
 }
 
 size_t a5x_digest_lds(int algo) {
-  const u32 per = algo == A5X_ALGO_MD5 ? (u32)sizeof(DWave<DCfg<true>::BLK>)
-                                       : (u32)sizeof(DWave<DCfg<false>::BLK>) + 64u * USTRIDE;
+  const u32 per = algo == A5X_ALGO_MD5 ? (u32)sizeof(DWave<DCfg<true>::BLK>) : (u32)sizeof(DWave<DCfg<false>::BLK>);
   return 4u * ((per + 15u) & ~15u);
 }
 

@@ -25,6 +25,9 @@
 #ifndef FX6_ZBE
 #define FX6_ZBE 255      // the window entry that holds the empty piece (set by the includer)
 #endif
+#ifndef FX_PIPE
+#define FX_PIPE 1        // fx7_round, > FX_HOLDNB pieces: entry reads one candidate ahead of the ORs
+#endif
 
 // (FxRun, the wave's staging state, and the ring flush are defined by the includer.)
 
@@ -259,17 +262,38 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
       }
     } else
 #endif
-    {
+    if constexpr (HOLD) {
 #pragma unroll
-    for (int c = 0; c < K; c++) {
+      for (int c = 0; c < K; c++)
 #pragma unroll
-      for (int b = 0; b < NB; b++) {
-        uint4 e;
-        if constexpr (HOLD) e = ent[c][b];
-        else e = be[idx[c][b]];
-        fx7_put<NOOR>(e, P, sink);
+        for (int b = 0; b < NB; b++) fx7_put<NOOR>(ent[c][b], P, sink);
+    } else if constexpr (!FX_PIPE) {
+#pragma unroll
+      for (int c = 0; c < K; c++)
+#pragma unroll
+        for (int b = 0; b < NB; b++) fx7_put<NOOR>(be[idx[c][b]], P, sink);
+    } else {
+      // Entries read again here, one candidate ahead: candidate c + 1's NB reads are
+      // issued before candidate c's ORs (in the same basic block, ahead of the puts'
+      // uniform branches), so each candidate waits only for its own reads
+      // (lgkmcnt(#ORs since)).  Read right before its put, every piece cost a full LDS
+      // round trip behind the previous piece's ORs (s_waitcnt lgkmcnt(0)).
+      uint4 cur[NB], nxt[NB];
+#pragma unroll
+      for (int b = 0; b < NB; b++) cur[b] = be[idx[0][b]];
+#pragma unroll
+      for (int c = 0; c < K; c++) {
+        if (c + 1 < K) {
+#pragma unroll
+          for (int b = 0; b < NB; b++) nxt[b] = be[idx[c + 1][b]];
+        }
+#pragma unroll
+        for (int b = 0; b < NB; b++) fx7_put<NOOR>(cur[b], P, sink);
+        if (c + 1 < K) {
+#pragma unroll
+          for (int b = 0; b < NB; b++) cur[b] = nxt[b];
+        }
       }
-    }
     }
   }
   (void)nsm;

@@ -90,8 +90,11 @@ struct a5x_ctx {
   DevBuf<uint8_t> m_item_fl;  // per item: the layout that expands it (a5x_modes.hip m_item)
   DevBuf<uint32_t> m_item_w;
   uint64_t m_items = 0;
-  uint64_t m_nglob = 0;
-  bool dg_two_pass = false;   // a5x_expand_digest_device: the hybrid's sub-batch call (no fused path)       // mode pass G words of the current batch (their list: glob)
+  uint64_t m_nglob = 0;       // mode pass G words of the current batch (their list: glob)
+  // hybrid fused digest: the non-FAST words of a batch gathered into a sub-batch
+  DevBuf<uint32_t> hy_list;
+  DevBuf<uint64_t> hy_lens, hy_off;
+  DevBuf<uint8_t> hy_words;
   uint8_t* mgscr = nullptr;   // mode pass G scratch: A5X_G_SLOTS x a5x_mode_gslot_bytes(), on first use
   uint64_t mseg = 1024;  // candidates per mode-engine item
   // fused digest + lookup (a5x_digest.hip)
@@ -592,8 +595,11 @@ A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_
 // Keyspace of the -r / -s / -s -r engines: per-word counts (DP), items of mseg
 // candidates, a length pass over every item (output bytes are not closed-form under
 // sequential strings.ReplaceAll), and the scans.  Synchronises twice.
+// lengths = false (the fused digest): counts and items only -- no length pass, no
+// output layout (B->total_bytes = 0).
 int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn,
-                      int mx, uint64_t* d_cand_off, uint64_t* d_byte_off, hipStream_t st, Batch* B, bool timed) {
+                      int mx, uint64_t* d_cand_off, uint64_t* d_byte_off, hipStream_t st, Batch* B, bool timed,
+                      bool lengths = true) {
   int rc;
   if ((rc = upload_mtable(c))) return rc;
   if (nw > 0xffffffffull) return fail(c, A5X_E_ARG, "batch of %llu words (max 2^32-1)", (unsigned long long)nw);
@@ -686,10 +692,15 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   M.cand_off = d_cand_off;
   M.item_begin = 0;
   M.item_end = items;
-  if (items) {
-    HIPCHK(c, a5x_launch_plan(c->m_seg_off.p, nw, 1, c->m_item_w.p, st));
-    HIPCHK(c, a5x_launch_mode_items(M, 0, st));
+  if (items) HIPCHK(c, a5x_launch_plan(c->m_seg_off.p, nw, 1, c->m_item_w.p, st));
+  if (!lengths) {
+    HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+    B->total_bytes = 0;
+    return A5X_OK;
   }
+  if (items) HIPCHK(c, a5x_launch_mode_items(M, 0, st));
   if (items)
     HIPCHK(c, a5x_launch_scan(c->m_seg_bytes.p, c->m_seg_bytes.p, items, c->m_seg_boff.p, c->m_tmp.p,
                               c->scan_tmp.p, c->d_scalars + 2, st));
@@ -714,6 +725,7 @@ struct Job {
   uint64_t nw = 0;
   int mode = 0, mn = 0, mx = 0;
   hipStream_t st = nullptr;
+  bool lengths = true;  // -r / -s engines: output layout wanted (false: the fused digest)
   Batch B;
 };
 
@@ -725,7 +737,8 @@ struct Range {
 int job_prepare(a5x_ctx* c, Job& J, uint64_t* d_cand_off, uint64_t* d_byte_off, bool timed) {
   int rc;
   if (J.mode != A5X_MODE_DEFAULT)
-    return run_keyspace_mode(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, d_cand_off, d_byte_off, J.st, &J.B, timed);
+    return run_keyspace_mode(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, d_cand_off, d_byte_off, J.st, &J.B, timed,
+                             J.lengths);
   if ((rc = run_keyspace(c, J.w, J.wo, J.nw, J.mn, J.mx, d_cand_off, d_byte_off, J.st, &J.B, timed))) return rc;
   if (J.B.total_cands) {  // chunk -> first word map, consumed by every range's k_expand_fast
     const uint64_t nchunks = (J.B.total_cands + c->chunk - 1) / c->chunk;
@@ -954,6 +967,261 @@ int dig_block_prefix(a5x_ctx* c, A5xDigLaunch& D, hipStream_t st, uint64_t* tota
   return A5X_OK;
 }
 
+static_assert(sizeof(a5x_hit) == sizeof(A5xHitRaw), "resolved device hits are copied out as a5x_hit");
+
+// a5x_expand_digest_device.  allow_fused: default-mode batches take the fused kernel
+// (the hybrid's sub-batch of non-FAST words passes false: those words are exactly the
+// ones the fused kernel skips).
+int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn, int mx,
+                  uint64_t scratch_bytes, a5x_hit* hits, uint64_t hit_cap, uint64_t* n_hits, a5x_stats* stats,
+                  hipStream_t st, bool allow_fused) {
+  int rc;
+  Job J;
+  job_open(c, J, d_words, d_woff, nw, mode, mn, mx, st);
+  J.lengths = mode == A5X_MODE_DEFAULT || !allow_fused;  // the fused -r / -s digest needs no layout
+  if ((rc = grow(c, c->dg_cand_off, nw + 1)) || (rc = grow(c, c->dg_byte_off, nw + 1))) return rc;
+  if ((rc = job_prepare(c, J, c->dg_cand_off.p, c->dg_byte_off.p, true))) return rc;
+  const uint64_t tc = J.B.total_cands, tb = J.B.total_bytes;
+  // Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm hash each FAST
+  // word's candidates in the LDS ring where they are built -- no HBM scratch, no second
+  // pass, hits already (word, candidate).  The other candidate-bearing words (slow / BIG
+  // / pass G) are gathered into a sub-batch for the two-pass path (hybrid).  Modes
+  // -r / -s / -s -r: the two-pass range loop below.
+  if (mode != A5X_MODE_DEFAULT && allow_fused) {
+    // -r / -s / -s -r: every item's candidates hashed where the engine builds them
+    // (positional ring or byte-builder buffer), hits as (word, candidate) directly
+    uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
+    if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+    uint64_t nh = 0;
+    float ms = 0;
+    for (;;) {
+      A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx);
+      const A5xDigLaunch D = dig_launch(c);
+      M.cand_off = J.B.cand_off;
+      M.item_begin = 0;
+      M.item_end = c->m_items;
+      M.dg_algo = c->t_algo;
+      M.dg_bitmap = D.bitmap; M.dg_bm_mask = D.bm_mask; M.dg_has_zero = D.has_zero_target;
+      M.dg_table = D.table; M.dg_tmask = D.tmask;
+      M.dg_hits = c->dg_hits.p; M.dg_hit_cap = (uint32_t)dev_hits; M.dg_nhits = c->d_scalars + 8;
+      HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
+      HIPCHK(c, hipEventRecord(c->ev[1], J.st));
+      HIPCHK(c, a5x_launch_mode_items(M, 2, J.st));
+      HIPCHK(c, hipEventRecord(c->ev[2], J.st));
+      HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      HIPCHK(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+      if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+      nh = c->h_scalars[8];
+      if (nh <= dev_hits || hit_cap <= dev_hits) break;
+      dev_hits = std::min<uint64_t>(nh, hit_cap);  // run again with room for every hit the caller takes
+      if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+    }
+    const uint64_t take = std::min(std::min(nh, dev_hits), hit_cap);
+    if (take) {
+      HIPCHK(c, hipMemcpyAsync(hits, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+    }
+    float a = 0;
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    a5x_stats total;
+    memset(&total, 0, sizeof total);
+    total.words = nw;
+    total.candidates = tc;
+    total.expand_launches = 1;
+    total.ms_keyspace = a;
+    total.ms_expand = ms;  // build + digest + lookup, fused
+    total.ms_total = a + ms;
+    if (n_hits) *n_hits = nh;
+    if (stats) *stats = total;
+    if (nh > hit_cap)
+      return fail(c, A5X_E_CAPACITY, "%llu hits, buffer has %llu", (unsigned long long)nh, (unsigned long long)hit_cap);
+    return A5X_OK;
+  }
+  const bool fused = mode == A5X_MODE_DEFAULT && tc > 0 && allow_fused;
+  const bool hybrid = fused && (J.B.nslow || J.B.nbig || J.B.nglob);
+  if (fused) {
+    uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
+    if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+    uint64_t nh = 0;
+    float ms = 0;
+    for (;;) {
+      A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
+      const A5xDigLaunch D = dig_launch(c);
+      E.cand_begin = 0;
+      E.cand_end = tc;
+      E.dg_bitmap = D.bitmap; E.dg_bm_mask = D.bm_mask; E.dg_has_zero = D.has_zero_target;
+      E.dg_table = D.table; E.dg_tmask = D.tmask;
+      E.dg_hits = c->dg_hits.p; E.dg_hit_cap = (uint32_t)dev_hits; E.dg_nhits = c->d_scalars + 8;
+      HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
+      HIPCHK(c, hipEventRecord(c->ev[1], J.st));
+      HIPCHK(c, a5x_launch_expand(E, c->t_algo == A5X_ALGO_MD5 ? 3 : 5, J.st));
+      HIPCHK(c, hipEventRecord(c->ev[2], J.st));
+      HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      HIPCHK(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+      if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
+      nh = c->h_scalars[8];
+      if (nh <= dev_hits || hit_cap <= dev_hits) break;
+      dev_hits = std::min<uint64_t>(nh, hit_cap);  // run again with room for every hit the caller takes
+      if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+    }
+    uint64_t take = std::min(std::min(nh, dev_hits), hit_cap);
+    if (take) {
+      HIPCHK(c, hipMemcpyAsync(hits, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+    }
+    float a = 0;  // this batch's keyspace (before the sub-batch reuses the events)
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    float ms_sub = 0;
+    if (hybrid) {
+      // The words the fused kernel skipped, in batch order, as a compact sub-batch in
+      // the context's hybrid buffers (sized with grow(): no per-call allocation).
+      // Host memory touched with device-produced values: idx[] (sized by the device count
+      // m, itself bounded by nw) and the caller's hits[take, take + got) with got <= room.
+      if ((rc = grow(c, c->hy_list, std::max<uint64_t>(1, nw)))) return rc;
+      HIPCHK(c, hipMemsetAsync(c->d_scalars + 9, 0, 4, J.st));
+      HIPCHK(c, a5x_launch_nonfast_list(c->flags.p, J.B.cand_off, nw, c->hy_list.p, c->d_scalars + 9, J.st));
+      HIPCHK(c, hipMemcpyAsync(c->h_scalars + 9, c->d_scalars + 9, 4, hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      const uint32_t m = c->h_scalars[9];
+      if (m > nw) return fail(c, A5X_E_HIP, "non-FAST word list of %u words in a batch of %llu", m, (unsigned long long)nw);
+      std::vector<uint32_t> idx(m);
+      std::vector<uint64_t> off((size_t)m + 1, 0);
+      if ((rc = grow(c, c->hy_lens, (size_t)m + 1)) || (rc = grow(c, c->hy_off, (size_t)m + 1))) return rc;
+      if (m) {
+        HIPCHK(c, hipMemcpyAsync(idx.data(), c->hy_list.p, (size_t)m * 4, hipMemcpyDeviceToHost, J.st));
+        HIPCHK(c, hipStreamSynchronize(J.st));
+        std::sort(idx.begin(), idx.end());
+        HIPCHK(c, hipMemcpyAsync(c->hy_list.p, idx.data(), (size_t)m * 4, hipMemcpyHostToDevice, J.st));
+        HIPCHK(c, a5x_launch_gather_words(J.w, J.wo, c->hy_list.p, m, c->hy_lens.p, nullptr, nullptr, J.st));
+        HIPCHK(c, hipMemcpyAsync(off.data() + 1, c->hy_lens.p, (size_t)m * 8, hipMemcpyDeviceToHost, J.st));
+        HIPCHK(c, hipStreamSynchronize(J.st));
+        for (uint32_t k = 0; k < m; k++) off[k + 1] += off[k];
+      }
+      if ((rc = grow(c, c->hy_words, off[m] + 16))) return rc;
+      HIPCHK(c, hipMemcpyAsync(c->hy_off.p, off.data(), ((size_t)m + 1) * 8, hipMemcpyHostToDevice, J.st));
+      HIPCHK(c, hipMemsetAsync(c->hy_words.p, 0, off[m] + 16, J.st));
+      HIPCHK(c, a5x_launch_gather_words(J.w, J.wo, c->hy_list.p, m, nullptr, c->hy_off.p, c->hy_words.p, J.st));
+      // their candidates through the two-pass path; hit word indices mapped back to the batch
+      const uint64_t room = hit_cap > take ? hit_cap - take : 0;
+      uint64_t nh2 = 0;
+      a5x_stats st2;
+      memset(&st2, 0, sizeof st2);
+      rc = expand_digest(c, c->hy_words.p, c->hy_off.p, m, mode, mn, mx, scratch_bytes, room ? hits + take : nullptr,
+                         room, &nh2, &st2, J.st, false);
+      if (rc && rc != A5X_E_CAPACITY) return rc;
+      const uint64_t got = std::min(nh2, room);
+      for (uint64_t i = take; i < take + got; i++) {
+        if (hits[i].word >= m)
+          return fail(c, A5X_E_HIP, "sub-batch hit word %llu of %u", (unsigned long long)hits[i].word, m);
+        hits[i].word = idx[hits[i].word];
+      }
+      take += got;
+      nh += nh2;
+      ms_sub = st2.ms_total;
+    }
+    a5x_stats total;
+    memset(&total, 0, sizeof total);
+    total.words = nw;
+    total.candidates = tc;
+    total.bytes = tb;
+    total.expand_launches = 1;
+    total.ms_keyspace = a;
+    total.ms_expand = ms + ms_sub;  // expansion + digest + lookup: fused (+ the two-pass sub-batch)
+    total.ms_total = a + ms + ms_sub;
+    if (n_hits) *n_hits = nh;
+    if (stats) *stats = total;
+    if (nh > hit_cap)
+      return fail(c, A5X_E_CAPACITY, "%llu hits, buffer has %llu", (unsigned long long)nh,
+                  (unsigned long long)hit_cap);
+    return A5X_OK;
+  }
+  uint64_t cap = scratch_bytes ? scratch_bytes : ((uint64_t)2 << 30);
+  cap = std::max<uint64_t>(4096, std::min<uint64_t>(cap, tb + 64));
+  std::vector<Range> ranges;
+  if ((rc = plan_ranges(c, J, cap, ranges))) return rc;
+  if ((rc = grow(c, c->dg_scratch, cap + 64))) return rc;
+  uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
+  if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+  a5x_stats total;
+  memset(&total, 0, sizeof total);
+  total.words = nw;
+  total.candidates = tc;
+  total.bytes = tb;
+  uint64_t found = 0, copied = 0;
+  float ms_exp = 0, ms_dig = 0, ms_ks = 0;
+  HIPCHK(c, hipEventRecord(c->ev[3], J.st));  // the keyspace (and the range plan) ends here
+  HIPCHK(c, hipEventSynchronize(c->ev[3]));
+  HIPCHK(c, hipEventElapsedTime(&ms_ks, c->ev[0], c->ev[3]));
+  for (const Range& R : ranges) {
+    HIPCHK(c, hipEventRecord(c->ev[1], J.st));
+    if ((rc = job_launch(c, J, R, c->dg_scratch.p, cap))) return rc;
+    HIPCHK(c, hipEventRecord(c->ev[2], J.st));
+    A5xDigLaunch D = dig_launch(c);
+    D.out = c->dg_scratch.p;
+    D.nbytes = R.b1 - R.b0;
+    const uint64_t nblk = a5x_digest_blocks(D.nbytes, D.algo);
+    if ((rc = grow(c, c->dg_blk_cnt, nblk + 1)) || (rc = grow(c, c->dg_blk_pre, nblk + 1)) ||
+        (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nblk + 1) + 16)))
+      return rc;
+    D.blk_cnt = c->dg_blk_cnt.p;
+    uint64_t nh = 0;
+    {
+      float me = 0;  // the range's expansion, once (a retry below re-runs only the digest)
+      HIPCHK(c, hipEventSynchronize(c->ev[2]));
+      HIPCHK(c, hipEventElapsedTime(&me, c->ev[1], c->ev[2]));
+      ms_exp += me;
+    }
+    for (;;) {  // a range with more hits than the device buffer is digested again with room for all
+      D.hits = c->dg_hits.p;
+      D.hit_cap = (uint32_t)dev_hits;
+      D.nhits = c->d_scalars + 8;
+      HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
+      HIPCHK(c, hipEventRecord(c->dev_ev[0], J.st));
+      HIPCHK(c, a5x_launch_digest_stream(D, 0, dig_grid(c), J.st));
+      HIPCHK(c, hipEventRecord(c->dev_ev[1], J.st));
+      HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      float md = 0;
+      HIPCHK(c, hipEventElapsedTime(&md, c->dev_ev[0], c->dev_ev[1]));
+      ms_dig += md;
+      const uint32_t e = c->h_scalars[2] & ~(1u << 10);
+      if ((rc = decode_dev_err(c, e))) return rc;
+      nh = c->h_scalars[8];
+      if (nh <= dev_hits || copied >= hit_cap) break;
+      dev_hits = nh;  // grow and run this range's digest again (its candidates are still in scratch)
+      if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
+      HIPCHK(c, hipMemsetAsync(c->d_scalars + 2, 0, 4, J.st));
+    }
+    if (nh) {
+      const uint64_t got = std::min<uint64_t>(nh, dev_hits);
+      HIPCHK(c, a5x_launch_scan(c->dg_blk_cnt.p, c->dg_blk_cnt.p, nblk, c->dg_blk_pre.p, c->dg_blk_pre.p,
+                                c->scan_tmp.p, c->d_scalars + 2, J.st));
+      HIPCHK(c, a5x_launch_hits_resolve(c->dg_hits.p, (uint32_t)got, c->dg_blk_pre.p, R.cb, c->dg_cand_off.p, nw,
+                                        J.st));
+      const uint64_t take = std::min(hit_cap - std::min(hit_cap, copied), got);
+      if (take)
+        HIPCHK(c, hipMemcpyAsync(hits + copied, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, J.st));
+      HIPCHK(c, hipStreamSynchronize(J.st));
+      copied += take;
+      found += nh;
+    }
+    total.expand_launches += 1;
+  }
+  total.ms_keyspace = ms_ks;
+  total.ms_expand = ms_exp;
+  total.ms_total = total.ms_keyspace + ms_exp + ms_dig;
+  total.words_slow = J.B.nslow;
+  total.words_pass_b = J.B.nbig;
+  if (n_hits) *n_hits = found;
+  if (stats) *stats = total;
+  if (found > hit_cap)
+    return fail(c, A5X_E_CAPACITY, "%llu hits, buffer has %llu", (unsigned long long)found,
+                (unsigned long long)hit_cap);
+  return A5X_OK;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1017,6 +1285,7 @@ void a5x_destroy(a5x_ctx* c) {
   release(c->m_item_w);
   release(c->t_bitmap); release(c->t_table); release(c->dg_scratch); release(c->dg_blk_cnt); release(c->dg_blk_pre);
   release(c->dg_cand_off); release(c->dg_byte_off); release(c->dg_hits);
+  release(c->hy_list); release(c->hy_lens); release(c->hy_off); release(c->hy_words);
   for (auto& e : c->dev_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->d_mtab) (void)hipFree(c->d_mtab);
@@ -1373,7 +1642,11 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   std::vector<u64> wrec(FX_WREC + FW_PMAX + 16, 0);
   ArraySink sk;
   sk.rec = wrec.data(); sk.np = ff_np(C.flags);
-  const Plan P = plan_word<true>(gw, (u32)len, T, sk);
+  // (diagnostics: A5X_BAL_SLACK8 overrides the balanced big-piece slack of the device
+  // build, FB_BAL_SLACK8, for the window simulation in tools/window_sim.py)
+  u32 slack = FB_BAL_SLACK8;
+  if (const char* e = getenv("A5X_BAL_SLACK8")) slack = (u32)atoi(e);
+  const Plan P = plan_word<true>(gw, (u32)len, T, sk, fb_balanced_cap(C.count + 1, slack));
   wrec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
   wrec[FX_ZSLOT] = 0;
   if (!P.ok || P.ng != ff_ng(C.flags) || P.ne != ff_ne(C.flags) || P.np != ff_np(C.flags))
@@ -1487,8 +1760,6 @@ int a5x_set_targets(a5x_ctx* c, int algo, const uint8_t* dig, uint64_t n) {
   return A5X_OK;
 }
 
-static_assert(sizeof(a5x_hit) == sizeof(A5xHitRaw), "resolved device hits are copied out as a5x_hit");
-
 int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode,
                              int mn, int mx, uint64_t scratch_bytes, a5x_hit* hits, uint64_t hit_cap,
                              uint64_t* n_hits, a5x_stats* stats, void* stream) {
@@ -1498,203 +1769,9 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
   int rc;
   if ((rc = check_mode(c, mode))) return rc;
   HIPCHK(c, hipSetDevice(c->device));
-  Job J;
-  job_open(c, J, d_words, d_woff, nw, mode, mn, mx, stream ? (hipStream_t)stream : c->stream);
-  if ((rc = grow(c, c->dg_cand_off, nw + 1)) || (rc = grow(c, c->dg_byte_off, nw + 1))) return rc;
-  if ((rc = job_prepare(c, J, c->dg_cand_off.p, c->dg_byte_off.p, true))) return rc;
-  const uint64_t tc = J.B.total_cands, tb = J.B.total_bytes;
-  // Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm hash each FAST
-  // word's candidates in the LDS ring where they are built -- no HBM scratch, no second
-  // pass, hits already (word, candidate).  The other candidate-bearing words (slow / BIG
-  // / pass G) are gathered into a sub-batch for the two-pass path (hybrid).  Modes
-  // -r / -s / -s -r: the two-pass range loop below.
-  const bool fused = mode == A5X_MODE_DEFAULT && tc > 0 && !c->dg_two_pass && !getenv("A5X_NO_FUSED_DIGEST");
-  const bool hybrid = fused && (J.B.nslow || J.B.nbig || J.B.nglob);
-  if (fused) {
-    uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
-    if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
-    uint64_t nh = 0;
-    float ms = 0;
-    for (;;) {
-      A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
-      const A5xDigLaunch D = dig_launch(c);
-      E.cand_begin = 0;
-      E.cand_end = tc;
-      E.dg_bitmap = D.bitmap; E.dg_bm_mask = D.bm_mask; E.dg_has_zero = D.has_zero_target;
-      E.dg_table = D.table; E.dg_tmask = D.tmask;
-      E.dg_hits = c->dg_hits.p; E.dg_hit_cap = (uint32_t)dev_hits; E.dg_nhits = c->d_scalars + 8;
-      HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
-      HIPCHK(c, hipEventRecord(c->ev[1], J.st));
-      HIPCHK(c, a5x_launch_expand(E, c->t_algo == A5X_ALGO_MD5 ? 3 : 5, J.st));
-      HIPCHK(c, hipEventRecord(c->ev[2], J.st));
-      HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
-      HIPCHK(c, hipStreamSynchronize(J.st));
-      HIPCHK(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
-      if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
-      nh = c->h_scalars[8];
-      if (nh <= dev_hits || hit_cap <= dev_hits) break;
-      dev_hits = std::min<uint64_t>(nh, hit_cap);  // run again with room for every hit the caller takes
-      if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
-    }
-    uint64_t take = std::min(std::min(nh, dev_hits), hit_cap);
-    if (take) {
-      HIPCHK(c, hipMemcpyAsync(hits, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, J.st));
-      HIPCHK(c, hipStreamSynchronize(J.st));
-    }
-    float a = 0;  // this batch's keyspace (before the sub-batch reuses the events)
-    HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-    float ms_sub = 0;
-    if (hybrid) {
-      // the words the fused kernel skipped, in batch order, as a compact sub-batch
-      struct DTmp {
-        void* p = nullptr;
-        ~DTmp() { if (p) (void)hipFree(p); }
-      } d_list, d_n, d_lens, d_off, d_sw;
-      HIPCHK(c, hipMalloc(&d_list.p, std::max<uint64_t>(1, nw) * 4));
-      HIPCHK(c, hipMalloc(&d_n.p, 4));
-      HIPCHK(c, hipMemsetAsync(d_n.p, 0, 4, J.st));
-      HIPCHK(c, a5x_launch_nonfast_list(c->flags.p, J.B.cand_off, nw, (uint32_t*)d_list.p, (uint32_t*)d_n.p, J.st));
-      uint32_t m = 0;
-      HIPCHK(c, hipMemcpyAsync(&m, d_n.p, 4, hipMemcpyDeviceToHost, J.st));
-      HIPCHK(c, hipStreamSynchronize(J.st));
-      std::vector<uint32_t> idx(m);
-      if (m) HIPCHK(c, hipMemcpy(idx.data(), d_list.p, (size_t)m * 4, hipMemcpyDeviceToHost));
-      std::sort(idx.begin(), idx.end());
-      std::vector<uint64_t> off((size_t)m + 1, 0);
-      if (m) {
-        HIPCHK(c, hipMemcpy(d_list.p, idx.data(), (size_t)m * 4, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMalloc(&d_lens.p, (size_t)m * 8));
-        HIPCHK(c, a5x_launch_gather_words(J.w, J.wo, (const uint32_t*)d_list.p, m, (uint64_t*)d_lens.p, nullptr, nullptr,
-                                          J.st));
-        HIPCHK(c, hipMemcpyAsync(off.data() + 1, d_lens.p, (size_t)m * 8, hipMemcpyDeviceToHost, J.st));
-        HIPCHK(c, hipStreamSynchronize(J.st));
-        for (uint32_t k = 0; k < m; k++) off[k + 1] += off[k];
-      }
-      HIPCHK(c, hipMalloc(&d_off.p, ((size_t)m + 1) * 8));
-      HIPCHK(c, hipMemcpy(d_off.p, off.data(), ((size_t)m + 1) * 8, hipMemcpyHostToDevice));
-      HIPCHK(c, hipMalloc(&d_sw.p, off[m] + 16));
-      HIPCHK(c, hipMemsetAsync(d_sw.p, 0, off[m] + 16, J.st));
-      HIPCHK(c, a5x_launch_gather_words(J.w, J.wo, (const uint32_t*)d_list.p, m, nullptr, (const uint64_t*)d_off.p,
-                                        (uint8_t*)d_sw.p, J.st));
-      HIPCHK(c, hipStreamSynchronize(J.st));
-      // their candidates through the two-pass path (the recursion sees no FAST word, or
-      // fewer words); hit word indices mapped back to the batch
-      const uint64_t room = hit_cap > take ? hit_cap - take : 0;
-      uint64_t nh2 = 0;
-      a5x_stats st2;
-      memset(&st2, 0, sizeof st2);
-      c->dg_two_pass = true;  // (the sub-batch's words are the ones the fused kernel skips)
-      rc = a5x_expand_digest_device(c, (const uint8_t*)d_sw.p, (const uint64_t*)d_off.p, m, mode, mn, mx,
-                                    scratch_bytes, room ? hits + take : nullptr, room, &nh2, &st2, stream);
-      c->dg_two_pass = false;
-      if (rc && rc != A5X_E_CAPACITY) return rc;
-      const uint64_t got = std::min(nh2, room);
-      for (uint64_t i = take; i < take + got; i++) {
-        if (hits[i].word >= m) return fail(c, A5X_E_HIP, "sub-batch hit word %llu of %u", (unsigned long long)hits[i].word, m);
-        hits[i].word = idx[hits[i].word];
-      }
-      take += got;
-      nh += nh2;
-      ms_sub = st2.ms_total;
-    }
-    a5x_stats total;
-    memset(&total, 0, sizeof total);
-    total.words = nw;
-    total.candidates = tc;
-    total.bytes = tb;
-    total.expand_launches = 1;
-    total.ms_keyspace = a;
-    total.ms_expand = ms + ms_sub;  // expansion + digest + lookup: fused (+ the two-pass sub-batch)
-    total.ms_total = a + ms + ms_sub;
-    if (n_hits) *n_hits = nh;
-    if (stats) *stats = total;
-    if (nh > hit_cap)
-      return fail(c, A5X_E_CAPACITY, "%llu hits, buffer has %llu", (unsigned long long)nh,
-                  (unsigned long long)hit_cap);
-    return A5X_OK;
-  }
-  uint64_t cap = scratch_bytes ? scratch_bytes : ((uint64_t)2 << 30);
-  cap = std::max<uint64_t>(4096, std::min<uint64_t>(cap, tb + 64));
-  std::vector<Range> ranges;
-  if ((rc = plan_ranges(c, J, cap, ranges))) return rc;
-  if ((rc = grow(c, c->dg_scratch, cap + 64))) return rc;
-  uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
-  if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
-  a5x_stats total;
-  memset(&total, 0, sizeof total);
-  total.words = nw;
-  total.candidates = tc;
-  total.bytes = tb;
-  uint64_t found = 0, copied = 0;
-  float ms_exp = 0, ms_dig = 0;
-  for (const Range& R : ranges) {
-    HIPCHK(c, hipEventRecord(c->ev[1], J.st));
-    if ((rc = job_launch(c, J, R, c->dg_scratch.p, cap))) return rc;
-    HIPCHK(c, hipEventRecord(c->ev[2], J.st));
-    A5xDigLaunch D = dig_launch(c);
-    D.out = c->dg_scratch.p;
-    D.nbytes = R.b1 - R.b0;
-    const uint64_t nblk = a5x_digest_blocks(D.nbytes, D.algo);
-    if ((rc = grow(c, c->dg_blk_cnt, nblk + 1)) || (rc = grow(c, c->dg_blk_pre, nblk + 1)) ||
-        (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nblk + 1) + 16)))
-      return rc;
-    D.blk_cnt = c->dg_blk_cnt.p;
-    uint64_t nh = 0;
-    for (;;) {  // a range with more hits than the device buffer is digested again with room for all
-      D.hits = c->dg_hits.p;
-      D.hit_cap = (uint32_t)dev_hits;
-      D.nhits = c->d_scalars + 8;
-      HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
-      HIPCHK(c, hipEventRecord(c->dev_ev[0], J.st));
-      HIPCHK(c, a5x_launch_digest_stream(D, 0, dig_grid(c), J.st));
-      HIPCHK(c, hipEventRecord(c->dev_ev[1], J.st));
-      HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
-      HIPCHK(c, hipStreamSynchronize(J.st));
-      float me = 0, md = 0;
-      HIPCHK(c, hipEventElapsedTime(&me, c->ev[1], c->ev[2]));
-      HIPCHK(c, hipEventElapsedTime(&md, c->dev_ev[0], c->dev_ev[1]));
-      ms_exp += me;
-      ms_dig += md;
-      const uint32_t e = c->h_scalars[2] & ~(1u << 10);
-      if (e & (1u << 9))
-        return fail(c, A5X_E_UNSUPPORTED, "an NTLM candidate is longer than 64 UTF-16 code units (device limit)");
-      if ((rc = decode_dev_err(c, e))) return rc;
-      nh = c->h_scalars[8];
-      if (nh <= dev_hits || copied >= hit_cap) break;
-      dev_hits = nh;  // grow and run this range's digest again (its candidates are still in scratch)
-      if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
-      HIPCHK(c, hipMemsetAsync(c->d_scalars + 2, 0, 4, J.st));
-    }
-    if (nh) {
-      const uint64_t got = std::min<uint64_t>(nh, dev_hits);
-      HIPCHK(c, a5x_launch_scan(c->dg_blk_cnt.p, c->dg_blk_cnt.p, nblk, c->dg_blk_pre.p, c->dg_blk_pre.p,
-                                c->scan_tmp.p, c->d_scalars + 2, J.st));
-      HIPCHK(c, a5x_launch_hits_resolve(c->dg_hits.p, (uint32_t)got, c->dg_blk_pre.p, R.cb, c->dg_cand_off.p, nw,
-                                        J.st));
-      const uint64_t take = std::min(hit_cap - std::min(hit_cap, copied), got);
-      if (take)
-        HIPCHK(c, hipMemcpyAsync(hits + copied, c->dg_hits.p, take * sizeof(a5x_hit), hipMemcpyDeviceToHost, J.st));
-      HIPCHK(c, hipStreamSynchronize(J.st));
-      copied += take;
-      found += nh;
-    }
-    total.expand_launches += 1;
-  }
-  total.ms_keyspace = 0;
-  {
-    float a = 0;
-    if (hipEventElapsedTime(&a, c->ev[0], c->ev[1]) == hipSuccess && ranges.size() <= 1) total.ms_keyspace = a;
-  }
-  total.ms_expand = ms_exp;
-  total.ms_total = total.ms_keyspace + ms_exp + ms_dig;
-  total.words_slow = J.B.nslow;
-  total.words_pass_b = J.B.nbig;
-  if (n_hits) *n_hits = found;
-  if (stats) *stats = total;
-  if (found > hit_cap)
-    return fail(c, A5X_E_CAPACITY, "%llu hits, buffer has %llu", (unsigned long long)found,
-                (unsigned long long)hit_cap);
-  return A5X_OK;
+  const bool fused = !getenv("A5X_NO_FUSED_DIGEST");
+  return expand_digest(c, d_words, d_woff, nw, mode, mn, mx, scratch_bytes, hits, hit_cap, n_hits, stats,
+                       stream ? (hipStream_t)stream : c->stream, fused);
 }
 
 int a5x_expand_digest(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
@@ -1737,8 +1814,6 @@ int a5x_digest_lines_device(a5x_ctx* c, int algo, const uint8_t* d_lines, uint64
   HIPCHK(c, a5x_launch_digest_stream(D, 2, dig_grid(c), st));
   HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
-  if (c->h_scalars[2] & (1u << 9))
-    return fail(c, A5X_E_UNSUPPORTED, "an NTLM candidate is longer than 64 UTF-16 code units (device limit)");
   return decode_dev_err(c, c->h_scalars[2]);
 }
 
@@ -1801,16 +1876,18 @@ int a5x_format_plain(const uint8_t* plain, size_t len, uint8_t* out, size_t cap,
   return A5X_OK;
 }
 
-static int collect_sink(void* user, const uint8_t* data, size_t len) {
-  ((std::string*)user)->append((const char*)data, len);
-  return 0;
-}
-
 int a5x_format_hits(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
                     const a5x_hit* hits, uint64_t n_hits, a5x_sink_fn sink, void* user) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
   if (!c || !sink || (n_hits && (!hits || !words || !woff))) return A5X_E_ARG;
   if (!n_hits) return A5X_OK;
-  // the hit words, once each, as a sub-batch; their candidates regenerated on the device
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  // The hit words, once each, as a sub-batch; only the hit candidates themselves are
+  // regenerated on the device (located, then expanded as single-candidate ranges, or
+  // one range per run of nearby hits), never a hit word's whole keyspace: a word's
+  // output may exceed host memory and 2^32 bytes.
   std::vector<uint64_t> uw(n_hits);
   for (uint64_t h = 0; h < n_hits; h++) {
     if (hits[h].word >= nw) return fail(c, A5X_E_ARG, "hit word index beyond the batch");
@@ -1825,33 +1902,98 @@ int a5x_format_hits(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint
     so.push_back(sb.size());
   }
   sb.resize(sb.size() + 16, 0);
-  std::vector<uint64_t> cnt(uw.size()), byt(uw.size());
-  int rc;
-  if ((rc = a5x_keyspace(c, sb.data(), so.data(), uw.size(), mode, mn, mx, cnt.data(), byt.data()))) return rc;
-  std::string cand;
-  if ((rc = a5x_expand(c, sb.data(), so.data(), uw.size(), mode, mn, mx, collect_sink, &cand, nullptr))) return rc;
-  std::vector<uint64_t> base(uw.size() + 1, 0);
-  for (size_t k = 0; k < uw.size(); k++) base[k + 1] = base[k] + byt[k];
-  if (base.back() != cand.size()) return fail(c, A5X_E_ARG, "hit words re-expanded to an unexpected size");
-  std::vector<std::vector<uint32_t>> starts(uw.size());  // line starts per hit word (built on demand)
+  const uint64_t m = uw.size();
+  if ((rc = grow(c, c->s_words, sb.size())) || (rc = grow(c, c->s_woff, m + 1))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->s_words.p, sb.data(), sb.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->s_woff.p, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  Job J;
+  job_open(c, J, c->s_words.p, c->s_woff.p, m, mode, mn, mx, c->stream);
+  if ((rc = job_prepare(c, J, nullptr, nullptr, false))) return rc;
+  std::vector<uint64_t> coff(m + 1);
+  HIPCHK(c, hipMemcpyAsync(coff.data(), J.B.cand_off, (m + 1) * 8, hipMemcpyDeviceToHost, J.st));
+  HIPCHK(c, hipStreamSynchronize(J.st));
+  // global candidate index (in the sub-batch) of every hit
+  std::vector<uint64_t> g(n_hits);
+  for (uint64_t h = 0; h < n_hits; h++) {
+    const size_t k = (size_t)(std::lower_bound(uw.begin(), uw.end(), hits[h].word) - uw.begin());
+    if (hits[h].cand >= coff[k + 1] - coff[k])
+      return fail(c, A5X_E_ARG, "hit candidate index beyond its word's keyspace");
+    g[h] = coff[k] + hits[h].cand;
+  }
+  std::vector<uint64_t> ug(g);
+  std::sort(ug.begin(), ug.end());
+  ug.erase(std::unique(ug.begin(), ug.end()), ug.end());
+  // runs of hit candidates: a run spans at most 4096 candidates (its bytes are checked
+  // after the locate: a run over 1 MiB is split into single-candidate ranges)
+  struct Run { size_t a, b; };  // ug[a..b)
+  std::vector<Run> runs;
+  for (size_t i = 0; i < ug.size();) {
+    size_t j = i + 1;
+    while (j < ug.size() && ug[j] - ug[i] < 4096) j++;
+    runs.push_back({i, j});
+    i = j;
+  }
+  std::vector<uint64_t> q;
+  for (auto& r : runs) { q.push_back(ug[r.a]); q.push_back(ug[r.b - 1] + 1); }
+  std::vector<uint64_t> loc;
+  if ((rc = job_locate(c, J, q, loc))) return rc;
+  std::vector<Range> ranges;  // one per run, or per candidate of an oversize run
+  std::vector<std::pair<size_t, size_t>> rcand;  // ug[first, last) covered by each range
+  std::vector<uint64_t> q2;
+  std::vector<size_t> split_runs;
+  for (size_t r = 0; r < runs.size(); r++) {
+    const uint64_t* lb = &loc[3 * (2 * r)];
+    const uint64_t* le = &loc[3 * (2 * r + 1)];
+    if (le[0] - lb[0] <= (1u << 20) || runs[r].b - runs[r].a == 1) {
+      ranges.push_back(range_of(J, ug[runs[r].a], ug[runs[r].b - 1] + 1, lb, le));
+      rcand.push_back({runs[r].a, runs[r].b});
+    } else {
+      split_runs.push_back(r);
+      for (size_t i = runs[r].a; i < runs[r].b; i++) { q2.push_back(ug[i]); q2.push_back(ug[i] + 1); }
+    }
+  }
+  if (!q2.empty()) {
+    std::vector<uint64_t> loc2;
+    if ((rc = job_locate(c, J, q2, loc2))) return rc;
+    size_t t = 0;
+    for (size_t r : split_runs)
+      for (size_t i = runs[r].a; i < runs[r].b; i++, t++) {
+        ranges.push_back(range_of(J, ug[i], ug[i] + 1, &loc2[3 * (2 * t)], &loc2[3 * (2 * t + 1)]));
+        rcand.push_back({i, i + 1});
+      }
+  }
+  // expand every range into the staging buffer and cut out the hit candidates
+  std::vector<std::string> plain(ug.size());
+  std::vector<uint8_t> hb;
+  for (size_t r = 0; r < ranges.size(); r++) {
+    const Range& R = ranges[r];
+    const uint64_t nb = R.b1 - R.b0;
+    if ((rc = grow(c, c->s_out[0], nb + 64))) return rc;
+    if ((rc = job_launch(c, J, R, c->s_out[0].p, nb + 64))) return rc;
+    hb.resize(nb);
+    HIPCHK(c, hipMemcpyAsync(hb.data(), c->s_out[0].p, nb, hipMemcpyDeviceToHost, J.st));
+    if ((rc = job_check(c, J))) return rc;
+    // the range's lines are candidates R.cb, R.cb + 1, ... in order
+    size_t want = rcand[r].first;
+    uint64_t cand = R.cb, p0 = 0;
+    for (uint64_t x = 0; x < nb && want < rcand[r].second; x++) {
+      if (hb[x] != '\n') continue;
+      if (cand == ug[want]) plain[want++].assign((const char*)hb.data() + p0, (size_t)(x - p0));
+      cand++;
+      p0 = x + 1;
+    }
+    if (want != rcand[r].second) return fail(c, A5X_E_HIP, "hit candidates not found in their located range");
+  }
   static const char* hx = "0123456789abcdef";
   std::string o;
   for (uint64_t h = 0; h < n_hits; h++) {
-    const size_t k = (size_t)(std::lower_bound(uw.begin(), uw.end(), hits[h].word) - uw.begin());
-    if (hits[h].cand >= cnt[k]) return fail(c, A5X_E_ARG, "hit candidate index beyond its word's keyspace");
-    auto& st = starts[k];
-    if (st.empty()) {
-      st.push_back(0);
-      for (uint64_t i = base[k]; i < base[k + 1]; i++)
-        if (cand[i] == '\n') st.push_back((uint32_t)(i + 1 - base[k]));
-    }
-    const uint64_t a = base[k] + st[hits[h].cand], e = base[k] + st[hits[h].cand + 1] - 1;
+    const size_t k = (size_t)(std::lower_bound(ug.begin(), ug.end(), g[h]) - ug.begin());
     for (int i = 0; i < 16; i++) {
       o += hx[hits[h].digest[i] >> 4];
       o += hx[hits[h].digest[i] & 15];
     }
     o += ':';
-    append_plain(o, (const uint8_t*)cand.data() + a, e - a);
+    append_plain(o, (const uint8_t*)plain[k].data(), plain[k].size());
     o += '\n';
     if (o.size() >= (1u << 20) || h + 1 == n_hits) {
       if (sink(user, (const uint8_t*)o.data(), o.size())) return fail(c, A5X_E_SINK, "sink returned non-zero");

@@ -266,10 +266,11 @@ __device__ __forceinline__ u32 ks_classify(const W& wd, u64 L64, const Tab& T, c
 }
 
 template <class W>
-__device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const KsArgs& a, u32 f, u64* rec, u64* g) {
+__device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const KsArgs& a, u32 f, u64 count, u64* rec,
+                                         u64* g) {
   DevRecSink sk;
   sk.g = g; sk.c = g + 256 * FW_UMAXR; sk.rec = rec; sk.np = ff_np(f);
-  const Plan P = plan_word<true>(wd, L, T, sk);
+  const Plan P = plan_word<true>(wd, L, T, sk, fb_balanced_cap(count + 1));
   rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
   if (!P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
 }
@@ -422,7 +423,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       u64* rec = a.rec + tile * FW_TILE_REC + ro;
       DevRecSink sk;
       sk.g = gbuf + tid; sk.c = sk.g; sk.rec = rec; sk.np = ff_np(f);  // no clusters here
-      Planner<true, LWord, DevRecSink, KS_GCAP> pb(lw, T, sk);
+      Planner<true, LWord, DevRecSink, KS_GCAP> pb(lw, T, sk, build ? fb_balanced_cap(C.count + 1) : 0u);
       CountAcc A2;
       bool c2 = false;
       // replay the logged units (no second byte walk); words with more units re-walk
@@ -440,6 +441,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       if (!(KS_ABL & 1)) psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2);
       if (build && !(KS_ABL & 1)) {
         pb.finish(L);
+        pb.pick_balanced();
         const Plan& P = pb.P;
         rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
         if (c2 || !P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
@@ -506,12 +508,12 @@ __global__ void __launch_bounds__(256) k_keyspace_cplx(KsArgs a) {
       LWord lw;
       lw.base = wst; lw.off = threadIdx.x * KC_SLOT;
       f = ks_classify(lw, L64, T, a, C);
-      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(lw, (u32)L64, T, a, f, rec, gbuf + threadIdx.x);
+      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(lw, (u32)L64, T, a, f, C.count, rec, gbuf + threadIdx.x);
     } else {
       GWord gw;
       gw.p = a.words + s;
       f = ks_classify(gw, L64, T, a, C);
-      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(gw, (u32)L64, T, a, f, rec, gbuf + threadIdx.x);
+      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(gw, (u32)L64, T, a, f, C.count, rec, gbuf + threadIdx.x);
     }
     if ((f & A5X_WF_FAST) && C.count > 0) {
       if (fits) a.roff[w] = (u32)(a.cplx_base + (u64)i * FW_RMAX);
@@ -1345,12 +1347,6 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #ifndef FX_PFM
 #define FX_PFM 1      // next window's metadata loaded before the current window's rounds
 #endif
-#ifndef FX_SPEC
-#define FX_SPEC 0     // speculative next-window records with the metadata loads (spills VGPRs: off)
-#endif
-#ifndef FX_SPEC_N
-#define FX_SPEC_N 2   // ... KiB of them (uint4 per lane)
-#endif
 #ifndef FX_ABL
 #define FX_ABL 0      // timing ablations (variant builds only; output is garbage when set):
                       // 4 no global stores, 8 no rounds, 16 no big entries, 32 no prefix,
@@ -1648,20 +1644,37 @@ __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FL& fl,
 // Big entry (a5x_plan.h fb_entry, same bytes): combination c of the span <= FB_SPAN small
 // pieces whose descriptors are rec[d0 ..], entries rec[wbe ..]; the loop runs smax
 // (wave-uniform) iterations instead of FB_SPAN.
+//
+// Three LDS trips per entry, not two per small piece: every descriptor read is issued
+// at once, the digits are a VALU chain, then every small entry read is issued at once
+// (the descriptors do not depend on the digits; read in turn, each piece waited for
+// its descriptor and then its entry, s_waitcnt lgkmcnt(0) each: 2 smax serial trips).
 __device__ __forceinline__ uint4 fx_entry(const u64* rec, u32 d0, u32 wbe, u32 span, u32 smax, u32 c) {
   u64 lo64 = 0, hi64 = 0;
   u32 off = 0;
+  u64 G[FB_SPAN], EV[FB_SPAN];
+#pragma unroll
+  for (u32 i = 0; i < FB_SPAN; i++)
+    if (i < smax) G[i] = rec[i < span ? d0 + i : (u32)FX_RZ];
+  u32 ei[FB_SPAN];
+#pragma unroll
+  for (u32 i = 0; i < FB_SPAN; i++) {
+    if (i < smax) {
+      const u32 ghi = (u32)(G[i] >> 32);
+      u32 q = __umulhi(c, (u32)G[i]);
+      q += c & (u32)((int)ghi >> 31);  // R = 1: q = c
+      const u32 d = c - q * (((ghi >> 8) & 31u) + 1u);
+      c = q;
+      ei[i] = i < span ? wbe + (ghi & 255u) + d : (u32)FX_RZ;
+    }
+  }
+#pragma unroll
+  for (u32 i = 0; i < FB_SPAN; i++)
+    if (i < smax) EV[i] = rec[ei[i]];
 #pragma unroll
   for (u32 i = 0; i < FB_SPAN; i++) {
     if (i >= smax) break;
-    const bool valid = i < span;
-    const u64 G = rec[valid ? d0 + i : (u32)FX_RZ];
-    const u32 ghi = (u32)(G >> 32);
-    u32 q = __umulhi(c, (u32)G);
-    q += c & (u32)((int)ghi >> 31);  // R = 1: q = c
-    const u32 d = c - q * (((ghi >> 8) & 31u) + 1u);
-    c = q;
-    const u64 ev = rec[valid ? wbe + (ghi & 255u) + d : (u32)FX_RZ];
+    const u64 ev = EV[i];
     const u64 cv = ev & FW_M56;
     const u32 sh = 8u * off;
     const u64 x = cv << (sh & 63u), y = cv >> ((64u - sh) & 63u);
@@ -1670,84 +1683,6 @@ __device__ __forceinline__ uint4 fx_entry(const u64* rec, u32 d0, u32 wbe, u32 s
     off += fw_len(ev);
   }
   return make_uint4((u32)lo64, (u32)(lo64 >> 32), (u32)hi64, ((u32)(hi64 >> 32) & 0xFFFFFFu) | (off << 24));
-}
-
-#ifndef FX_DIRECT
-#define FX_DIRECT 0   // single-big-piece word runs built and placed without an entry table (A/B: neutral)
-#endif
-
-// Direct window (see expand_chunk_fast): words [0, k) of the window, each with at most
-// one big piece; rs = the word's record size (0: no candidates), rb = its record base
-// in rec (ring bytes 16.., moved here to the entry table's space first), ranks inside
-// [g, g1).  Passes of 64 candidates (one per lane): fx_entry -> DPP scan -> OR
-// placement; the ring is flushed when less than 1 KiB is left (FxDigest: every pass).
-template <class FL>
-__device__ __forceinline__ void fx_direct_window(FXWin& F, u32* ring, const u64* rec, const ExpArgs& a, FxRun& R,
-                                                 FL& fl, u32 rs, u32 rb, u32 k, u32 ntot, u64 g, u64 g1, u64 c0, u64 c1,
-                                                 u64 bo, u64 w) {
-  const u32 lane = lane_id();
-  u64* const rc = (u64*)F.be;  // the records, moved out of the ring
-  for (u32 i = lane; i < (ntot + 1) / 2; i += 64) ((uint4*)rc)[i] = ((const uint4*)rec)[i];
-  if (lane == 0) rc[FX_RZ] = 0;
-  const u64 wc0 = uniform64(c0);
-  if (!FL::DIGEST) {  // run position of g
-    const u64 r0 = g - wc0;
-    u64 pos = uniform64(bo) - a.out_base;
-    if (r0) pos += fast_prefix_bytes(rec + readlane_u32(rb, 0), r0);
-    if (!R.open || R.pos != pos) {
-      fx_close(R, ring, a);
-      R.B = pos & ~15ull; R.lo = pos; R.pos = pos; R.carry = 0; R.open = true;
-    }
-  }
-  WAVE_SYNC();
-  for (u32 i = 1 + lane; i <= (ntot + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);  // OR ring
-  const u32 rbw = lane == 0 ? (u32)(g - wc0) : 0u;
-  const u32 ncw = rs ? (u32)(min(c1, g1) - c0) - rbw : 0u;  // the word's candidates in [g, g1)
-  const u32 incN = wave_incl_scan_u32(lane < k ? ncw : 0u);
-  const u32 tot = readlane_u32(incN, k - 1);
-  const u32 est = lane < k ? incN - ncw : 0xffffffffu;
-  const u32 ringa = fx6_addr(ring), cap = FX_RING - 32u;
-  WAVE_SYNC();
-  u32 jb = 0;
-  for (u32 t0 = 0; t0 < tot; t0 += 64) {
-    if (!FL::DIGEST && (u32)(R.pos - R.B) + 64u * 16u > cap) fl(R);  // room for a pass
-    const u32 t = t0 + lane;
-    u32 j = jb;
-    for (;;) {
-      const u32 jn = uniform(jb + 1);
-      if (jn >= k) break;
-      const u32 sj = uniform(readlane_u32(est, jn));
-      if (sj >= t0 + 64) break;
-      jb = jn;
-      j += (t >= sj) ? 1u : 0u;
-    }
-    const u32 wrb = (u32)__shfl((int)rb, (int)j);
-    const u32 rank = t - (u32)__shfl((int)est, (int)j) + (u32)__shfl((int)rbw, (int)j);
-    const bool on = t < tot;
-    const u64 h = rc[on ? wrb : (u32)FX_RZ];
-    const u32 np = frh_np(h);
-    const u32 span = on ? np : 0u;  // the one big piece spans every small piece
-    const uint4 e = fx_entry(rc, wrb + 1u, wrb + 1u + np, span, wave_max_u32(span), rank + 1u);
-    const u32 len = on ? e.w >> 24 : 0u;
-    const u32 incl = wave_incl_scan_u32(len);
-    const u32 used = (u32)(R.pos - R.B);
-    u32 P = ringa + used + incl - len, sink = 0;
-    if (on) fx7_put(e, P, sink);
-    R.pos = uniform64(R.pos + readlane_u32(incl, 63));
-    WAVE_SYNC();
-    if constexpr (FL::DIGEST) {
-      FxLaneRun lr;
-      lr.off = used + incl - len;
-      lr.nc = on ? 1u : 0u;
-      lr.j = j;
-      lr.st = rank;
-      lr.clen[0] = len; lr.clen[1] = 0; lr.clen[2] = 0; lr.clen[3] = 0;
-      fl.digest(lr);
-      fl(R);
-    }
-  }
-  if (!FL::DIGEST) fl(R);  // the next window stages its records in ring bytes 16..
-  (void)w;
 }
 
 // DIG: 0 = write the stream, 1 = fused MD5, 2 = fused NTLM
@@ -1774,14 +1709,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
   typename std::conditional<DIG != 0, FxDigest<DIG == 1>, FxFlush>::type fl;
   fl.ring = ring; fl.a = &a; fl.wbase = 0;
   FxMeta M = fx_meta(a, w);
-#if FX_SPEC
-  // speculative records of the next window, loaded together with its metadata (records
-  // of consecutive windows are contiguous inside a keyspace tile): one global round trip
-  // per window setup instead of metadata -> records.  Live only between windows.
-  u64 spb = ~0ull;  // sp holds record u64 [spb, spb + 128 nsp) (spb even)
-  u32 nsp = 2;      // 1 KiB per step, sized from the last window's records
-  uint4 sp[FX_SPEC_N];
-#endif
   STAMP_DECL
   while (g < g1) {
     if (w >= a.nw) { guard_trip(a, 4, chunk, w, g, g1); break; }
@@ -1796,7 +1723,7 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     const u64 rm = __ballot(rs > 0);
     const u32 rbase = readlane_u32(M.roff, rm ? (u32)__builtin_ctzll(rm) : 0u);
     const bool contig = rs == 0 || M.roff == rbase + (incR - rs);
-    const bool ok = fast && incR < FX_RZ && contig;
+    const bool ok = fast && incR + 1u < FX_RZ && contig;  // (+1: the copy's alignment shift)
     const u64 badm = __ballot(!ok);
     u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
     STAMP(0);
@@ -1821,30 +1748,26 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     const u32 jf = (u32)__builtin_ctzll(fm);
     const u64 src0 = (u64)readlane_u32(M.roff, jf);
     const u32 ntot = readlane_u32(incR, k - 1);
-#if FX_SPEC
-    if (spb <= src0 && src0 + ntot <= spb + 128ull * nsp) {
-      const u32 d = (u32)(src0 - spb);  // speculated u64 i lands at rec[i - d]
-#pragma unroll
-      for (u32 q = 0; q < FX_SPEC_N; q++) {
-        if (q < nsp) {
-          const u32 i0 = 2 * (lane + 64 * q);
-          // (only the window's ntot: the OR rounds need the rest of the ring zero)
-          if (i0 >= d && i0 - d < ntot) rec[i0 - d] = ((u64)sp[q].y << 32) | sp[q].x;
-          if (i0 + 1 >= d && i0 + 1 - d < ntot) rec[i0 + 1 - d] = ((u64)sp[q].w << 32) | sp[q].z;
-        }
-      }
-    } else
-#endif
+    // Every load of the copy issued before the first LDS store: one global round trip
+    // (a load-store loop waited vmcnt(0) per KiB -- a trip each, and each behind the
+    // wave's outstanding output stores, which share the counter).  16-B loads from the
+    // aligned-down source: record u64 src0 lands at rec[sh].
+    const u32 sh = (u32)(src0 & 1u);
     {
-      const u64* s64 = a.rec + src0;
-      if ((src0 & 1) == 0) {
-        const uint4* src = (const uint4*)s64;
-        for (u32 i = lane; i < (ntot + 1) / 2; i += 64) ((uint4*)rec)[i] = src[i];
-      } else {
-        for (u32 i = lane; i < ntot; i += 64) rec[i] = s64[i];
-      }
+      static_assert((FX_RZ + 1) / 2 <= 4 * 64, "window records: at most 4 uint4 per lane");
+      const uint4* src = (const uint4*)(a.rec + (src0 - sh));
+      const u32 nq = (ntot + sh + 1u) / 2u;
+      // (clamped, unconditional loads: the excess lanes re-read the last quad)
+      const u32 nq1 = nq - 1u;
+      const uint4 v0 = src[min(lane, nq1)], v1 = src[min(lane + 64u, nq1)];
+      const uint4 v2 = src[min(lane + 128u, nq1)], v3 = src[min(lane + 192u, nq1)];
+      uint4* r4 = (uint4*)rec;
+      if (lane < nq) r4[lane] = v0;
+      if (lane + 64u < nq) r4[lane + 64u] = v1;
+      if (lane + 128u < nq) r4[lane + 128u] = v2;
+      if (lane + 192u < nq) r4[lane + 192u] = v3;
     }
-    const u32 rb = incR - rs;
+    const u32 rb = incR - rs + sh;
     const u64 bo = M.bo;
     if (lane == 0) rec[FX_RZ] = 0;
     WAVE_SYNC();
@@ -1860,22 +1783,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
       R2 = frh_R(hdr, 2);
       R3 = frh_R(hdr, 3);
     }
-#if FX_DIRECT
-    // ---- a run of single-big-piece words: every candidate IS one big entry, so it is
-    // built (fx_entry) and placed straight away -- no entry table, and the window is
-    // limited by its records, not by 255 entries ----
-    if (!(__ballot(lane < k && rs > 0 && nbw >= 2) & 1ull)) {
-      const u64 m2w = __ballot(lane < k && rs > 0 && nbw >= 2);
-      if (m2w) k = (u32)__builtin_ctzll(m2w);
-      fl.wbase = w;
-      fx_direct_window(F, ring, rec, a, R, fl, lane < k ? rs : 0u, rb, k, ntot, g, g1, c0, c1, M.bo, w);
-      g = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
-      w += k;
-      M = fx_meta(a, w);
-      WAVE_SYNC();
-      continue;
-    }
-#endif
     const u32 E = R0 + R1 + R2 + R3 - (FB_NMAX - nbw);  // fb_R = 1 past the last big piece
     const u32 incE = wave_incl_scan_u32(E);
     const u64 over = __ballot(lane < k && incE > FX_ZBE);
@@ -1973,7 +1880,7 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     fl.wbase = w;
 #ifdef FX_OR
     // the records' ring bytes [16, 16 + 8 ntot) back to zero for the OR rounds
-    for (u32 i = 1 + lane; i <= (ntot + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+    for (u32 i = 1 + lane; i <= (ntot + sh + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
     WAVE_SYNC();
 #endif
     STAMP(2);
@@ -1982,20 +1889,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     // metadata registers are dead from here on)
     const u64 gnext = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     M = fx_meta(a, w + k);
-#if FX_SPEC
-    {
-      // the next window's records, loaded under this window's rounds too: right after
-      // this window's, or the start of the next tile's region
-      const u64 wn = w + k;
-      const u64 nx = (wn % FW_TILE == 0) ? (wn / FW_TILE) * (u64)FW_TILE_REC : src0 + ntot;
-      nsp = min((u32)FX_SPEC_N, (ntot + 2u * 128u - 1u) / 128u);  // this window's size + 1 KiB
-      spb = nx & ~1ull;
-      const uint4* src = (const uint4*)(a.rec + spb);
-#pragma unroll
-      for (u32 q = 0; q < FX_SPEC_N; q++)
-        if (q < nsp) sp[q] = spb + 2ull * (lane + 64 * q) + 2 <= a.rec_n ? src[lane + 64 * q] : make_uint4(0, 0, 0, 0);
-    }
-#endif
 #endif
     // ---- rounds ----
     if (!(FX_ABL & 8))
@@ -2068,8 +1961,9 @@ __device__ __forceinline__ u32 lds_per_wave_slow() { return (A5X_RING_A + (u32)s
 
 __global__ void __launch_bounds__(256) k_expand_slow(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  load_table(smem, a.table, a.table_bytes);
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
+  if (blockIdx.x * nwv >= *a.nsegs) return;  // idle workgroup (uniform): release its LDS at once
+  load_table(smem, a.table, a.table_bytes);
   const u32 tb = (a.table_bytes + 15u) & ~15u;
   uint8_t* mine = smem + tb + wv * lds_per_wave_slow();
   u32* ring = (u32*)mine;
@@ -2084,6 +1978,7 @@ __global__ void __launch_bounds__(256) k_expand_slow(ExpArgs a) {
 
 __global__ void __launch_bounds__(64) k_expand_b(ExpArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  if (blockIdx.x >= *a.nsegs) return;  // idle workgroup: release its 160 KB of LDS at once
   load_table(smem, a.table, a.table_bytes);
   const u32 tb = (a.table_bytes + 15u) & ~15u;
   u32* ring = (u32*)(smem + tb);
@@ -2320,7 +2215,10 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   else if (kind == 5)
     hipLaunchKernelGGL(k_expand_fast_ntlm, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st,
                        a);
-  else if (kind == 1)
+  else if (kind == 1)  // (the bound counts the range's candidates, not the slow words' segments:
+                       // workgroups past *nsegs exit before they stage anything.  A grid capped at
+                       // 2 workgroups per CU measured 2-3 % slower on C3: its grid-stride waves
+                       // held their LDS beside k_expand_fast for the whole slow-word work)
     hipLaunchKernelGGL(k_expand_slow, dim3(blocks_for(L.nsegs_bound, waves, 65536)), dim3(64 * waves),
                        a5x_expand_lds(L.table_bytes, 1, waves), st, a);
   else if (kind == 2)

@@ -47,7 +47,7 @@ struct A5xExpLaunch {
   const uint32_t* chunk_w0;
   const uint64_t* segs;    // k_expand_slow / k_expand_b items (a5x_launch_segments)
   const uint32_t* nsegs;   // device count of segs
-  uint64_t nsegs_bound;    // host bound on *nsegs (grid size)
+  uint64_t nsegs_bound;    // host bound on *nsegs
   uint64_t cand_begin, cand_end;
   uint64_t CH;
   uint64_t SEG;  // candidates per slow / BIG segment
@@ -131,12 +131,22 @@ struct A5xModeLaunch {
   uint32_t* glob_n;
   uint8_t* gscr;
   uint32_t gslots;
+  // fused digest (op 2): every candidate hashed where it is built and probed against the
+  // target set; hits as (word, candidate in word) -- see A5xDigLaunch
+  int dg_algo;
+  const uint32_t* dg_bitmap;
+  uint32_t dg_bm_mask, dg_has_zero, dg_hit_cap;
+  const uint4* dg_table;
+  uint64_t dg_tmask;
+  struct A5xHitRaw* dg_hits;
+  uint32_t* dg_nhits;
 };
 size_t a5x_mode_lds(uint32_t mtab_bytes);
 uint64_t a5x_mode_gslot_bytes();
 hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st);
 hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st);
-// op 0: per-item output bytes (seg_bytes); op 1: expand items [item_begin, item_end)
+// op 0: per-item output bytes (seg_bytes); op 1: expand items [item_begin, item_end);
+// op 2: fused digest of items [item_begin, item_end) (no length pass needed before it)
 hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st);
 // out[3q..3q+2] = {item, index in item, byte offset} of global candidate cands[q]
 hipError_t a5x_launch_mode_locate(const A5xModeLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out,

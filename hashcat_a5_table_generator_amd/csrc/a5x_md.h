@@ -128,15 +128,22 @@ __device__ __forceinline__ void md_lds(const uint8_t* base, uint32_t off, uint32
   }
 }
 
-// Next UTF-16 unit of Go's utf16.Encode([]rune(s)) over message bytes [0, len) at
-// base + off (LDS, readable 4 bytes past the message): i = byte position, pend = the
-// pending low surrogate (0: none).  Invalid UTF-8 -> U+FFFD consuming one byte, as
-// utf8.DecodeRune.  Returns false at the end of the message.
-__device__ __forceinline__ bool utf16_next(const uint8_t* base, uint32_t off, uint32_t len, uint32_t& i,
-                                           uint32_t& pend, uint32_t& u) {
+// Message byte sources for the UTF-16 walk: 4 bytes at message offset i (readable
+// past the message end).
+struct MdLds {  // LDS buffer, readable 4 bytes past the message
+  const uint8_t* base;
+  uint32_t off;
+  __device__ __forceinline__ uint32_t at4(uint32_t i) const { return lds4(base, off + i); }
+};
+
+// Next UTF-16 unit of Go's utf16.Encode([]rune(s)) over message bytes [0, len) of src:
+// i = byte position, pend = the pending low surrogate (0: none).  Invalid UTF-8 ->
+// U+FFFD consuming one byte, as utf8.DecodeRune.  Returns false at the end of the message.
+template <class S>
+__device__ __forceinline__ bool utf16_next(const S& src, uint32_t len, uint32_t& i, uint32_t& pend, uint32_t& u) {
   if (pend) { u = pend; pend = 0; return true; }
   if (i >= len) return false;
-  const uint32_t x = lds4(base, off + i);
+  const uint32_t x = src.at4(i);
   const uint32_t b0 = x & 255u, b1 = (x >> 8) & 255u, b2 = (x >> 16) & 255u, b3 = x >> 24;
   uint32_t r = b0, sz = 1;
   if (b0 >= 0x80u) {
@@ -167,8 +174,10 @@ __device__ __forceinline__ bool utf16_next(const uint8_t* base, uint32_t off, ui
 
 // NTLM = MD4 over the UTF-16LE of the candidate's runes (Go []rune + utf16.Encode), the
 // units produced while each 64-byte message block is filled (no UTF-16 buffer, any
-// length).  Wave-collective loop: lanes whose digest is done keep their state.
-__device__ __forceinline__ void ntlm_lds(const uint8_t* base, uint32_t off, uint32_t len, uint32_t* d) {
+// length).  Wave-collective loop over the active lanes: lanes whose digest is done keep
+// their state.
+template <class S>
+__device__ __forceinline__ void ntlm_stream(const S& src, uint32_t len, uint32_t* d) {
   uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
   uint32_t i = 0, pend = 0, nu = 0;
   bool padded = false, fin = false;
@@ -182,7 +191,7 @@ __device__ __forceinline__ void ntlm_lds(const uint8_t* base, uint32_t off, uint
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         uint32_t u = 0;
-        if (utf16_next(base, off, len, i, pend, u)) {
+        if (utf16_next(src, len, i, pend, u)) {
           w |= u << (16 * h);
           nu++;
         } else if (!padded) {
@@ -206,4 +215,12 @@ __device__ __forceinline__ void ntlm_lds(const uint8_t* base, uint32_t off, uint
     fin = fin || last;
   }
   d[0] = st[0]; d[1] = st[1]; d[2] = st[2]; d[3] = st[3];
+}
+
+// the fused kernel's form: the candidate in the LDS ring
+__device__ __forceinline__ void ntlm_lds(const uint8_t* base, uint32_t off, uint32_t len, uint32_t* d) {
+  MdLds src;
+  src.base = base;
+  src.off = off;
+  ntlm_stream(src, len, d);
 }

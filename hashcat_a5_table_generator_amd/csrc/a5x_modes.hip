@@ -33,12 +33,19 @@
 // one candidate per round in its own LDS buffer (stride 132 B: the 64 lanes' byte
 // columns fall in distinct banks), a wave scan of the lengths places them, and the
 // lane stores its bytes.  These engines are not the headline path.
+//
+// Fused digest (op 2, SURVEY 8(a) a8 for -r / -s / -s -r; README.MD:159,163 pipes
+// `-s -r` into hashcat): every candidate is hashed (MD5, or NTLM over Go's UTF-16LE)
+// where it is built -- the positional engine's LDS ring, the byte builder's lane
+// buffer -- and probed against the target set; nothing but hits leaves the CU, and no
+// length pass or output layout is needed.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "a5x.h"
 #include "a5x_format.h"
 #include "a5x_launch.h"
+#include "a5x_md.h"
 #include "a5x_ring.h"
 
 namespace {
@@ -863,6 +870,67 @@ __device__ void m_pos_expand(SL& S, const MT& T, const MInfo& I, const A5xModeLa
   M_WAVE_SYNC();
 }
 
+// Hash candidate t of word w (len bytes at base + off: LDS, or a pass-G slot in HBM,
+// readable 8 bytes past the end) and record a hit.  Wave-collective (NTLM's block loop):
+// every lane calls it, on = whether the lane holds a candidate.
+__device__ __forceinline__ void m_digest_probe(const A5xModeLaunch& a, const uint8_t* base, u32 off, u32 len, bool on,
+                                               u64 w, u64 t) {
+  u32 d[4];
+  if (a.dg_algo == A5X_ALGO_MD5) md_lds<true>(base, off, on ? len : 0u, d);
+  else ntlm_lds(base, off, on ? len : 0u, d);
+  if (on && md_probe(a.dg_bitmap, a.dg_bm_mask, a.dg_table, a.dg_tmask, a.dg_has_zero != 0, d)) {
+    const u32 h = atomicAdd(a.dg_nhits, 1u);
+    if (h < a.dg_hit_cap) {
+      A5xHitRaw r;
+      r.blk = w;
+      r.idx = t;
+      r.d[0] = d[0]; r.d[1] = d[1]; r.d[2] = d[2]; r.d[3] = d[3];
+      a.dg_hits[h] = r;
+    }
+  }
+}
+
+// Fused digest of leaves [tb, te) of the positional word w set up in S: 64 leaves per
+// round placed into the zeroed ring exactly as m_pos_expand places them (without the
+// newline), hashed there by their lanes, then the round's bytes are zeroed again.
+template <class SL>
+__device__ void m_pos_digest(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 w, u64 tb, u64 te,
+                             u32 ntok, u32& err) {
+  const u32 lane = m_lane();
+  uint4* r4 = (uint4*)&S.buf[0];
+  constexpr u32 RB = sizeof(S.buf) / 16;
+  static_assert(SL::RING && sizeof(S.buf) >= 16 + 64 * A5X_M_CBUF + 32, "ring: one round of 64 candidates");
+  const u32 ringa = fx6_addr(r4);
+  for (u32 i = lane; i < RB; i += 64) r4[i] = make_uint4(0, 0, 0, 0);
+  M_WAVE_SYNC();
+  const bool rev = a.mode == A5X_MODE_REVERSE;
+  for (u64 t0 = tb; t0 < te; t0 += 64) {
+    const u64 t = t0 + lane;
+    u64 sel = 0;
+    u32 len = 0;
+    if (t < te) {
+      len = m_pos_sel(S, T, I, a.mode, t, sel);
+      if (len + 1 > A5X_M_CBUF) { err |= M_ERR_CLEN; len = 0; }
+    }
+    const u32 incl = m_incl_scan(len);
+    const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    const u32 o = incl - len;
+    u32 P = ringa + o, sink = 0;
+    if (t < te && len) {
+      for (u32 k = 0; k < ntok; k++) {
+        const u32 d = S.tok[k], pi = d >> 16;
+        const u32 ix = (d & 0xFFFFu) + (pi ? (rev ? (u32)(sel >> (pi - 1)) & 1u : (u32)(sel >> (4 * (pi - 1))) & 15u) : 0u);
+        fx7_put(S.ent[ix], P, sink);
+      }
+    }
+    M_WAVE_SYNC();
+    m_digest_probe(a, (const uint8_t*)r4, o, len, t < te, w, t);
+    M_WAVE_SYNC();
+    for (u32 b = lane; b < (tot + 31u) / 16u && b < RB; b += 64) r4[b] = make_uint4(0, 0, 0, 0);
+    M_WAVE_SYNC();
+  }
+}
+
 __device__ __forceinline__ void m_err(u32* e, u32 bits) {
   if (bits && m_lane() == 0) atomicOr(e, bits);
 }
@@ -945,6 +1013,11 @@ __device__ u64 m_run(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a,
         else err |= M_ERR_STATE;  // (item routed to the wrong layout)
       }
     }
+    if (op == 2) {  // fused digest: the candidate where the builder left it (len - 1 bytes)
+      const uint8_t* base = p ? p : S.word;
+      m_digest_probe(a, base, 0, len ? len - 1 : 0u, v && len > 0, g0, t0 + k);
+      continue;
+    }
     const u32 incl = m_incl_scan(len);
     const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
     if (op == 1 && v) {
@@ -986,6 +1059,14 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
   u32 err = 0, ntok = 0;
   if constexpr (!SL::G && !SL::BUILDER) {
     ntok = a.mode != A5X_MODE_DEFAULT ? m_pos_setup(S, T, I, a.mode) : 0u;
+    if (op == 2) {  // fused digest: positional items here, the others to the byte builder
+      if constexpr (SL::RING) {
+        if (ntok) m_pos_digest(S, T, I, a, w, t0, t0 + nc, ntok, err);
+        if (m_lane() == 0) a.item_fl[i] = ntok ? MI_POS : MI_BUILD;
+      }
+      m_err(a.err, m_wave_or(err));
+      return;
+    }
     if (op == 1) {
       if constexpr (SL::RING) {
         // the leaves of this item inside [cand_begin, cand_end); the first one's bytes start
@@ -1011,7 +1092,8 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
   if constexpr (!SL::G && SL::BUILDER)
     if (op == 0 && m_lane() == 0) a.item_fl[i] = MI_BUILD;
   const u64 base = op == 1 ? a.seg_boff[i] : 0;
-  const u64 run = m_run(S, T, I, a, t0, nc, op, cw0, base, err, ntok);
+  // (op 2: m_run's g0 carries the word index for the hit records)
+  const u64 run = m_run(S, T, I, a, t0, nc, op, op == 2 ? w : cw0, base, err, ntok);
   if (op == 0 && m_lane() == 0) a.seg_bytes[i] = run;
   m_err(a.err, m_wave_or(err));
 }
@@ -1037,6 +1119,8 @@ __global__ void __launch_bounds__(64) k_mode_items_len(A5xModeLaunch a) { m_item
 __global__ void __launch_bounds__(64) k_mode_items_len_b(A5xModeLaunch a) { m_items<MLds>(a, 0, MI_BUILD_LEN); }
 __global__ void __launch_bounds__(64) k_mode_items_pos(A5xModeLaunch a) { m_items<MLdsR>(a, 1, MI_POS); }
 __global__ void __launch_bounds__(64) k_mode_items_b(A5xModeLaunch a) { m_items<MLds>(a, 1, MI_BUILD); }
+__global__ void __launch_bounds__(64) k_mode_digest_pos(A5xModeLaunch a) { m_items<MLdsR>(a, 2, 0); }
+__global__ void __launch_bounds__(64) k_mode_digest_b(A5xModeLaunch a) { m_items<MLds>(a, 2, MI_BUILD); }
 
 // the items of the listed pass-G words inside [item_begin, item_end), dealt to the slots
 __global__ void __launch_bounds__(64) k_mode_items_g(A5xModeLaunch a, int op) {
@@ -1137,9 +1221,12 @@ hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st)
     hipLaunchKernelGGL(k_mode_items_len, g, dim3(64), m_lds<MLdsC>(L.mtab_bytes), st, L);
     if (L.mode != A5X_MODE_REVERSE)
       hipLaunchKernelGGL(k_mode_items_len_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
-  } else {
+  } else if (op == 1) {
     hipLaunchKernelGGL(k_mode_items_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_items_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
+  } else {
+    hipLaunchKernelGGL(k_mode_digest_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
+    hipLaunchKernelGGL(k_mode_digest_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   }
   if (L.gscr && L.gslots)
     hipLaunchKernelGGL(k_mode_items_g, dim3(L.gslots), dim3(64), (L.mtab_bytes + 15u) & ~15u, st, L, op);

@@ -383,25 +383,44 @@ struct Planner {
   bool open;                    // a group piece is being built
   u32 bR, bl, bspan;            // the big piece being filled
   u32 cR, cmax, cmin, cpi, prev;
+  // Balanced big pieces (BUILD walks): a second grouping of the same small pieces with
+  // R per big piece capped at acap (0: none).  The greedy grouping fills every big piece
+  // up to FB_RMAX combinations, e.g. R 4 4 4 3 -> 64 + 3 = 67 entries; capped near
+  // P^(1 / nbig) the same two pieces are 16 + 12 = 28 entries.  k_expand_fast's windows
+  // are bounded by their big entries, so fewer entries = more words and candidates per
+  // window setup.  pick_balanced() takes it when it has as many big pieces as the greedy.
+  u32 acap, aR, al, aspan;
+  Plan A;
 
-  A5X_HD Planner(const W& w, const Tab& t, S& s) : wd(w), T(t), sk(s) {
+  A5X_HD Planner(const W& w, const Tab& t, S& s, u32 balanced_cap = 0) : wd(w), T(t), sk(s) {
     P.np = 0; P.ng = 0; P.ne = 0; P.lconst = 0; P.maxl = 0; P.minl = 0; P.ok = true;
     P.nbig = 0; P.bstarts = 0; P.bent = 0; P.bRp = 0;
     open = false; bR = 1; bl = 0; bspan = 0; cR = 1; cmax = 0; cmin = 0; cpi = 0; prev = 0;
+    acap = balanced_cap; aR = 1; al = 0; aspan = 0;
+    A.nbig = 0; A.bstarts = 0; A.bent = 0; A.bRp = 0;
+  }
+  static A5X_HD void big_join(Plan& Q, u32& qR, u32& ql, u32& qspan, u32 cap, u32 R, u32 maxlen, u32 pi) {
+    if (Q.nbig && ql + maxlen <= FB_PLEN && qR * R <= cap && qspan < FB_SPAN) {
+      Q.bent += qR * R - qR;
+      qR *= R; ql += maxlen; qspan++;
+    } else {
+      if (Q.nbig >= 1 && Q.nbig <= 3) Q.bstarts |= (pi & 7u) << (3 * (Q.nbig - 1));
+      Q.nbig++;
+      Q.bent += R;
+      qR = R; ql = maxlen; qspan = 1;
+    }
+    if (Q.nbig <= FB_NMAX) {
+      const u32 sh = 6u * (Q.nbig - 1u);
+      Q.bRp = (Q.bRp & ~(63u << sh)) | (((qR - 1u) & 63u) << sh);
+    }
   }
   A5X_HD void big_add(u32 R, u32 maxlen, u32 pi) {  // small piece pi (in order) joins a big piece
-    if (P.nbig && bl + maxlen <= FB_PLEN && bR * R <= FB_RMAX && bspan < FB_SPAN) {
-      P.bent += bR * R - bR;
-      bR *= R; bl += maxlen; bspan++;
-    } else {
-      if (P.nbig >= 1 && P.nbig <= 3) P.bstarts |= (pi & 7u) << (3 * (P.nbig - 1));
-      P.nbig++;
-      P.bent += R;
-      bR = R; bl = maxlen; bspan = 1;
-    }
-    if (P.nbig <= FB_NMAX) {
-      const u32 sh = 6u * (P.nbig - 1u);
-      P.bRp = (P.bRp & ~(63u << sh)) | (((bR - 1u) & 63u) << sh);
+    big_join(P, bR, bl, bspan, FB_RMAX, R, maxlen, pi);
+    if (acap) big_join(A, aR, al, aspan, acap, R, maxlen, pi);
+  }
+  A5X_HD void pick_balanced() {
+    if (acap && A.nbig == P.nbig && A.bent < P.bent) {
+      P.bstarts = A.bstarts; P.bRp = A.bRp; P.bent = A.bent;
     }
   }
   A5X_HD void close_group() {
@@ -508,13 +527,35 @@ struct Planner {
 };
 
 template <bool BUILD, class W, class S>
-A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk) {
-  Planner<BUILD, W, S> pl(wd, T, sk);
+A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk, u32 balanced_cap = 0) {
+  Planner<BUILD, W, S> pl(wd, T, sk, balanced_cap);
   u32 p = 0;
   Unit U;
   while (pl.P.ok && next_unit(wd, L, p, T, U)) pl.unit(U);
   pl.finish(L);
+  pl.pick_balanced();
   return pl.P;
+}
+
+// The balanced grouping's cap for a FAST word of P = prod R = count + 1: the fewest big
+// pieces nb with FB_RMAX^nb >= P, then about P^(1 / nb) with slack for the
+// discreteness of the small pieces' R (slack8 in 1/8 units; 0: no balanced grouping).
+#ifndef FB_BAL_SLACK8
+#define FB_BAL_SLACK8 10
+#endif
+A5X_HD u32 fb_balanced_cap(u64 P, u32 slack8 = FB_BAL_SLACK8) {
+  if (!slack8 || P <= FB_RMAX) return 0;
+  u32 nb = 1;
+  for (u64 x = FB_RMAX; x < P && nb < FB_NMAX; nb++) x *= FB_RMAX;
+  u32 r = 2;
+  while (r < FB_RMAX) {
+    u64 x = 1;
+    for (u32 i = 0; i < nb && x < P; i++) x *= r;
+    if (x >= P) break;
+    r++;
+  }
+  const u32 c = (r * slack8 + 7u) / 8u;
+  return c < r ? r : (c > FB_RMAX ? FB_RMAX : c);
 }
 
 // The unit of a lone match of key k at position s (next_unit's single-match case).

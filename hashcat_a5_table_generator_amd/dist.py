@@ -135,3 +135,44 @@ def allreduce_min_u64(dist, values, backend: str = "nccl") -> np.ndarray:
     t = torch.from_numpy(v.astype(np.int64)).to(dev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return t.cpu().numpy().astype(np.uint64)
+
+
+def gather_rows_u64(dist, rows, backend: str = "nccl", dst: int = 0):
+    """Concatenation, in rank order, of every rank's (n_r, k) u64 rows, on rank ``dst``
+    (other ranks get None): one all-gather of the row counts, then one all-gather of
+    the rows padded to the largest count (exact: 32-bit halves).  The hit gather of
+    north_star (e): each rank's hit records (global word, candidate, digest) -> rank 0."""
+    import torch
+    r = np.asarray(rows, dtype=np.uint64)
+    k = r.shape[1] if r.ndim == 2 else 0
+    world = _world(dist)
+    if world == 1:
+        return r.reshape(-1, k)
+    counts = allgather_u64(dist, [r.shape[0]], backend)[:, 0].astype(np.int64)
+    m = int(counts.max())
+    pad = np.zeros((max(m, 1), k), dtype=np.uint64)
+    pad[: r.shape[0]] = r
+    dev = "cuda" if backend == "nccl" else "cpu"
+    t = torch.from_numpy(_to_halves(pad.reshape(-1))).to(dev)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    if dist.get_rank() != dst:
+        return None
+    parts = [_from_halves(o.cpu().numpy()).reshape(-1, k)[: int(c)] for o, c in zip(outs, counts)]
+    return np.concatenate(parts) if parts else np.zeros((0, k), dtype=np.uint64)
+
+
+def hits_to_rows(hits, word_base: int = 0) -> np.ndarray:
+    """[(word, cand, digest16)] -> (n, 4) u64 rows {word + word_base, cand, digest lo, digest hi}."""
+    out = np.zeros((len(hits), 4), dtype=np.uint64)
+    for i, (w, c, d) in enumerate(hits):
+        out[i, 0] = w + word_base
+        out[i, 1] = c
+        out[i, 2] = int.from_bytes(d[:8], "little")
+        out[i, 3] = int.from_bytes(d[8:], "little")
+    return out
+
+
+def rows_to_hits(rows):
+    """Inverse of hits_to_rows: [(word, cand, digest16)]."""
+    return [(int(r[0]), int(r[1]), int(r[2]).to_bytes(8, "little") + int(r[3]).to_bytes(8, "little")) for r in rows]

@@ -23,7 +23,7 @@ import ctypes
 import io
 import os
 import sys
-from typing import BinaryIO, Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import BinaryIO, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -375,25 +375,85 @@ def process_word_substitute_all_reverse(word: bytes, sub_map: SubMap, min_substi
     return _engine(word, sub_map, min_substitute, max_substitute, MODE_SUBALL_REVERSE)
 
 
+MAX_SCAN_TOKEN = 64 * 1024  # bufio.MaxScanTokenSize
+
+
+def iter_word_batches(f: BinaryIO, batch_words: int = 1 << 22,
+                      chunk: int = 64 << 20) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
+    """The dictionary stream of ``main.go:52-56,72-74`` in bounded memory: ScanLines over
+    ``chunk``-byte reads (LF split, one trailing CR dropped, a final unterminated line
+    kept, and the first line with no newline in 64 KiB silently ends the input: the
+    reference never checks ``scanner.Err()``).  Yields packed batches of at most
+    ``batch_words`` words (``split_words`` layout)."""
+    pend_w: List[np.ndarray] = []
+    pend_o: List[np.ndarray] = []
+    npend = 0
+
+    def flush_pending():
+        nonlocal pend_w, pend_o, npend
+        lens = np.concatenate([np.diff(o.astype(np.int64)) for o in pend_o])
+        body = np.concatenate([w[: int(o[-1])] for w, o in zip(pend_w, pend_o)])
+        offs = np.zeros(len(lens) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        data = np.zeros(len(body) + 16, dtype=np.uint8)
+        data[: len(body)] = body
+        pend_w, pend_o, npend = [], [], 0
+        return data, offs
+
+    def take(words, offs):
+        # split (words, offs) into the pending batch, yielding every full batch
+        nonlocal npend
+        n = len(offs) - 1
+        i = 0
+        while i < n:
+            k = min(n - i, batch_words - npend)
+            sub_o = (offs[i:i + k + 1] - offs[i]).astype(np.uint64)
+            pend_w.append(words[int(offs[i]):int(offs[i + k])])
+            pend_o.append(sub_o)
+            npend += k
+            i += k
+            if npend == batch_words:
+                yield flush_pending()
+
+    rest = b""
+    while True:
+        block = f.read(chunk)
+        eof = not block
+        buf = rest + block
+        if eof:
+            part, rest = buf, b""
+        else:
+            cut = buf.rfind(b"\n") + 1
+            part, rest = buf[:cut], buf[cut:]
+        if part:
+            words, offs = split_words(part)
+            yield from take(words, offs)
+            complete = part.count(b"\n") + (0 if part.endswith(b"\n") else 1)
+            if len(offs) - 1 < complete:  # ErrTooLong inside this part: the input ends here
+                break
+        if eof:
+            break
+        if len(rest) >= MAX_SCAN_TOKEN:  # no newline in 64 KiB: ErrTooLong
+            break
+    if npend:
+        yield flush_pending()
+
+
 def generate(dict_file: str, table_files: Sequence[str], table_min: int = 0, table_max: int = 15,
              substitute_all: bool = False, reverse_sub: bool = False, out: Optional[BinaryIO] = None,
-             device: int = 0, batch_words: int = 1 << 22) -> int:
-    """The whole ``main()`` (``main.go:28-100``): dict -> candidates on ``out``; returns candidates."""
+             device: int = 0, batch_words: int = 1 << 22, chunk: int = 64 << 20) -> int:
+    """The whole ``main()`` (``main.go:28-100``): dict -> candidates on ``out``; returns
+    candidates.  The dictionary is streamed (``iter_word_batches``): memory is bounded by
+    one chunk and one batch, whatever the file size."""
     out = out if out is not None else sys.stdout.buffer
     mode = mode_of(substitute_all, reverse_sub)
     with Context(device) as c:
         c.load_tables(table_files)
-        with open(dict_file, "rb") as f:
-            data = f.read()
-        words, offs = split_words(data)
-        n = len(offs) - 1
         total = 0
-        for b0 in range(0, n, batch_words):
-            b1 = min(n, b0 + batch_words)
-            sub_off = (offs[b0:b1 + 1] - offs[b0]).astype(np.uint64)
-            sub_words = np.ascontiguousarray(words[int(offs[b0]):int(offs[b1]) + 16])
-            _, st = c.expand(sub_words, sub_off, mode, table_min, table_max, sink=lambda d: out.write(d) and 0)
-            total += st["candidates"]
+        with open(dict_file, "rb") as f:
+            for sub_words, sub_off in iter_word_batches(f, batch_words, chunk):
+                _, st = c.expand(sub_words, sub_off, mode, table_min, table_max, sink=lambda d: out.write(d) and 0)
+                total += st["candidates"]
         out.flush()
         return total
 

@@ -146,3 +146,39 @@ def test_partition_properties():
             # split r starts at the first word whose start offset reaches r/parts of the total
             assert int(prefix[s[r]]) >= total * r // parts
             assert s[r] == 0 or int(prefix[s[r] - 1]) < -(-total * r // parts)
+
+
+GATHER_WORKER = r"""
+import os, sys, json
+sys.path.insert(0, {root!r})
+import numpy as np
+from hashcat_a5_table_generator_amd import dist as D
+dist, rank, world, _ = D.init_from_env("gloo")
+# rank r found r + 1 hits (rank 1 none at all, to cover an empty contribution) in its
+# shard [w0, w0 + 1000): local word indices, mapped to global ones by the shard base
+n = 0 if rank == 1 else rank + 2
+rng = np.random.default_rng(rank)
+hits = [(int(rng.integers(0, 1000)), int(rng.integers(0, 1 << 40)), rng.bytes(16)) for _ in range(n)]
+rows = D.hits_to_rows(hits, word_base=1000 * rank)
+got = D.gather_rows_u64(dist, rows, "gloo")
+ok = True
+if rank == 0:
+    want = []
+    for r in range(world):
+        m = 0 if r == 1 else r + 2
+        g = np.random.default_rng(r)
+        want += [(int(g.integers(0, 1000)) + 1000 * r, int(g.integers(0, 1 << 40)), g.bytes(16)) for _ in range(m)]
+    ok = D.rows_to_hits(got) == want
+else:
+    ok = got is None
+print(json.dumps(dict(rank=rank, ok=bool(ok))), flush=True)
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_hit_gather_global_word_indices(tmp_path, world):
+    """north_star (e) "gather hits": every rank's hit records, word indices rebased from
+    its shard to the global list, arrive on rank 0 in rank order (empty ranks included)."""
+    res = _run_ranks(tmp_path, GATHER_WORKER.format(root=ROOT), world)
+    assert all(r["ok"] for r in res), res

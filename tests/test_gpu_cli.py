@@ -66,7 +66,7 @@ def test_engine_generate_end_to_end(dict_file, mode):
     path, body = dict_file
     out = io.BytesIO()
     n = generate(path, [table_path("qwerty-azerty")], substitute_all=mode >= 2, reverse_sub=bool(mode & 1), out=out,
-                 batch_words=3000)  # several batches
+                 batch_words=3000, chunk=4099)  # several batches, read in many small chunks
     words, offs = _oracle_words(body)
     _per_word_check(out.getvalue(), words, offs, mode, ["qwerty-azerty"])
     assert n == out.getvalue().count(b"\n")
@@ -104,3 +104,42 @@ def test_cli_hashes_mode_reports_hash_plain(tmp_path, algo):
     assert set(got) == want and len(got) == len(want)
     assert any(b"$HEX[" in x for x in got)
     assert b"1 line(s)" in r.stderr
+
+
+def test_cli_streams_dictionary_in_chunks(tmp_path):
+    """The dictionary is read in bounded chunks (ScanLines across chunk edges, CRLF,
+    empty lines) and expanded in small batches by the two-context pipeline, in batch
+    order; the first line with no newline in 64 KiB ends the input silently, as the
+    reference's unchecked bufio.Scanner does (main.go:72-74)."""
+    from hashcat_a5_table_generator_amd import synth
+    _, (d, o) = synth.config_words("c1", 6000, seed=0xC11)
+    words = [bytes(d[int(o[i]):int(o[i + 1])]) for i in range(len(o) - 1)]
+    body = b"\n".join(words[:4000]) + b"\nab\r\n\n" + b"\n".join(words[4000:]) + b"\n"
+    long_line = b"q" * (64 * 1024) + b"\n"
+    full = body + long_line + b"never\nseen\n"
+    p = tmp_path / "d.txt"
+    p.write_bytes(full)
+    env = dict(os.environ, A5X_CLI_CHUNK="4099", A5X_CLI_BATCH="700")
+    r = subprocess.run([CLI, str(p), "-t", table_path("qwerty-azerty")], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr.decode(errors="replace")[-2000:]
+    ow, oo = _oracle_words(full)  # split_words stops at the long line too
+    assert len(oo) - 1 == 6002  # 6000 words + "ab" + ""
+    # batch order is kept, so the stream is the per-word concatenation
+    _per_word_check(r.stdout, ow, oo, 0, ["qwerty-azerty"])
+
+
+def test_cli_hashes_long_potfile_line(tmp_path):
+    """A --hashes line longer than any fixed buffer (a potfile line with a 10 KB plain)
+    is one line: its digest is loaded once, no piece of it becomes a target."""
+    from oracle import digest_oracle as dg
+    (tmp_path / "d.txt").write_bytes(b"qa\n")
+    d = dg.md5(b"aa")  # qwerty-azerty: q -> a
+    piece = dg.md5(b"zz").hex()
+    lines = [d.hex() + ":" + "x" * 5000 + piece + ":" + "y" * 5000]
+    (tmp_path / "h.txt").write_text("\n".join(lines) + "\n")
+    r = subprocess.run([CLI, str(tmp_path / "d.txt"), "-t", table_path("qwerty-azerty"), "--hashes",
+                        str(tmp_path / "h.txt")], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert r.returncode == 0, r.stderr.decode(errors="replace")[-2000:]
+    assert r.stdout == d.hex().encode() + b":aa\n"
+    assert b"line(s)" not in r.stderr

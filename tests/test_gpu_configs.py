@@ -202,7 +202,7 @@ def test_fused_equals_two_pass(algo, wl, tabs):
 
 @pytest.mark.parametrize("algo", [0, 1])
 def test_hybrid_fused_digest_mixed_batch(algo):
-    """A batch with non-FAST words (more than 8 pieces, BIG and pass-G lines for MD5)
+    """A batch with non-FAST words (more than 8 pieces, BIG and pass-G lines)
     among FAST ones: the fused kernel hashes the FAST words and the others go through the
     two-pass path as a gathered sub-batch; the hits equal the all-two-pass run's and
     include every planted (word, candidate)."""
@@ -220,8 +220,7 @@ def test_hybrid_fused_digest_mixed_batch(algo):
         return bytes(w)
 
     extra = [spread(int(rng.integers(57, 62)), b"aeu") for _ in range(300)]   # > 8 pieces: not FAST
-    if algo == 0:                                                              # BIG and pass-G lines
-        extra += [spread(L, b"ae") for L in (100, 700, 2100, 5000)]
+    extra += [spread(L, b"ae") for L in (100, 700, 2100, 5000)]                # BIG and pass-G lines
     pos = sorted(rng.choice(len(words) + len(extra), size=len(extra), replace=False))
     for p, w in zip(pos, extra):
         words.insert(int(p), w)
@@ -249,3 +248,119 @@ def test_hybrid_fused_digest_mixed_batch(algo):
     got = {(w, c) for w, c, _ in fused}
     assert set(planted) <= got
     assert any(w in set(int(p) for p in pos) for w, _ in got)  # hits in the non-FAST words too
+
+
+def test_hybrid_digest_hit_cap_below_hits():
+    """Regression for the hybrid path's host-side hit handling (round-2 segfault record,
+    gpurun_out/th.log at 02:01): the caller's buffer smaller than the hits
+    found -- hit_cap 0 with a null buffer, hit_cap filled by the fused FAST words alone
+    (the non-FAST sub-batch gets room == 0), and room for only some of the sub-batch's
+    hits.  Every call reports the full count with A5X_E_CAPACITY, writes only inside
+    the buffer, and returns a subset of the uncapped run's hits."""
+    import ctypes
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, _lib, pack_words, synth
+    from oracle import digest_oracle as dg
+    _, (data, offs) = synth.global_words("c3", 0, 4000, seed=0xB8)
+    words = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in range(len(offs) - 1)]
+    rng = np.random.default_rng(23)
+    extra = [bytes(rng.choice(list(b"0123456789"), size=58).astype(np.uint8)) + b"aeu" for _ in range(40)]
+    extra += [b"1" * 700 + b"ae", b"2" * 2100 + b"ea"]  # BIG and pass-G lines
+    words += extra
+    with Context(0) as ctx:
+        ctx.load_tables([table_path("czech"), table_path("german")])
+        cands = ctx.expand_words(words, 0, 0, 15)
+        # every candidate of 30 FAST words and of every non-FAST word is a target: many
+        # hits on both sides of the hybrid split
+        pick = list(range(30)) + list(range(len(words) - len(extra), len(words)))
+        tg = {dg.md5(c) for i in pick for c in cands[i][:64]}
+        ctx.set_targets(0, b"".join(sorted(tg)))
+        d, o = pack_words(words)
+        dw, do = DeviceBuffer.from_array(ctx, d), DeviceBuffer.from_array(ctx, o)
+        full, _ = ctx.expand_digest_device(dw.ptr, do.ptr, len(words), 0, 0, 15, hit_cap=1 << 16)
+        fset = set(full)
+        n_fast = sum(1 for w, _, _ in full if w < 30)
+        assert n_fast > 0 and len(full) > n_fast
+        for cap in (0, n_fast, n_fast + 3, len(full) - 1):
+            arr = (_lib.Hit * (cap + 8))()  # 8 guard entries past the cap stay untouched
+            for k in range(cap, cap + 8):
+                arr[k].word = 0xDEADBEEF
+            nh = ctypes.c_uint64()
+            rc = ctx._L.a5x_expand_digest_device(ctx.h, dw.ptr, do.ptr, len(words), 0, 0, 15, 0,
+                                                 arr if cap else None, cap, ctypes.byref(nh), None, None)
+            assert rc == -8, (cap, rc)  # A5X_E_CAPACITY
+            assert nh.value == len(full)
+            assert all(arr[k].word == 0xDEADBEEF for k in range(cap, cap + 8))
+            got = ctx._hits(arr, cap)
+            assert set(got) <= fset and len(set(got)) == cap
+
+
+def test_c2_shape_greek_and_ascii():
+    """C2 = configs[1] (qwerty-greek.table; greek-dictionary.txt is not in the snapshot,
+    .MISSING_LARGE_BLOBS:1): 1M synthetic Greek words give exactly 0 candidates (every
+    qwerty-greek key is ASCII, so processWord never matches a Greek byte), and the
+    ASCII variant -- 1M [a-z] words x qwerty-greek, ~971 multi-byte candidates per word --
+    equals the C oracle's per-word digests."""
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
+    from oracle import c_oracle as co
+    with Context(0) as ctx:
+        ctx.load_tables([table_path("qwerty-greek")])
+        _, (data, offs) = synth.global_words("c2", 0, 1_000_000, seed=0xC2)
+        dw, do = DeviceBuffer.from_array(ctx, data), DeviceBuffer.from_array(ctx, offs)
+        tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, len(offs) - 1)
+        assert (tc, tb) == (0, 0)
+        dw.free()
+        do.free()
+        _, (data, offs) = synth.global_words("c2a", 0, 1_000_000, seed=0xC2A)
+        tc, tb, got = _gpu_digest(ctx, data, offs)
+    n = len(offs) - 1
+    assert 900 * n < tc < 1050 * n and tb > 15 * tc
+    want = co.CTable([table_path("qwerty-greek")]).digest_batch(data, offs, 0, 0, 15, nthreads=NTH)
+    _check(got, want, data, offs)
+
+
+@pytest.mark.parametrize("algo,mode,mn,wl,tabs,ntarget", [
+    (0, 3, 1, "c5", ["greek-hebrew"], 1_000_000),   # README.MD:159,163: -s -r -m 1 | hashcat, C5 shape
+    (1, 3, 1, "c5", ["greek-hebrew"], 1_000_000),
+    (0, 2, 0, "c5", ["greek-hebrew"], 20_000),
+    (1, 1, 0, "c5", ["greek-hebrew"], 20_000),
+    (0, 2, 0, "c3", ["czech", "german"], 20_000),    # non-confluent s / ss: the byte builder
+    (1, 1, 2, "c3", ["czech", "german"], 20_000),    # -r with the running-offset bug: builder
+])
+def test_mode_fused_digest_equals_two_pass(algo, mode, mn, wl, tabs, ntarget):
+    """-r / -s / -s -r fused digest (op 2 of the mode engines: every candidate hashed in
+    the positional ring or the builder's lane buffer, no length pass, no HBM stream)
+    reports exactly the two-pass path's hits (expansion into HBM scratch +
+    k_digest_stream), including every planted (word, candidate) -- with lines past the
+    LDS engines' 128 B (mode pass G) in the batch."""
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, pack_words, synth
+    from oracle import digest_oracle as dg
+    _, (data, offs) = synth.global_words(wl, 0, 40_000, seed=0xF6 + mode)
+    words = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in range(len(offs) - 1)]
+    words[100:100] = [b"0" * 150 + words[7], words[9] + b"1" * 300]  # > 128 B: mode pass G
+    n = len(words)
+    rng = np.random.default_rng(5 + mode)
+    f = dg.ALGOS[algo]
+    with Context(0) as ctx:
+        ctx.load_tables([table_path(t) for t in tabs])
+        ws = sorted(set(int(x) for x in rng.choice(n, size=300, replace=False)) | {100, 101})
+        cands = ctx.expand_words([words[i] for i in ws], mode, mn, 15)
+        planted = {}
+        for w, cs in zip(ws, cands):
+            if cs:
+                c = int(rng.integers(0, len(cs)))
+                planted[(w, c)] = f(cs[c])
+        rand = rng.integers(0, 256, size=(ntarget - len(planted), 16), dtype=np.uint8)
+        ctx.set_targets(algo, b"".join(planted.values()) + rand.tobytes())
+        d, o = pack_words(words)
+        dw, do = DeviceBuffer.from_array(ctx, d), DeviceBuffer.from_array(ctx, o)
+        fused, st = ctx.expand_digest_device(dw.ptr, do.ptr, n, mode, mn, 15, hit_cap=1 << 16)
+        os.environ["A5X_NO_FUSED_DIGEST"] = "1"
+        try:
+            two, st2 = ctx.expand_digest_device(dw.ptr, do.ptr, n, mode, mn, 15, hit_cap=1 << 16)
+        finally:
+            os.environ.pop("A5X_NO_FUSED_DIGEST")
+    assert st["candidates"] == st2["candidates"] > 0
+    assert sorted(fused) == sorted(two)
+    got = {(w, c) for w, c, _ in fused}
+    assert set(planted) <= got
+    assert (100, 0) in {(w, 0) for w, _ in got} or all(w != 100 for w, _ in planted)

@@ -34,7 +34,8 @@ def test_digest_every_candidate(gpu_ctx, algo, tabs):
     gpu_ctx.load_tables([table_path(t) for t in tabs])
     words = _words(algo * 7 + len(tabs), 1500, greek=tabs == ["greek-hebrew"])
     # MD5 block edges (55/56/63/64/119/120 bytes) with one substitutable letter each
-    words += [b"1" * (n - 1) + b"a" for n in (54, 55, 56, 63, 64, 119, 120, 200)]
+    # (and lines past the 256 B staging margin -- hashed from HBM -- up to a pass-G word)
+    words += [b"1" * (n - 1) + b"a" for n in (54, 55, 56, 63, 64, 119, 120, 200, 600, 1500, 3000)]
     data, offs = pack_words(words)
     dw = DeviceBuffer.from_array(gpu_ctx, data)
     do = DeviceBuffer.from_array(gpu_ctx, offs)
@@ -43,12 +44,6 @@ def test_digest_every_candidate(gpu_ctx, algo, tabs):
     gpu_ctx.expand_device(dw.ptr, do.ptr, len(words), out.ptr, tb)
     stream = bytes(out.to_array(count=tb))
     lines = stream.split(b"\n")[:-1]
-    if algo == 1:  # NTLM device limit: 64 UTF-16 units
-        keep = [ln for ln in lines if len(dg.utf16le_go(ln)) <= 128]
-        if len(keep) != len(lines):
-            stream = b"".join(x + b"\n" for x in keep)
-            lines = keep
-            out = DeviceBuffer.from_array(gpu_ctx, np.frombuffer(stream, dtype=np.uint8))
     dig = DeviceBuffer(gpu_ctx, 16 * len(lines) + 16)
     n = gpu_ctx.digest_lines_device(algo, out.ptr, len(stream), dig.ptr, len(lines))
     assert n == len(lines)
@@ -120,8 +115,8 @@ def test_digest_long_candidates_cross_block_edges(gpu_ctx, algo):
     gpu_ctx.clear_table()
     gpu_ctx.load_tables([table_path("czech")])
     rng = np.random.default_rng(11 + algo)
-    top = 300 if algo == 0 else 60  # NTLM device limit: 64 UTF-16 units
-    words = [b"1" * int(rng.integers(top - 50, top)) + b"a" for _ in range(200 if algo == 0 else 600)]
+    # (NTLM streams its UTF-16LE into the MD4 blocks: no length limit, same lines as MD5)
+    words = [b"1" * int(rng.integers(250, 300)) + b"a" for _ in range(200)]
     data, offs = pack_words(words)
     dw, do = DeviceBuffer.from_array(gpu_ctx, data), DeviceBuffer.from_array(gpu_ctx, offs)
     tc, tb = gpu_ctx.keyspace_device(dw.ptr, do.ptr, len(words))
@@ -178,3 +173,28 @@ def test_fused_ntlm_multi_block_candidates(gpu_ctx):
     assert got == {(w, i) for w, cs in enumerate(per_word) for i in range(len(cs))}
     for w, c, d in hits:
         assert dg.ntlm(per_word[w][c]) == d
+
+
+def test_format_hits_word_past_4gib_of_output(gpu_ctx):
+    """a5x_format_hits regenerates only the hit candidates (located, expanded as short
+    ranges), so a hit in a word whose output is past 2^32 bytes -- "a" x 32 with a -> b,
+    1.85e9 candidates, 61 GB -- still yields its exact plain (the whole-word
+    re-expansion truncated its uint32 line offsets and exhausted host memory)."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer, pack_words
+    from oracle import digest_oracle as dg
+    word = b"a" * 32
+    plains = [b"b" * 15 + b"a" * 17, b"a" * 31 + b"b", b"ab" * 7 + b"a" * 18]
+    gpu_ctx.clear_table()
+    gpu_ctx.set_table({b"a": [b"b"]})
+    try:
+        d, o = pack_words([b"qq", word, b"a"])
+        dw, do = DeviceBuffer.from_array(gpu_ctx, d), DeviceBuffer.from_array(gpu_ctx, o)
+        tc, tb = gpu_ctx.keyspace_device(dw.ptr, do.ptr, 3)
+        assert tb > (1 << 32) and tc == 1846943452 + 1
+        gpu_ctx.set_targets(0, b"".join(dg.md5(p) for p in plains))
+        hits, _ = gpu_ctx.expand_digest_device(dw.ptr, do.ptr, 3, 0, 0, 15, scratch_bytes=8 << 30)
+        assert sorted(w for w, _, _ in hits) == [1, 1, 1]
+        lines = gpu_ctx.format_hits(d, o, hits).split(b"\n")[:-1]
+        assert sorted(lines) == sorted(dg.md5(p).hex().encode() + b":" + p for p in plains)
+    finally:
+        gpu_ctx.clear_table()

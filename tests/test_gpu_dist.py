@@ -1,0 +1,86 @@
+"""Multi-rank path on the GPU: bench.py's own sharding driven by two ranks (gloo
+collectives, both ranks on device 0 of the one-GPU box) through liba5x.
+
+north_star (e): ONE global word list, split across ranks by balanced output-byte prefix
+(each rank keyspaces an equal word-count block on its device; dist.distributed_split),
+every rank expands (or expands + digests + looks up) its shard with no data-path
+collective; hit records are gathered on rank 0 with global word indices.  The
+concatenated per-word digests and the gathered hits must equal a single-rank run over
+the same global list (main.go:77: words are independent).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(world, args, dump):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--backend", "gloo",
+               "--same-device", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--dump", str(dump), *args]
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        assert p.returncode == 0, e[-3000:]
+        outs.append(o)
+    return json.loads(outs[0].strip().splitlines()[-1])
+
+
+def _digests(dump):
+    parts = []
+    for f in os.listdir(dump):
+        if f.startswith("digest_"):
+            w0, w1 = (int(x) for x in f[len("digest_"):-len(".npy")].split("_"))
+            parts.append((w0, w1, np.load(os.path.join(dump, f))))
+    parts.sort()
+    assert all(a[1] == b[0] for a, b in zip(parts, parts[1:])), [(a, b) for a, b, _ in parts]
+    return parts[0][0], parts[-1][1], np.concatenate([p[2] for p in parts])
+
+
+def test_two_ranks_expand_equals_one_rank(tmp_path):
+    """C3 words: 2 ranks x 30k words per rank == 1 rank x 60k words, per-word digests."""
+    r2 = _bench(2, ["--workload", "c3", "--words", "30000"], tmp_path / "w2")
+    r1 = _bench(1, ["--workload", "c3", "--words", "60000"], tmp_path / "w1")
+    a0, a1, d2 = _digests(tmp_path / "w2")
+    b0, b1, d1 = _digests(tmp_path / "w1")
+    assert (a0, a1) == (b0, b1) == (0, 60000)
+    assert np.array_equal(d2, d1)
+    assert r2["n_gpus"] == 2 and r2["config"]["candidates_per_gpu_step"] > 0
+    # every rank's candidates sum to the single-rank run's (value = all ranks' candidates / time)
+    assert int(d2[:, 0].sum()) == r1["config"]["candidates_per_gpu_step"]
+
+
+@pytest.mark.parametrize("algo", ["md5", "ntlm"])
+def test_two_ranks_digest_hits_gathered(tmp_path, algo):
+    """C5 words, fused digest + lookup: the hits gathered on rank 0 (global word indices)
+    equal the single-rank run's over the same global list and target set."""
+    args = ["--workload", "c5", "--digest", algo, "--targets", "20000"]
+    r2 = _bench(2, args + ["--words", "20000"], tmp_path / "h2")
+    r1 = _bench(1, args + ["--words", "40000"], tmp_path / "h1")
+    h2 = np.load(tmp_path / "h2" / "hits.npy")
+    h1 = np.load(tmp_path / "h1" / "hits.npy")
+    assert len(h1) >= r1["config"]["planted"] > 0
+    key = lambda h: sorted(map(tuple, h.tolist()))
+    assert key(h2) == key(h1)
+    assert r2["config"]["hits_gathered_on_rank0"] == len(h1) and r2["config"]["planted"] == r1["config"]["planted"]

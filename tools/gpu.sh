@@ -1,0 +1,164 @@
+#!/bin/bash
+# tools/gpu.sh -- the one GPU-box script: runs the named steps in order, stops at the
+# first failure (each GPU step under its own time limit).  Outputs go to gpurun_out/.
+#
+#   /usr/local/graft/bin/gpurun --timeout 900 -- 'TAG=r03a bash tools/gpu.sh test bench prof'
+#
+# steps (environment knobs in brackets):
+#   test        pytest -m gpu [TESTS=paths, K=-k expr, TT=per-step seconds]
+#   bench       one bench.py line -> gpurun_out/bench_$TAG$NAME.json [BENCH_ARGS, NAME]
+#   ab          A/B of liba5x variants on one workload [VARIANTS="name:ENV=v,LIB=path ...",
+#               STEPS, WORDS, WL, BENCH_ARGS]
+#   prof        rocprofv3 --kernel-trace --stats of a short bench run [BENCH_ARGS]
+#   traffic     PMC WRITE_SIZE / FETCH_SIZE of k_expand_fast -> gpurun_out/pmc_$TAG_$WL.json
+#               [WL, WORDS, KRE]
+#   pmc         PMC counter groups, one pass each (PMC="group\ngroup", KRE, BENCH_ARGS)
+#   digestprof  fused-digest kernel stats + VALU counters [ALGOS, KRE, WORDS]
+#   stamps      per-phase cycle stamps (diagnostic build _build_diag) [WL, SW]
+#   final       test + C3 bench/prof/traffic + C4 + C2a + fused digests + C5 modes + stdout path
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 2
+mkdir -p gpurun_out
+T=${TAG:-x}
+
+summ() {  # one-line summary of a bench JSON
+  python3 - "$1" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1]))
+r = d.get("roofline") or {}
+extra = ""
+if r.get("bound") == "hbm":
+    extra = "expand %.2f ms %.0f GB/s frac %.3f ks %.2f ms" % (r["ms_per_launch"], r["achieved"], r["frac"],
+                                                            r.get("ms_keyspace_scan_plan", 0))
+elif r:
+    extra = "%s frac %s" % (r.get("kernel"), r.get("frac"))
+ss = d.get("steady_state")
+if ss:
+    extra += " | steady %.3e cand/s frac %.3f" % (ss["value"], ss["frac"])
+c = d.get("cpu_baseline")
+print("%-28s value %.3e %s step %.2f ms %s%s" % (sys.argv[1].split("/")[-1], d["value"], d["unit"], d["ms_per_step"],
+                                              extra, (" cpu %.3e" % c["value"]) if c else ""))
+PY
+}
+
+step_test() {
+  timeout -k 10 ${TT:-600} python -u -m pytest ${TESTS:-tests/} -v -m gpu -x ${K:+-k "$K"} --timeout ${TTO:-200} \
+    --timeout-method thread > gpurun_out/test_$T.log 2>&1
+  local rc=$?
+  echo "pytest rc=$rc"; tail -2 gpurun_out/test_$T.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/test_$T.log | head -8; return 10; }
+}
+
+step_bench() {
+  local f=gpurun_out/bench_$T${NAME}.json
+  timeout -k 10 ${BT:-400} python bench.py ${BENCH_ARGS} > $f 2> ${f%.json}.err || { tail -5 ${f%.json}.err; return 11; }
+  summ $f
+}
+
+step_ab() {
+  for v in ${VARIANTS:-"cur:X=0"}; do
+    local name=${v%%:*} envs=${v#*:}
+    ( IFS=','; for kv in $envs; do
+        k=${kv%%=*}; val=${kv#*=}
+        if [ "$k" = LIB ]; then export A5X_LIB_PATH=$R/$val; else export $k=$val; fi
+      done
+      unset IFS
+      timeout -k 10 200 python bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --words ${WORDS:-10000000} \
+        --workload ${WL:-c3} ${BENCH_ARGS} > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.err ) \
+      || { echo "bench $name failed"; tail -5 gpurun_out/ab_$name.err; return 12; }
+    summ gpurun_out/ab_$name.json
+  done
+}
+
+step_prof() {
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$T \
+      -o run --output-format csv -- python3 $R/bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline \
+      ${BENCH_ARGS} > $R/gpurun_out/prof_$T.log 2>&1 ) || { tail -5 gpurun_out/prof_$T.log; return 13; }
+  python3 - <<PY
+import csv
+for r in list(csv.DictReader(open("$R/gpurun_out/prof_$T/run_kernel_stats.csv")))[:8]:
+    print("%-28s calls %4s avg %10.1f us total %8.2f ms %5s%%" % (r["Name"][:28], r["Calls"],
+          float(r["AverageNs"]) / 1e3, float(r["TotalDurationNs"]) / 1e6, r["Percentage"]))
+PY
+}
+
+step_traffic() {
+  local W=${WORDS:-10000000} WLx=${WL:-c3}
+  local ARGS="--steps 1 --warmup 0 --no-cpu-baseline --words $W --workload $WLx"
+  for grp in WRITE_SIZE FETCH_SIZE; do
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-k_expand_fast}" \
+        -d $R/gpurun_out/pmct_${T}_$grp -o run --output-format csv -- python3 $R/bench.py $ARGS \
+        > $R/gpurun_out/pmct_${T}_$grp.log 2>&1 ) || { echo "pmc $grp failed"; tail -5 gpurun_out/pmct_${T}_$grp.log; return 14; }
+  done
+  python3 tools/pmc_summary.py traffic "$T" "$WLx" "$W" "${KRE:-k_expand_fast}"
+}
+
+step_pmc() {
+  local i=0
+  while read -r grp; do
+    [ -z "$grp" ] && continue
+    i=$((i + 1))
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-k_expand_fast}" \
+        -d $R/gpurun_out/pmc_${T}_$i -o run --output-format csv -- python3 $R/bench.py \
+        ${BENCH_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --words 2000000} > $R/gpurun_out/pmc_${T}_$i.log 2>&1 ) \
+      || { echo "pmc pass $i failed"; tail -5 gpurun_out/pmc_${T}_$i.log; return 15; }
+  done <<GROUPS
+${PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES
+SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH
+GRBM_GUI_ACTIVE SQ_INSTS_SMEM SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL}
+GROUPS
+  python3 tools/pmc_summary.py mix gpurun_out/pmc_${T}_
+}
+
+step_digestprof() {
+  local W=${WORDS:-2000000}
+  for A in ${ALGOS:-md5 ntlm}; do
+    local K=${KRE:-k_expand_fast_$A}
+    local ARGS="--digest $A --workload c5 --words $W --no-cpu-baseline --targets 1000000 ${DARGS}"
+    ( cd /tmp && export TMPDIR=/tmp &&
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/dprof_$A -o run --output-format csv -- \
+        python3 $R/bench.py $ARGS --steps 2 --warmup 1 > $R/gpurun_out/dprof_$A.log 2>&1 &&
+      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        SQ_INSTS_SALU GRBM_GUI_ACTIVE --kernel-include-regex $K -d $R/gpurun_out/dpmc1_$A -o run --output-format csv -- \
+        python3 $R/bench.py $ARGS --steps 1 --warmup 0 > $R/gpurun_out/dpmc1_$A.log 2>&1 ) \
+      || { echo "digest prof $A failed"; tail -5 gpurun_out/dprof_$A.log gpurun_out/dpmc1_$A.log; return 16; }
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc VALUBusy VALUUtilization \
+        --kernel-include-regex $K -d $R/gpurun_out/dpmc2_$A -o run --output-format csv -- \
+        python3 $R/bench.py $ARGS --steps 1 --warmup 0 > $R/gpurun_out/dpmc2_$A.log 2>&1 ) \
+      || echo "derived VALUBusy pass $A failed (raw counters only)"
+    python3 tools/digest_prof_summary.py $A $W $K || return 16
+  done
+}
+
+step_stamps() {
+  timeout -k 10 120 python tools/stamps.py ${WL:-c3} ${SW:-2000000} > gpurun_out/stamps_$T.txt 2>&1 \
+    || { tail -5 gpurun_out/stamps_$T.txt; return 17; }
+  cat gpurun_out/stamps_$T.txt
+}
+
+step_final() {
+  TT=900 step_test || return $?
+  NAME=_c3 BENCH_ARGS="" step_bench || return $?
+  BENCH_ARGS="" step_prof || return $?
+  WL=c3 step_traffic || return $?
+  NAME=_c3_steady BENCH_ARGS="--steady-batches 4 --no-cpu-baseline" step_bench || return $?
+  NAME=_c4 BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --workload c4 --words 12500000" step_bench || return $?
+  NAME=_c2a BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --workload c2a --words 1000000" step_bench || return $?
+  ALGOS="md5 ntlm" step_digestprof || return $?
+  for alg in md5 ntlm; do
+    NAME=_digest_$alg BENCH_ARGS="--digest $alg --workload c5 --words 2000000 --targets 1000000 --steps 3 --warmup 1" \
+      step_bench || return $?
+  done
+  for m in 1 2 3; do
+    NAME=_c5_mode$m BENCH_ARGS="--mode $m --workload c5 --steps 3 --warmup 1 --no-cpu-baseline" step_bench || return $?
+  done
+  NAME=_stdout BENCH_ARGS="--stdout --no-cpu-baseline" step_bench || return $?
+}
+
+[ $# -gt 0 ] || set -- test
+for s in "$@"; do
+  echo "== step $s ($(date +%T))"
+  "step_$s" || { rc=$?; echo "step $s failed (rc $rc)"; exit $rc; }
+done
+echo "== done ($(date +%T))"
