@@ -69,6 +69,7 @@ constexpr u32 M_ERR_LIMIT = 1u << 6;  // word beyond the mode-engine limits
 constexpr u32 M_ERR_PANIC = 1u << 7;  // -r slice-bounds panic (main.go:255)
 constexpr u32 M_ERR_CLEN = 1u << 8;   // a candidate longer than the lane buffer
 constexpr u32 M_ERR_GWORD = 1u << 30; // (not an error) word longer than A5X_M_LMAX: mode pass G
+constexpr u64 M_WB_FAST = 1ull << 62;  // k_mode_count's wbytes of a single-item word: route MI_FAST
 
 
 // positional -s / -s -r words (m_pos_setup): entries (a5x_ring.h) and the token list
@@ -83,17 +84,35 @@ constexpr u32 MP_VMAX = 14;   // values per pattern (selector 1 + v <= 15)
 // (2 x 64 x STRIDE), the positional engine's ring only (MP_RING), or none (counting
 // and closed-form lengths): the smaller layouts run more waves per CU.
 constexpr u32 MP_RING = 16 + 64 * A5X_M_CBUF + 48;
-template <u32 LMAX, u32 CBUF, u32 NBUF = 2 * 64 * (CBUF + 4)>
+// radix words (MInfo::radix), piece expansion (m_fast_expand): the multi-token pieces'
+// entries follow the token entries (ent[MP_NE ..]); pieces of one word
+constexpr u32 MF_NPE = 256;
+constexpr u32 MF_PMAX = A5X_M_LMAX + 2;
+#ifndef MF_RING
+#define MF_RING 4096         // the piece engine's ring (runs that do not fit wait a round)
+#endif
+#ifndef MF_K
+#define MF_K 4               // leaves per lane run (odometer steps between them)
+#endif
+#ifndef MF_OFF
+#define MF_OFF 0             // 1: radix words stay on the token ring (A/B builds)
+#endif
+#ifndef MF_EMAX
+#define MF_EMAX 64           // entries of one multi-token piece
+#endif
+template <u32 LMAX, u32 CBUF, u32 NBUF = 2 * 64 * (CBUF + 4), u32 DPN = A5X_M_DPMAX, u32 NPE = 0>
 struct MLdsT {
   static constexpr u32 L_MAX = LMAX, STRIDE = CBUF + 4, CMAXLEN = CBUF - 1;
   static constexpr bool G = LMAX > A5X_M_LMAX;
   static constexpr bool BUILDER = NBUF >= 2 * 64 * STRIDE, RING = NBUF >= MP_RING;
-  u64 dp[A5X_M_DPMAX];
-  uint4 ent[MP_NE];
+  static constexpr bool FAST = NPE > 0;  // piece engine layout: no DP table (radix words only)
+  u64 dp[DPN ? DPN : 1];
+  uint4 ent[MP_NE + NPE];
+  uint4 pdesc[NPE ? MF_PMAX : 1];  // pieces: entry base (bias folded) | selector shifts | strides | sources
   u32 tok[A5X_M_LMAX + 2];   // entry base | (pattern index + 1) << 16 (0: literal chunk)
   uint8_t mpi[A5X_M_LMAX];   // pattern index + 1 matched at byte q (0: none)
   uint8_t pb[MP_PMAX], occ[MP_PMAX];
-  uint8_t elen[MP_NE];       // entry lengths
+  uint8_t elen[MP_NE + NPE]; // entry lengths
   u32 rmag[MP_PMAX];         // radix mode: magic of R_r = 1 + values of pattern r
   uint8_t rr[MP_PMAX];       // R_r
   u32 ntok, radix, shift;
@@ -107,6 +126,7 @@ struct MLdsT {
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF> MLds;                // byte builder (general words)
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MP_RING> MLdsR;      // positional expansion
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, 16> MLdsC;           // counts, closed-form lengths
+typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MF_RING + 48, 0, MF_NPE> MLdsF;  // piece expansion (radix words)
 typedef MLdsT<A5X_MG_LMAX, A5X_MG_CBUF> MLdsG;             // mode pass G (HBM)
 
 // wave sync over the word state: LDS, or (pass G) HBM written and read by the wave's own
@@ -133,7 +153,10 @@ struct MT {
 struct MInfo {
   u32 L, n, cmin, cmax, cols;
   u64 count;
-  u32 bad;  // M_ERR_* of the word (0: fine)
+  u32 bad;    // M_ERR_* of the word (0: fine)
+  u32 radix;  // leaves = every choice vector (no size window cuts): leaf t <-> t + cmin as a
+              // mixed radix over the patterns (-s, -s -r: R = 1 + values) or the position bit
+              // set (-r, positions pairwise disjoint: binary counting)
 };
 
 __device__ __forceinline__ u32 m_lane() { return __lane_id(); }
@@ -324,14 +347,39 @@ __device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
     for (u32 x = d1; x; x &= x - 1) S.pat[o++] = (uint16_t)(64 * lane + 32 + (u32)__builtin_ctz(x));
   }
   I.n = n;
+  I.radix = 0;
   if (a.mx < 0) return I;
   const u32 cmax = min((u32)a.mx, n);
   const u32 cmin = a.mn > 0 ? (u32)a.mn : 0u;
   if (cmin > cmax) return I;
   const u32 cols = cmax + 1;
-  if ((n + 1) * cols > A5X_M_DPMAX) { I.bad = M_ERR_LIMIT; return I; }
   I.cmin = cmin; I.cmax = cmax; I.cols = cols;
   m_sync<SL>();
+  // radix words: the size window [cmin, cmax] keeps every choice vector but (cmin = 1) the
+  // all-keep one; -r also needs pairwise disjoint positions (every subset is a leaf)
+  bool rad = cmin <= 1 && cmax >= n;
+  u64 rcount = 0;  // their count in closed form
+  if (a.mode == A5X_MODE_REVERSE) {
+    rad = rad && n <= 62 && !__ballot(lane < n && S.pnx[lane] != lane + 1);
+    rcount = rad ? (1ull << n) - cmin : 0;
+  } else if (rad) {
+    u32 R = 1;
+    if (lane < n) {
+      const u32 nv = T.keys[S.pat[lane]].nvals;
+      R = 1 + (a.mode == A5X_MODE_SUBALL ? nv : (nv ? 1u : 0u));
+    }
+    u64 P = 1;
+    for (u32 r = 0; r < n && P < (1ull << 27); r++) P *= (u32)__builtin_amdgcn_readlane((int)R, (int)r);
+    rad = P < (1ull << 27);
+    rcount = rad ? P - cmin : 0;
+  }
+  if constexpr (SL::FAST) {  // piece layout: radix words only, no DP table
+    if (!rad) { I.bad = M_ERR_STATE; return I; }
+    I.radix = 1;
+    I.count = rcount;
+    return I;
+  }
+  if ((n + 1) * cols > A5X_M_DPMAX) { I.bad = M_ERR_LIMIT; return I; }
   u64* D = S.dp;
   const u32 c = lane;
   if (c < cols) D[n * cols + c] = c == 0 ? 1ull : 0ull;
@@ -360,12 +408,15 @@ __device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
     if (__builtin_add_overflow(cnt, D[k], &cnt)) ovf = 1;
   if (m_wave_or(ovf)) { I.bad = M_ERR_OVF; return I; }
   I.count = m_uniform64(cnt);
+  if (rad && I.count != rcount) { I.bad = M_ERR_STATE; return I; }
+  I.radix = rad ? 1u : 0u;
   return I;
 }
 
 // -r: leaf t -> the chosen non-overlapping positions (bit j = position j)
 template <class SL>
 __device__ __forceinline__ u64 m_rsel(const SL& S, const MInfo& I, u64 t, u32& err) {
+  if (I.radix) return t + I.cmin;  // binary counting over the disjoint positions
   const u64* D = S.dp;
   const u32 cols = I.cols, n = I.n;
   u32 c = I.cmin;
@@ -705,7 +756,7 @@ __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode) {
     // every per-pattern choice vector (minus the all-keep one when min = 1), enumerated
     // as the mixed radix over patterns (pattern 0 least significant, digit 0 = keep);
     // exact 32-bit magic division needs leaf (R - 1) < 2^32: count < 2^27
-    S.radix = (I.cmin <= 1 && I.cmax >= n && I.count + 1 < (1ull << 27)) ? 1u : 0u;
+    S.radix = I.radix;
     S.shift = I.cmin;  // leaf 0 (all keep) skipped when min = 1
   }
   if (lane < n) {
@@ -870,6 +921,221 @@ __device__ void m_pos_expand(SL& S, const MT& T, const MInfo& I, const A5xModeLa
   M_WAVE_SYNC();
 }
 
+// ---------------------------------------------------------------------------
+// Piece engine (radix positional words: MInfo::radix and a token list).  The tokens
+// are grouped left to right into pieces of <= 15 bytes with <= 3 selector sources (a
+// -r position bit, a -s pattern digit) and <= MF_EMAX entries, each entry the bytes of
+// its tokens for one combination of its sources -- the big pieces of the default engine
+// (a5x_plan.h) for these engines: a candidate is a few entry reads and ORs instead of
+// one per token.  A lane takes a run of MF_K consecutive leaves and advances the leaf's
+// selector as an odometer: -r binary counting over the positions; -s packed 4-bit
+// digits stored as digit + 16 - R, so that + 1 carries into the next pattern by itself
+// (the fields that wrapped to 0 get their bias back).  A piece's entry is
+// base + sum_s field_s * stride_s (the biases folded into base).
+// ---------------------------------------------------------------------------
+
+// concatenation of entry x at byte off of (lo, hi) (off + its length <= 15)
+__device__ __forceinline__ void m_cat(u64& lo, u64& hi, u32& off, const uint4 x) {
+  const u64 clo = (u64)x.x | ((u64)x.y << 32), chi = (u64)x.z | ((u64)(x.w & 0xFFFFFFu) << 32);
+  const u32 sh = 8u * off;
+  if (off == 0) {
+    lo |= clo;
+    hi |= chi;
+  } else if (off < 8) {
+    lo |= clo << sh;
+    hi |= (clo >> (64u - sh)) | (chi << sh);
+  } else {
+    hi |= clo << (sh - 64u);
+  }
+  off += x.w >> 24;
+}
+
+// Pieces of the positional word set up in S (after m_pos_setup): descriptors in
+// S.pdesc, multi-token pieces' entries at S.ent[MP_NE ..].  Returns the piece count;
+// biasm = the -s field biases.  (The grouping loop is wave-uniform: every lane runs it.)
+template <class SL>
+__device__ u32 m_piece_setup(SL& S, const MInfo& I, int mode, u32 ntok, u64& biasm) {
+  const u32 lane = m_lane();
+  const bool rev = mode == A5X_MODE_REVERSE;
+  biasm = 0;
+  if (!rev)
+    for (u32 r = 0; r < I.n; r++) biasm |= (u64)(16u - S.rr[r]) << (4 * r);
+  u32 np = 0, pe = 0, k = 0;
+  while (k < ntok) {
+    u32 k1 = k, ns = 0, E = 1, ml = 0;
+    u32 s0 = 0, s1 = 0, s2 = 0, R0 = 1, R1 = 1, R2 = 1;
+    while (k1 < ntok) {
+      const u32 d = S.tok[k1], pi = d >> 16, eb = d & 0xFFFFu;
+      const u32 R = pi ? (rev ? 2u : (u32)S.rr[pi - 1]) : 1u;
+      u32 mlk = 0;
+      for (u32 v = 0; v < R; v++) mlk = max(mlk, S.ent[eb + v].w >> 24);
+      const bool known = pi && ((ns > 0 && s0 == pi) || (ns > 1 && s1 == pi) || (ns > 2 && s2 == pi));
+      const bool add = pi && !known;
+      const u32 E2 = add ? E * R : E, ns2 = ns + (add ? 1u : 0u);
+      if (k1 > k && (ml + mlk > 15u || ns2 > 3u || E2 > MF_EMAX || pe + E2 > MF_NPE)) break;
+      if (add) {
+        if (ns == 0) { s0 = pi; R0 = R; }
+        else if (ns == 1) { s1 = pi; R1 = R; }
+        else { s2 = pi; R2 = R; }
+      }
+      ns = ns2;
+      E = E2;
+      ml += mlk;
+      k1++;
+    }
+    u32 base;
+    if (k1 == k + 1) {
+      base = S.tok[k] & 0xFFFFu;  // one token: its own entries, indexed by its digit
+    } else {
+      base = MP_NE + pe;
+      for (u32 e = lane; e < E; e += 64) {
+        const u32 d0 = e % R0, d1 = (e / R0) % R1, d2 = e / (R0 * R1);
+        u64 lo = 0, hi = 0;
+        u32 off = 0;
+        for (u32 kk = k; kk < k1; kk++) {
+          const u32 d = S.tok[kk], pi = d >> 16;
+          const u32 dg = !pi ? 0u : pi == s0 ? d0 : pi == s1 ? d1 : d2;
+          m_cat(lo, hi, off, S.ent[(d & 0xFFFFu) + dg]);
+        }
+        S.ent[base + e] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, ((u32)(hi >> 32) & 0xFFFFFFu) | (off << 24));
+        S.elen[base + e] = (uint8_t)off;
+      }
+      pe += E;
+    }
+    if (lane == 0) {
+      const u32 mk = rev ? 1u : 15u;
+      auto sh = [&](u32 src) -> u32 { return src ? (rev ? src - 1u : 4u * (src - 1u)) : 0u; };
+      const u32 st0 = ns > 0 ? 1u : 0u, st1 = ns > 1 ? R0 : 0u, st2 = ns > 2 ? R0 * R1 : 0u;
+      int b = (int)base;
+      if (!rev) b -= (int)((16u - R0) * st0 + (16u - R1) * st1 + (16u - R2) * st2);
+      S.pdesc[np] = make_uint4((u32)b, sh(s0) | (sh(s1) << 8) | (sh(s2) << 16) | (mk << 24),
+                               st0 | (st1 << 8) | (st2 << 16), ns);
+    }
+    np++;
+    k = k1;
+  }
+  m_sync<SL>();
+  return np;
+}
+
+__device__ __forceinline__ u32 m_piece_ix(const uint4 pd, u64 sel) {
+  const u32 mk = pd.y >> 24;
+  const u32 f0 = (u32)(sel >> (pd.y & 63u)) & mk, f1 = (u32)(sel >> ((pd.y >> 8) & 63u)) & mk,
+            f2 = (u32)(sel >> ((pd.y >> 16) & 63u)) & mk;
+  return pd.x + f0 * (pd.z & 255u) + f1 * ((pd.z >> 8) & 255u) + f2 * ((pd.z >> 16) & 255u);
+}
+
+// selector of leaf t (radix word): -r the position set t + cmin; -s the biased digits
+template <class SL>
+__device__ __forceinline__ u64 m_fast_sel(const SL& S, const MInfo& I, bool rev, u64 t) {
+  if (rev) return t + I.cmin;
+  u32 x = (u32)t + I.cmin;  // < 2^27 (MInfo::radix)
+  u64 sel = 0;
+  for (u32 r = 0; r < I.n; r++) {
+    const u32 mg = S.rmag[r], R = S.rr[r];
+    const u32 q = __umulhi(x, mg) + (mg ? 0u : x);
+    sel |= (u64)(x - q * R + 16u - R) << (4 * r);
+    x = q;
+  }
+  return sel;
+}
+
+__device__ __forceinline__ u64 m_fast_step(u64 sel, bool rev, u64 biasm) {
+  const u64 y = sel + 1;
+  if (rev) return y;
+  const u32 nf = (u32)__builtin_ctzll(y) >> 2;  // fields below the first that did not wrap
+  return y | (biasm & (nf >= 16 ? ~0ull : (1ull << (4 * nf)) - 1ull));
+}
+
+// Expand leaves [tb, te) of the radix word set up in S (pieces from m_piece_setup);
+// the first one's bytes start at a.out + pos0.  A round: 64 runs of MF_K leaves,
+// lengths -> wave scan -> the runs that fit the ring OR-place their pieces (piece-major:
+// one descriptor read per piece per run) -> complete 16-B blocks streamed out.
+template <class SL>
+__device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64 tb, u64 te, u64 pos0, u32 np,
+                              u64 biasm, u32& err) {
+  const u32 lane = m_lane();
+  uint4* r4 = (uint4*)&S.buf[0];
+  constexpr u32 RB = sizeof(S.buf) / 16;
+  constexpr u32 CAP = (RB - 3) * 16;  // (the ORs' zero overhang past the round's bytes)
+  static_assert(CAP >= MF_K * A5X_M_CBUF + 16, "ring: one run of the longest candidates");
+  const u32 ringa = fx6_addr(r4);
+  for (u32 i = lane; i < RB; i += 64) r4[i] = make_uint4(0, 0, 0, 0);
+  M_WAVE_SYNC();
+  const bool rev = a.mode == A5X_MODE_REVERSE;
+  const u32 Lc = I.L + 1;
+  u64 B = pos0 & ~15ull, pos = pos0;
+  const u64 lo = pos0;
+  const uint4 nl = make_uint4(0x0Au, 0u, 0u, 1u << 24);
+  const u64 nruns = (te - tb + MF_K - 1) / MF_K;
+  for (u64 rr = 0; rr < nruns;) {
+    const u64 run = rr + lane;
+    const u64 t = tb + run * MF_K;
+    const u32 nc = run < nruns ? (u32)min((u64)MF_K, te - t) : 0u;
+    u64 sel[MF_K];
+    sel[0] = nc ? m_fast_sel(S, I, rev, t) : 0ull;
+#pragma unroll
+    for (int c = 1; c < MF_K; c++) sel[c] = m_fast_step(sel[c - 1], rev, biasm);
+    u32 clen[MF_K], len = 0;
+#pragma unroll
+    for (int c = 0; c < MF_K; c++) clen[c] = (u32)c < nc ? (rev ? Lc : 1u) : 0u;
+    if (!rev) {
+      for (u32 p = 0; p < np; p++) {
+        const uint4 pd = S.pdesc[p];
+#pragma unroll
+        for (int c = 0; c < MF_K; c++)
+          if ((u32)c < nc) clen[c] += S.elen[m_piece_ix(pd, sel[c])];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < MF_K; c++) len += clen[c];
+    const u32 incl = m_incl_scan(len);
+    const u32 used = (u32)(pos - B);
+    const bool fit = nc > 0 && used + incl <= CAP;
+    const u32 nact = (u32)__popcll(__ballot(fit));
+    const u32 tot = nact ? (u32)__builtin_amdgcn_readlane((int)incl, (int)nact - 1) : 0u;
+    if (fit) {
+      u32 P[MF_K], sink = 0;
+      P[0] = ringa + used + incl - len;
+#pragma unroll
+      for (int c = 1; c < MF_K; c++) P[c] = P[c - 1] + clen[c - 1];
+      for (u32 p = 0; p < np; p++) {
+        const uint4 pd = S.pdesc[p];
+#pragma unroll
+        for (int c = 0; c < MF_K; c++)
+          if ((u32)c < nc) fx7_put(S.ent[m_piece_ix(pd, sel[c])], P[c], sink);
+      }
+#pragma unroll
+      for (int c = 0; c < MF_K; c++)
+        if ((u32)c < nc) fx7_put(nl, P[c], sink);
+    }
+    pos += tot;
+    rr += nact;
+    M_WAVE_SYNC();
+    const u32 nb = (u32)((pos - B) >> 4);
+    if (B + 16ull * nb > a.out_cap) { err |= M_ERR_GUARD; return; }
+    for (u32 b = lane; b < nb; b += 64) {
+      const uint4 x = r4[b];
+      const u64 X = B + 16ull * b;
+      if (X >= lo) m_store16_nt(a.out + X, x);
+      else m_store_part(a.out, X, x, lo, X + 16);
+      r4[b] = make_uint4(0, 0, 0, 0);
+    }
+    if (lane == 0 && nb) {
+      const uint4 x = r4[nb];
+      r4[nb] = make_uint4(0, 0, 0, 0);
+      r4[0] = x;
+    }
+    B += 16ull * nb;
+    M_WAVE_SYNC();
+  }
+  if (lane == 0 && pos > B) {
+    if (pos > a.out_cap) err |= M_ERR_GUARD;
+    else m_store_part(a.out, B, r4[0], lo > B ? lo : B, pos);
+  }
+  M_WAVE_SYNC();
+}
+
 // Hash candidate t of word w (len bytes at base + off: LDS, or a pass-G slot in HBM,
 // readable 8 bytes past the end) and record a hit.  Wave-collective (NTLM's block loop):
 // every lane calls it, on = whether the lane holds a candidate.
@@ -961,6 +1227,7 @@ __device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLa
       const u32 ntok = m_pos_setup(S, T, I, a.mode);
       if (ntok && a.mode == A5X_MODE_REVERSE) wb = I.count * (u64)(I.L + 1);
       else if (ntok && S.radix) wb = m_pos_prefix(S, I, I.count) - m_pos_prefix(S, I, 0);
+      if (wb != ~0ull && I.radix && !MF_OFF) wb |= M_WB_FAST;
     }
     if (m_lane() == 0) a.wbytes[w] = wb;
   }
@@ -1047,6 +1314,7 @@ __device__ u64 m_run(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a,
 constexpr uint8_t MI_POS = 1;       // positional: lengths done, ring expansion
 constexpr uint8_t MI_BUILD = 2;     // byte builder for the expansion, lengths done
 constexpr uint8_t MI_BUILD_LEN = 3; // byte builder for the lengths too
+constexpr uint8_t MI_FAST = 4;      // positional radix word: lengths done, piece engine
 template <class SL>
 __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op) {
   const u64 w = a.item_w[i];
@@ -1057,6 +1325,22 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
   const MInfo I = m_setup(S, T, a, w);
   if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
   u32 err = 0, ntok = 0;
+  if constexpr (SL::FAST) {  // op 1 of MI_FAST items (the only route here)
+    ntok = op == 1 ? m_pos_setup(S, T, I, a.mode) : 0u;
+    if (!ntok) {
+      err |= M_ERR_STATE;
+    } else {
+      u64 biasm;
+      const u32 np = m_piece_setup(S, I, a.mode, ntok, biasm);
+      const u64 rb = a.cand_begin > cw0 ? a.cand_begin - cw0 : 0;
+      const u64 re = a.cand_end - cw0 < t0 + nc ? a.cand_end - cw0 : t0 + nc;  // (cand_end > cw0 here)
+      const u64 tb = rb > t0 ? rb : t0;
+      if (a.cand_end > cw0 && tb < re)
+        m_fast_expand(S, I, a, tb, re, tb == t0 ? a.seg_boff[i] - a.out_base : 0, np, biasm, err);
+    }
+    m_err(a.err, m_wave_or(err));
+    return;
+  }
   if constexpr (!SL::G && !SL::BUILDER) {
     ntok = a.mode != A5X_MODE_DEFAULT ? m_pos_setup(S, T, I, a.mode) : 0u;
     if (op == 2) {  // fused digest: positional items here, the others to the byte builder
@@ -1081,7 +1365,8 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
       m_err(a.err, m_wave_or(err));
       return;
     }
-    if (m_lane() == 0) a.item_fl[i] = ntok ? MI_POS : a.mode == A5X_MODE_REVERSE ? MI_BUILD : MI_BUILD_LEN;
+    if (m_lane() == 0)
+      a.item_fl[i] = ntok ? (I.radix && !MF_OFF ? MI_FAST : MI_POS) : a.mode == A5X_MODE_REVERSE ? MI_BUILD : MI_BUILD_LEN;
     if (!ntok && a.mode != A5X_MODE_REVERSE) return;  // lengths need the byte builder
     if (ntok && S.radix) {  // op 0, radix mode: closed form, no candidate is visited
       const u64 run = m_pos_prefix(S, I, t0 + nc) - m_pos_prefix(S, I, t0);
@@ -1109,7 +1394,8 @@ __device__ __forceinline__ void m_items(const A5xModeLaunch& a, int op, uint8_t 
     if (a.flags[w] & A5X_WF_GLOB) continue;
     if (route && a.item_fl[i] != route) continue;
     if (op == 0 && !route && a.wbytes[w] != ~0ull) {  // sized by k_mode_count (one item)
-      if (m_lane() == 0) { a.seg_bytes[i] = a.wbytes[w]; a.item_fl[i] = MI_POS; }
+      const u64 wb = a.wbytes[w];
+      if (m_lane() == 0) { a.seg_bytes[i] = wb & ~M_WB_FAST; a.item_fl[i] = (wb & M_WB_FAST) ? MI_FAST : MI_POS; }
       continue;
     }
     m_item(S, T, a, i, op);
@@ -1119,6 +1405,7 @@ __global__ void __launch_bounds__(64) k_mode_items_len(A5xModeLaunch a) { m_item
 __global__ void __launch_bounds__(64) k_mode_items_len_b(A5xModeLaunch a) { m_items<MLds>(a, 0, MI_BUILD_LEN); }
 __global__ void __launch_bounds__(64) k_mode_items_pos(A5xModeLaunch a) { m_items<MLdsR>(a, 1, MI_POS); }
 __global__ void __launch_bounds__(64) k_mode_items_b(A5xModeLaunch a) { m_items<MLds>(a, 1, MI_BUILD); }
+__global__ void __launch_bounds__(64) k_mode_items_fast(A5xModeLaunch a) { m_items<MLdsF>(a, 1, MI_FAST); }
 __global__ void __launch_bounds__(64) k_mode_digest_pos(A5xModeLaunch a) { m_items<MLdsR>(a, 2, 0); }
 __global__ void __launch_bounds__(64) k_mode_digest_b(A5xModeLaunch a) { m_items<MLds>(a, 2, MI_BUILD); }
 
@@ -1222,6 +1509,7 @@ hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st)
     if (L.mode != A5X_MODE_REVERSE)
       hipLaunchKernelGGL(k_mode_items_len_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   } else if (op == 1) {
+    hipLaunchKernelGGL(k_mode_items_fast, g, dim3(64), m_lds<MLdsF>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_items_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_items_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   } else {

@@ -37,6 +37,11 @@ ss = d.get("steady_state")
 if ss:
     extra += " | steady %.3e cand/s frac %.3f" % (ss["value"], ss["frac"])
 c = d.get("cpu_baseline")
+if "ms_per_step" not in d:  # the stdout line: one record per path
+    print("%-28s value %.3e %s " % (sys.argv[1].split("/")[-1], d["value"], d["unit"]) + " ".join(
+        "%s %.1f GB/s (pcie %.2f)" % (k, v["GB_per_s"], v["pcie_frac"]) for k, v in d.items()
+        if isinstance(v, dict) and "GB_per_s" in v))
+    sys.exit(0)
 print("%-28s value %.3e %s step %.2f ms %s%s" % (sys.argv[1].split("/")[-1], d["value"], d["unit"], d["ms_per_step"],
                                               extra, (" cpu %.3e" % c["value"]) if c else ""))
 PY
