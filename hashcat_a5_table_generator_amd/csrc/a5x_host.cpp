@@ -96,7 +96,7 @@ struct a5x_ctx {
   DevBuf<uint64_t> hy_lens, hy_off;
   DevBuf<uint8_t> hy_words;
   uint8_t* mgscr = nullptr;   // mode pass G scratch: A5X_G_SLOTS x a5x_mode_gslot_bytes(), on first use
-  uint64_t mseg = 1024;  // candidates per mode-engine item
+  uint64_t mseg = 4096;  // candidates per mode-engine item (C5 -r: most words one item, sized by k_mode_count)
   // fused digest + lookup (a5x_digest.hip)
   int t_algo = -1;
   uint64_t n_targets = 0;

@@ -87,6 +87,7 @@ constexpr u32 MP_RING = 16 + 64 * A5X_M_CBUF + 48;
 // radix words (MInfo::radix), piece expansion (m_fast_expand): the multi-token pieces'
 // entries follow the token entries (ent[MP_NE ..]); pieces of one word
 constexpr u32 MF_NPE = 256;
+constexpr u32 MF_ZE = MP_NE + MF_NPE - 1;  // the empty entry
 constexpr u32 MF_PMAX = A5X_M_LMAX + 2;
 #ifndef MF_RING
 #define MF_RING 4096         // the piece engine's ring (runs that do not fit wait a round)
@@ -96,6 +97,9 @@ constexpr u32 MF_PMAX = A5X_M_LMAX + 2;
 #endif
 #ifndef MF_OFF
 #define MF_OFF 0             // 1: radix words stay on the token ring (A/B builds)
+#endif
+#ifndef MF_ABL
+#define MF_ABL 0             // timing ablations (diagnostic builds): 1 = no expansion, 2 = no pieces, 4 = no tokens
 #endif
 #ifndef MF_EMAX
 #define MF_EMAX 64           // entries of one multi-token piece
@@ -204,12 +208,16 @@ __device__ __forceinline__ MT m_table(uint8_t* lds, const uint8_t* g, u32 bytes)
   return T;
 }
 
-// does key k match the word at q (the word is in LDS, length L)?
-__device__ __forceinline__ bool m_match(const MT& T, const uint8_t* wd, u32 L, u32 q, u32 k) {
+// does key k match the word at q (length L)?  w4 = m_lds4(wd, q): the key's first 4
+// bytes in one masked dword compare (the blob is 16-B aligned with an 8-byte tail)
+__device__ __forceinline__ bool m_match4(const MT& T, const uint8_t* wd, u32 L, u32 q, u32 w4, u32 k) {
   const A5xMKey K = T.keys[k];
   if (K.klen == 0 || q + K.klen > L) return false;
+  const u32 n4 = K.klen < 4u ? (u32)K.klen : 4u;
+  const u32 mask = n4 == 4u ? ~0u : (1u << (8u * n4)) - 1u;
+  if ((w4 ^ m_lds4(T.blob, K.key_off)) & mask) return false;
   const uint8_t* p = T.blob + K.key_off;
-  for (u32 i = 0; i < K.klen; i++)
+  for (u32 i = 4; i < K.klen; i++)
     if (wd[q + i] != p[i]) return false;
   return true;
 }
@@ -295,19 +303,31 @@ __device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
     // positions in (start, keyLength) order (main.go:215-226): starts q = lane, lane+64
     for (u32 q0 = 0; q0 < L; q0 += 64) {
       const u32 q = q0 + lane;
-      u32 k0 = 0, k1 = 0, m = 0;
+      u32 k0 = 0, k1 = 0, m = 0, w4 = 0;
+      u64 mb = 0;  // matches among the bucket's first 64 keys
       if (q < L) {
         const u32 b = S.word[q];
         k0 = T.bucket[b];
         k1 = T.bucket[b + 1];
-        for (u32 k = k0; k < k1; k++) m += m_match(T, S.word, L, q, k) ? 1u : 0u;
+        w4 = m_lds4(S.word, q);
+        for (u32 k = k0; k < k1; k++)
+          if (m_match4(T, S.word, L, q, w4, k)) {
+            m++;
+            if (k - k0 < 64) mb |= 1ull << (k - k0);
+          }
       }
       const u32 incl = m_incl_scan(m);
       const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
       u32 o = n + incl - m;
-      if (n + tot <= A5X_M_NMAX && m)
-        for (u32 k = k0; k < k1; k++)
-          if (m_match(T, S.word, L, q, k)) { S.pat[o] = (uint16_t)k; S.pst[o] = (uint16_t)q; o++; }
+      if (n + tot <= A5X_M_NMAX && m) {
+        for (u64 x = mb; x; x &= x - 1) {
+          S.pat[o] = (uint16_t)(k0 + (u32)__builtin_ctzll(x));
+          S.pst[o] = (uint16_t)q;
+          o++;
+        }
+        for (u32 k = k0 + 64; k < k1; k++)
+          if (m_match4(T, S.word, L, q, w4, k)) { S.pat[o] = (uint16_t)k; S.pst[o] = (uint16_t)q; o++; }
+      }
       n += tot;
     }
     if (n > A5X_M_NMAX) { I.bad = M_ERR_LIMIT; return I; }
@@ -325,9 +345,9 @@ __device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
     for (u32 i = lane; i < nwd; i += 64) S.bitmap[i] = 0;
     m_sync<SL>();
     for (u32 q = lane; q < L; q += 64) {
-      const u32 b = S.word[q];
+      const u32 b = S.word[q], w4 = m_lds4(S.word, q);
       for (u32 k = T.bucket[b]; k < T.bucket[b + 1]; k++)
-        if (m_match(T, S.word, L, q, k)) atomicOr(&S.bitmap[k >> 5], 1u << (k & 31));
+        if (m_match4(T, S.word, L, q, w4, k)) atomicOr(&S.bitmap[k >> 5], 1u << (k & 31));
     }
     if (T.h->has_empty && L > 0 && lane == 0) atomicOr(&S.bitmap[0], 1u);
     m_sync<SL>();
@@ -954,7 +974,7 @@ __device__ __forceinline__ void m_cat(u64& lo, u64& hi, u32& off, const uint4 x)
 // S.pdesc, multi-token pieces' entries at S.ent[MP_NE ..].  Returns the piece count;
 // biasm = the -s field biases.  (The grouping loop is wave-uniform: every lane runs it.)
 template <class SL>
-__device__ u32 m_piece_setup(SL& S, const MInfo& I, int mode, u32 ntok, u64& biasm) {
+__device__ u32 m_piece_setup_serial(SL& S, const MInfo& I, int mode, u32 ntok, u64& biasm) {
   const u32 lane = m_lane();
   const bool rev = mode == A5X_MODE_REVERSE;
   biasm = 0;
@@ -972,7 +992,7 @@ __device__ u32 m_piece_setup(SL& S, const MInfo& I, int mode, u32 ntok, u64& bia
       const bool known = pi && ((ns > 0 && s0 == pi) || (ns > 1 && s1 == pi) || (ns > 2 && s2 == pi));
       const bool add = pi && !known;
       const u32 E2 = add ? E * R : E, ns2 = ns + (add ? 1u : 0u);
-      if (k1 > k && (ml + mlk > 15u || ns2 > 3u || E2 > MF_EMAX || pe + E2 > MF_NPE)) break;
+      if (k1 > k && (ml + mlk > 15u || ns2 > 3u || E2 > MF_EMAX || pe + E2 > MF_NPE - 1u)) break;
       if (add) {
         if (ns == 0) { s0 = pi; R0 = R; }
         else if (ns == 1) { s1 = pi; R1 = R; }
@@ -1009,17 +1029,123 @@ __device__ u32 m_piece_setup(SL& S, const MInfo& I, int mode, u32 ntok, u64& bia
       int b = (int)base;
       if (!rev) b -= (int)((16u - R0) * st0 + (16u - R1) * st1 + (16u - R2) * st2);
       S.pdesc[np] = make_uint4((u32)b, sh(s0) | (sh(s1) << 8) | (sh(s2) << 16) | (mk << 24),
-                               st0 | (st1 << 8) | (st2 << 16), ns);
+                               st0 | (st1 << 8) | (st2 << 16), ns | (fx8_slots(ml) << 8));
     }
     np++;
     k = k1;
+  }
+  if (lane == 0) {  // the empty entry (leaves past a run's end)
+    S.ent[MF_ZE] = make_uint4(0, 0, 0, 0);
+    S.elen[MF_ZE] = 0;
+  }
+  m_sync<SL>();
+  return np;
+}
+
+// m_piece_setup_serial's pieces (the same grouping), built lane-parallel for words of
+// <= 64 tokens: every token's choices and longest entry at once (lane = token), the
+// greedy grouping as a scalar loop over those registers (readlane: no LDS round trip
+// per step), descriptors lane = piece, entries lane = entry of any multi-token piece.
+template <class SL>
+__device__ u32 m_piece_setup(SL& S, const MInfo& I, int mode, u32 ntok, u64& biasm) {
+  if (ntok > 64) return m_piece_setup_serial(S, I, mode, ntok, biasm);
+  const u32 lane = m_lane();
+  const bool rev = mode == A5X_MODE_REVERSE;
+  {
+    u64 bl = (!rev && lane < I.n) ? (u64)(16u - S.rr[lane]) << (4 * lane) : 0ull;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) bl |= (u64)__shfl_xor((long long)bl, d, 64);
+    biasm = bl;
+  }
+  u32 tpi = 0, tR = 1, tml = 0, teb = 0;
+  if (lane < ntok) {
+    const u32 d = S.tok[lane];
+    tpi = d >> 16;
+    teb = d & 0xFFFFu;
+    tR = tpi ? (rev ? 2u : (u32)S.rr[tpi - 1]) : 1u;
+    for (u32 v = 0; v < tR; v++) tml = max(tml, S.ent[teb + v].w >> 24);
+  }
+  u32 np = 0, pe = 0, k = 0;
+  u32 pk0 = 0, pk1 = 0, psrc = 0, pR = 0, pE = 0, pbase = 0, pns = 0, pml = 0;  // lane p: piece p
+  while (k < ntok) {
+    u32 k1 = k, ns = 0, E = 1, ml = 0;
+    u32 s0 = 0, s1 = 0, s2 = 0, R0 = 1, R1 = 1, R2 = 1;
+    while (k1 < ntok) {
+      const u32 pi = (u32)__builtin_amdgcn_readlane((int)tpi, (int)k1);
+      const u32 R = (u32)__builtin_amdgcn_readlane((int)tR, (int)k1);
+      const u32 mlk = (u32)__builtin_amdgcn_readlane((int)tml, (int)k1);
+      const bool known = pi && ((ns > 0 && s0 == pi) || (ns > 1 && s1 == pi) || (ns > 2 && s2 == pi));
+      const bool add = pi && !known;
+      const u32 E2 = add ? E * R : E, ns2 = ns + (add ? 1u : 0u);
+      if (k1 > k && (ml + mlk > 15u || ns2 > 3u || E2 > MF_EMAX || pe + E2 > MF_NPE - 1u)) break;
+      if (add) {
+        if (ns == 0) { s0 = pi; R0 = R; }
+        else if (ns == 1) { s1 = pi; R1 = R; }
+        else { s2 = pi; R2 = R; }
+      }
+      ns = ns2;
+      E = E2;
+      ml += mlk;
+      k1++;
+    }
+    const bool multi = k1 > k + 1;
+    const u32 base = multi ? MP_NE + pe : (u32)__builtin_amdgcn_readlane((int)teb, (int)k);
+    if (lane == np) {
+      pk0 = k; pk1 = k1; psrc = s0 | (s1 << 8) | (s2 << 16); pR = R0 | (R1 << 8) | (R2 << 16);
+      pE = multi ? E : 0u; pbase = base; pns = ns; pml = ml;
+    }
+    if (multi) pe += E;
+    np++;
+    k = k1;
+  }
+  if (lane < np) {
+    const u32 mk = rev ? 1u : 15u;
+    const u32 s0 = psrc & 255u, s1 = (psrc >> 8) & 255u, s2 = psrc >> 16;
+    const u32 R0 = pR & 255u, R1 = (pR >> 8) & 255u, R2 = pR >> 16;
+    auto sh = [&](u32 src) -> u32 { return src ? (rev ? src - 1u : 4u * (src - 1u)) : 0u; };
+    const u32 st0 = pns > 0 ? 1u : 0u, st1 = pns > 1 ? R0 : 0u, st2 = pns > 2 ? R0 * R1 : 0u;
+    int b = (int)pbase;
+    if (!rev) b -= (int)((16u - R0) * st0 + (16u - R1) * st1 + (16u - R2) * st2);
+    S.pdesc[lane] = make_uint4((u32)b, sh(s0) | (sh(s1) << 8) | (sh(s2) << 16) | (mk << 24),
+                               st0 | (st1 << 8) | (st2 << 16), pns | (fx8_slots(pml) << 8));
+  }
+  // the multi-token pieces' entries: lane = entry g of [0, pe)
+  for (u32 g0 = 0; g0 < pe; g0 += 64) {
+    const u32 g = g0 + lane;
+    u32 p = 0;
+    for (u32 q = 0; q < np; q++) {
+      const u32 bq = (u32)__builtin_amdgcn_readlane((int)pbase, (int)q) - MP_NE;
+      const u32 eq = (u32)__builtin_amdgcn_readlane((int)pE, (int)q);
+      p = (eq && g >= bq && g < bq + eq) ? q : p;
+    }
+    const u32 k0 = (u32)__shfl((int)pk0, (int)p), k1 = (u32)__shfl((int)pk1, (int)p);
+    const u32 src = (u32)__shfl((int)psrc, (int)p), Rp = (u32)__shfl((int)pR, (int)p);
+    const u32 e = g - ((u32)__shfl((int)pbase, (int)p) - MP_NE);
+    if (g < pe) {
+      const u32 R0 = Rp & 255u, R1 = (Rp >> 8) & 255u;
+      const u32 s0 = src & 255u, s1 = (src >> 8) & 255u;
+      const u32 d0 = e % R0, d1 = (e / R0) % R1, d2 = e / (R0 * R1);
+      u64 lo = 0, hi = 0;
+      u32 off = 0;
+      for (u32 kk = k0; kk < k1; kk++) {
+        const u32 d = S.tok[kk], pi = d >> 16;
+        const u32 dg = !pi ? 0u : pi == s0 ? d0 : pi == s1 ? d1 : d2;
+        m_cat(lo, hi, off, S.ent[(d & 0xFFFFu) + dg]);
+      }
+      S.ent[MP_NE + g] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, ((u32)(hi >> 32) & 0xFFFFFFu) | (off << 24));
+      S.elen[MP_NE + g] = (uint8_t)off;
+    }
+  }
+  if (lane == 0) {  // the empty entry (leaves past a run's end)
+    S.ent[MF_ZE] = make_uint4(0, 0, 0, 0);
+    S.elen[MF_ZE] = 0;
   }
   m_sync<SL>();
   return np;
 }
 
 __device__ __forceinline__ u32 m_piece_ix(const uint4 pd, u64 sel) {
-  const u32 mk = pd.y >> 24;
+  const u32 mk = pd.y >> 24;  // (pd.w: sources | fx8 slots << 8)
   const u32 f0 = (u32)(sel >> (pd.y & 63u)) & mk, f1 = (u32)(sel >> ((pd.y >> 8) & 63u)) & mk,
             f2 = (u32)(sel >> ((pd.y >> 16) & 63u)) & mk;
   return pd.x + f0 * (pd.z & 255u) + f1 * ((pd.z >> 8) & 255u) + f2 * ((pd.z >> 16) & 255u);
@@ -1079,12 +1205,11 @@ __device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64
     u32 clen[MF_K], len = 0;
 #pragma unroll
     for (int c = 0; c < MF_K; c++) clen[c] = (u32)c < nc ? (rev ? Lc : 1u) : 0u;
-    if (!rev) {
+    if (!rev) {  // (leaves past the run read the empty entry: no per-leaf branches)
       for (u32 p = 0; p < np; p++) {
         const uint4 pd = S.pdesc[p];
 #pragma unroll
-        for (int c = 0; c < MF_K; c++)
-          if ((u32)c < nc) clen[c] += S.elen[m_piece_ix(pd, sel[c])];
+        for (int c = 0; c < MF_K; c++) clen[c] += S.elen[(u32)c < nc ? m_piece_ix(pd, sel[c]) : MF_ZE];
       }
     }
 #pragma unroll
@@ -1095,19 +1220,19 @@ __device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64
     const u32 nact = (u32)__popcll(__ballot(fit));
     const u32 tot = nact ? (u32)__builtin_amdgcn_readlane((int)incl, (int)nact - 1) : 0u;
     if (fit) {
-      u32 P[MF_K], sink = 0;
-      P[0] = ringa + used + incl - len;
+      // fx8_put: the piece's dword count from its longest entry (uniform, scalar branches)
+      u32 P1[MF_K];
+      P1[0] = ringa + used + incl - len - 1u;
 #pragma unroll
-      for (int c = 1; c < MF_K; c++) P[c] = P[c - 1] + clen[c - 1];
+      for (int c = 1; c < MF_K; c++) P1[c] = P1[c - 1] + clen[c - 1];
       for (u32 p = 0; p < np; p++) {
         const uint4 pd = S.pdesc[p];
+        const u32 nsl = (u32)__builtin_amdgcn_readfirstlane((int)(pd.w >> 8));
 #pragma unroll
-        for (int c = 0; c < MF_K; c++)
-          if ((u32)c < nc) fx7_put(S.ent[m_piece_ix(pd, sel[c])], P[c], sink);
+        for (int c = 0; c < MF_K; c++) fx8_put(S.ent[(u32)c < nc ? m_piece_ix(pd, sel[c]) : MF_ZE], P1[c], nsl);
       }
 #pragma unroll
-      for (int c = 0; c < MF_K; c++)
-        if ((u32)c < nc) fx7_put(nl, P[c], sink);
+      for (int c = 0; c < MF_K; c++) fx8_put((u32)c < nc ? nl : make_uint4(0, 0, 0, 0), P1[c], 2u);
     }
     pos += tot;
     rr += nact;
@@ -1326,16 +1451,16 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
   if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
   u32 err = 0, ntok = 0;
   if constexpr (SL::FAST) {  // op 1 of MI_FAST items (the only route here)
-    ntok = op == 1 ? m_pos_setup(S, T, I, a.mode) : 0u;
+    ntok = op == 1 ? ((MF_ABL & 4) ? 1u : m_pos_setup(S, T, I, a.mode)) : 0u;
     if (!ntok) {
       err |= M_ERR_STATE;
     } else {
-      u64 biasm;
-      const u32 np = m_piece_setup(S, I, a.mode, ntok, biasm);
+      u64 biasm = 0;
+      const u32 np = (MF_ABL & 2) ? 0u : m_piece_setup(S, I, a.mode, ntok, biasm);
       const u64 rb = a.cand_begin > cw0 ? a.cand_begin - cw0 : 0;
       const u64 re = a.cand_end - cw0 < t0 + nc ? a.cand_end - cw0 : t0 + nc;  // (cand_end > cw0 here)
       const u64 tb = rb > t0 ? rb : t0;
-      if (a.cand_end > cw0 && tb < re)
+      if (a.cand_end > cw0 && tb < re && !(MF_ABL & 1))
         m_fast_expand(S, I, a, tb, re, tb == t0 ? a.seg_boff[i] - a.out_base : 0, np, biasm, err);
     }
     m_err(a.err, m_wave_or(err));
