@@ -93,7 +93,7 @@ constexpr u32 MF_PMAX = A5X_M_LMAX + 2;
 #define MF_RING 4096         // the piece engine's ring (runs that do not fit wait a round)
 #endif
 #ifndef MF_K
-#define MF_K 4               // leaves per lane run (odometer steps between them)
+#define MF_K 2               // leaves per lane run (odometer steps between them; C5: 2 < 4 < 8)
 #endif
 #ifndef MF_OFF
 #define MF_OFF 0             // 1: radix words stay on the token ring (A/B builds)
@@ -640,8 +640,10 @@ __device__ u32 m_rpos_setup(SL& S, const MT& T, const MInfo& I) {
 
 // Tokens and entries of the word set up in S (after m_setup): returns the token count,
 // or 0 when the word is not positional (byte builder path).
+// check = false: the word is known positional (its item was routed MI_FAST by the
+// length pass, which ran the checks): the per-value checks are skipped.
 template <class SL>
-__device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode) {
+__device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode, bool check = true) {
   if (mode == A5X_MODE_REVERSE) return m_rpos_setup(S, T, I);
   const u32 lane = m_lane(), n = I.n, L = I.L;
   if (n == 0 || n > MP_PMAX || L > A5X_M_LMAX) return 0;
@@ -650,9 +652,10 @@ __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode) {
     const A5xMKey K = T.keys[S.pat[lane]];
     const uint8_t* kp = T.blob + K.key_off;
     const u32 nv = mode == A5X_MODE_SUBALL ? K.nvals : (K.nvals ? 1u : 0u);
-    ok = K.klen >= 1 && K.klen <= 4 && m_rune_len(kp, K.klen) == K.klen && (K.klen > 1 || kp[0] < 0x80u) &&
-         nv <= MP_VMAX;
-    for (u32 v = 0; ok && v < nv; v++) {
+    if (check)
+      ok = K.klen >= 1 && K.klen <= 4 && m_rune_len(kp, K.klen) == K.klen && (K.klen > 1 || kp[0] < 0x80u) &&
+           nv <= MP_VMAX;
+    for (u32 v = 0; check && ok && v < nv; v++) {
       const A5xMVal V = T.vals[K.val_base + v];
       const uint8_t* vp = T.blob + V.off;
       ok = V.len <= 15 && m_valid_utf8(vp, V.len);
@@ -1451,7 +1454,7 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
   if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
   u32 err = 0, ntok = 0;
   if constexpr (SL::FAST) {  // op 1 of MI_FAST items (the only route here)
-    ntok = op == 1 ? ((MF_ABL & 4) ? 1u : m_pos_setup(S, T, I, a.mode)) : 0u;
+    ntok = op == 1 ? ((MF_ABL & 4) ? 1u : m_pos_setup(S, T, I, a.mode, false)) : 0u;
     if (!ntok) {
       err |= M_ERR_STATE;
     } else {
@@ -1607,6 +1610,11 @@ __global__ void __launch_bounds__(256) k_mode_wordbytes(const u64* seg_off, cons
 }
 
 inline u32 m_grid(u64 n, u32 cap) { return (u32)(n < 1 ? 1 : (n < cap ? n : cap)); }
+// word / item kernels: every workgroup stages the mode table into LDS once, so the grid is
+// a few workgroups per CU looping over the work (262144 groups re-read the table 262144 times)
+#ifndef M_GRID_MAX
+#define M_GRID_MAX (1u << 18)
+#endif
 
 }  // namespace
 
@@ -1617,7 +1625,7 @@ static size_t m_lds(uint32_t mtab_bytes) { return sizeof(SL) + ((mtab_bytes + 15
 uint64_t a5x_mode_gslot_bytes() { return (sizeof(MLdsG) + 255) & ~(size_t)255; }
 
 hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st) {
-  hipLaunchKernelGGL(k_mode_count, dim3(m_grid(L.nw, 1u << 18)), dim3(64), m_lds<MLdsC>(L.mtab_bytes), st, L);
+  hipLaunchKernelGGL(k_mode_count, dim3(m_grid(L.nw, M_GRID_MAX)), dim3(64), m_lds<MLdsC>(L.mtab_bytes), st, L);
   return hipGetLastError();
 }
 
@@ -1628,7 +1636,7 @@ hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st) {
 
 hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st) {
   if (L.item_end <= L.item_begin) return hipSuccess;
-  const dim3 g(m_grid(L.item_end - L.item_begin, 1u << 18));
+  const dim3 g(m_grid(L.item_end - L.item_begin, M_GRID_MAX));
   if (op == 0) {
     hipLaunchKernelGGL(k_mode_items_len, g, dim3(64), m_lds<MLdsC>(L.mtab_bytes), st, L);
     if (L.mode != A5X_MODE_REVERSE)
