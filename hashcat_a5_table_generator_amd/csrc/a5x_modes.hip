@@ -284,8 +284,10 @@ __device__ u32 m_replace_all(const uint8_t* src, u32 n, const uint8_t* p, u32 pl
 
 // Per-word setup (wave-uniform result): word -> LDS, the pattern / position list,
 // the DP table and the count.
+// dp = false: a radix word's count in closed form, no DP table (callers that never
+// unrank a leaf through it: k_mode_count)
 template <class SL>
-__device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
+__device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w, bool dp = true) {
   const u32 lane = m_lane();
   MInfo I;
   I.L = I.n = I.cmin = I.cmax = I.cols = 0;
@@ -393,13 +395,14 @@ __device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
     rad = P < (1ull << 27);
     rcount = rad ? P - cmin : 0;
   }
-  if constexpr (SL::FAST) {  // piece layout: radix words only, no DP table
+  // (the limit holds for every layout, so that every kernel agrees on the word)
+  if ((n + 1) * cols > A5X_M_DPMAX) { I.bad = M_ERR_LIMIT; return I; }
+  if (SL::FAST || (!dp && rad)) {  // (the piece layout has no DP table: radix words only)
     if (!rad) { I.bad = M_ERR_STATE; return I; }
     I.radix = 1;
     I.count = rcount;
     return I;
   }
-  if ((n + 1) * cols > A5X_M_DPMAX) { I.bad = M_ERR_LIMIT; return I; }
   u64* D = S.dp;
   const u32 c = lane;
   if (c < cols) D[n * cols + c] = c == 0 ? 1ull : 0ull;
@@ -1334,7 +1337,7 @@ extern __shared__ __attribute__((aligned(16))) uint8_t m_dyn[];
 // per-word count, segments and flags of a set-up word
 template <class SL>
 __device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
-  const MInfo I = m_setup(S, T, a, w);
+  const MInfo I = m_setup(S, T, a, w, false);
   const bool gw = I.bad == M_ERR_GWORD;  // (LDS pass only) routed to mode pass G
   if (m_lane() == 0) {
     const u64 cnt = I.bad ? 0 : I.count;
