@@ -9,6 +9,10 @@
 #pragma once
 #include <stdint.h>
 
+#ifndef FX_MASKOR
+#define FX_MASKOR 0  // 1: exec-mask each ds_or slot to the lanes whose piece reaches it
+#endif
+
 // LDS byte addresses as plain uint32_t (ds_* instructions take a VGPR address + an offset)
 typedef __attribute__((address_space(3))) uint32_t fx6_lds32;
 __device__ __forceinline__ uint32_t fx6_addr(const void* p) {
@@ -42,6 +46,20 @@ __device__ __forceinline__ void fx7_put(const uint4 e, uint32_t& P, uint32_t& si
     if constexpr (NOOR) sink ^= v + a;
     else fx7_or(a, v);
   };
+#if FX_MASKOR
+  // Only the lanes whose piece reaches a slot take part in its ds_or: masked lanes do not
+  // enter the bank arbitration, so the random-address conflicts of a slot that few lanes
+  // need shrink (ring ORs land on data-dependent addresses: ~3.5-way per 32-lane group).
+  if (l) put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
+  if (t > 4u) put(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
+  if (__builtin_amdgcn_ballot_w64(t > 8u)) {
+    if (t > 8u) put(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
+    if (__builtin_amdgcn_ballot_w64(t > 12u)) {
+      if (t > 12u) put(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
+      if (t > 16u) put(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
+    }
+  }
+#else
   put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
   put(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
   if (__builtin_amdgcn_ballot_w64(t > 8u)) {  // pieces reaching a third dword (wave-uniform)
@@ -51,6 +69,7 @@ __device__ __forceinline__ void fx7_put(const uint4 e, uint32_t& P, uint32_t& si
       if (__builtin_amdgcn_ballot_w64(t > 16u)) put(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
     }
   }
+#endif
   P += l;
 }
 
