@@ -113,6 +113,7 @@ struct a5x_ctx {
   DevBuf<uint32_t> flags, defer, chunk_w0, slow_list, big_list, roff, cplx;
   DevBuf<uint64_t> segs;  // slow / BIG segment items
   DevBuf<uint32_t> glob;  // pass G word list (words beyond the pass-B LDS budget)
+  DevBuf<uint32_t> m_cl;  // -s / -s -r: words k_mode_count_thread leaves to k_mode_count
   uint8_t* gscr = nullptr;  // pass G scratch: A5X_G_SLOTS x a5x_gslot_bytes(), allocated on first use
   DevBuf<uint64_t> rec;  // FAST plan records (keyspace tiles of FW_TILE_REC u64)
   uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] nslow, [4] cplx_n, [5] slow segs, [6] BIG segs, [16..31] guard record
@@ -376,6 +377,7 @@ struct Batch {  // device-side per-batch state after keyspace
   uint64_t total_cands = 0, total_bytes = 0;
   uint32_t nbig = 0, nslow = 0;
   uint32_t nglob = 0;  // pass G words (on the BIG list, expanded by k_expand_g)
+  bool rfast = false;  // -r: FAST words probed by k_keyspace_thread (expanded by k_expand_fast)
   const uint64_t* cand_off = nullptr;
   const uint64_t* byte_off = nullptr;
 };
@@ -529,6 +531,47 @@ int compile_mtable(a5x_ctx* c) {
     }
     keys.push_back(K);
   }
+  // Static per-key facts for the lane-per-word -s / -s -r keyspace (k_mode_count_thread):
+  // bit 0 / 1 = the key passes m_pos_setup's positional checks in -s / -s -r for ANY
+  // word (one codepoint, ASCII if one byte; <= 14 values (-s) or subs[0] (-s -r) of <= 15
+  // valid UTF-8 bytes containing no key at all -- a superset of "no later pattern");
+  // bits 8-19 / 20-31 = sum over those values of (len - klen) + 2048.
+  {
+    auto valid_utf8 = [](const std::string& v) {
+      for (size_t i = 0; i < v.size();) {
+        int sz = 0;
+        const int r = a5x::gosem::decode_rune((const uint8_t*)v.data() + i, v.size() - i, &sz);
+        if (r == a5x::gosem::kRuneError && sz == 1) return false;
+        i += (size_t)sz;
+      }
+      return true;
+    };
+    auto has_key = [&](const std::string& v) {
+      for (uint32_t j : order)
+        if (!t.keys[j].empty() && v.find(t.keys[j]) != std::string::npos) return true;
+      return false;
+    };
+    const bool small = order.size() <= 1024;  // (the containment test is O(keys^2))
+    for (size_t i = 0; i < order.size(); i++) {
+      const std::string& k = t.keys[order[i]];
+      const auto& vs = t.vals[order[i]];
+      int sz = 0;
+      const int r0 = k.empty() ? 0 : a5x::gosem::decode_rune((const uint8_t*)k.data(), k.size(), &sz);
+      const bool cp = small && k.size() >= 1 && k.size() <= 4 && sz == (int)k.size() &&
+                      !(r0 == a5x::gosem::kRuneError && sz == 1) && !(sz == 1 && (uint8_t)k[0] >= 0x80);
+      auto vok = [&](const std::string& v) { return v.size() <= 15 && valid_utf8(v) && !has_key(v); };
+      bool ok2 = cp && vs.size() <= 14, ok3 = cp;
+      int d2 = 0, d3 = 0;
+      for (size_t v = 0; v < vs.size(); v++) {
+        const bool o = vok(vs[v]);
+        ok2 = ok2 && o;
+        if (v == 0) { ok3 = ok3 && o; d3 = (int)vs[0].size() - (int)k.size(); }
+        d2 += (int)vs[v].size() - (int)k.size();
+      }
+      keys[i].pad = (ok2 ? 1u : 0u) | (ok3 ? 2u : 0u) | ((uint32_t)(d2 + 2048) & 0xFFFu) << 8 |
+                    ((uint32_t)(d3 + 2048) & 0xFFFu) << 20;
+    }
+  }
   bucket[0] = (uint16_t)has_empty;
   for (int b = 0; b < 256; b++) bucket[b + 1] += bucket[b];
   auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -576,9 +619,10 @@ int upload_mtable(a5x_ctx* c) {
 }
 
 A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode,
-                          int mn, int mx) {
+                          int mn, int mx, bool rfast = false) {
   A5xModeLaunch M;
   memset(&M, 0, sizeof M);
+  M.rfast = rfast ? 1 : 0;
   M.mtab = c->d_mtab; M.mtab_bytes = c->mtab_bytes; M.words = d_words; M.woff = d_woff; M.nw = nw;
   M.mode = mode; M.mn = mn; M.mx = mx; M.SEG = c->mseg;
   M.count = c->count.p; M.nseg = c->m_nseg.p; M.flags = c->flags.p;
@@ -628,6 +672,7 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   B->cand_off = d_cand_off;
   B->byte_off = d_byte_off;
   B->nbig = B->nslow = 0;
+  B->rfast = false;
   if (nw == 0) {
     HIPCHK(c, hipMemsetAsync(d_cand_off, 0, 8, st));
     HIPCHK(c, hipMemsetAsync(d_byte_off, 0, 8, st));
@@ -636,7 +681,46 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     c->m_items = 0;
     return A5X_OK;
   }
-  A5xModeLaunch M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx);
+  // -r words with pairwise disjoint positions whose subs[0] keep the key lengths go to the
+  // FAST path (a5x_kernels.hip r_unit): the default keyspace kernel probes them (count,
+  // bytes, plan record; flags & A5X_WF_FAST), k_mode_count and the length pass skip them,
+  // k_expand_fast (k_expand_fast_md5 / _ntlm in the fused digest) writes them beside the
+  // mode engine's items, so every path numbers a word's candidates the same way.
+  bool rfast = mode == A5X_MODE_REVERSE && mx >= 1 && mn <= 1 && !getenv("A5X_NO_RFAST");
+  if (rfast && upload_table(c) != A5X_OK) {  // (a table the default engine refuses: mode engine only)
+    rfast = false;
+    c->err.clear();
+  }
+  B->rfast = rfast;
+  if (rfast) {
+    if ((rc = grow(c, c->roff, nw + 1)) ||
+        (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC + 2)))
+      return rc;
+    A5xKsLaunch K;
+    memset(&K, 0, sizeof K);
+    K.table = c->d_table; K.table_bytes = c->table_bytes; K.words = d_words; K.woff = d_woff; K.nw = nw;
+    K.mn = mn; K.mx = mx; K.count = c->count.p; K.bytes = c->bytes.p; K.flags = c->flags.p;
+    K.err = c->d_scalars + 2; K.rec = c->rec.p; K.roff = c->roff.p;
+    K.rmode = 1; K.rcmin = mn > 0 ? 1u : 0u; K.rnseg = c->m_nseg.p; K.rseg = c->mseg;
+    if ((rc = grow(c, c->m_cl, nw + 1))) return rc;
+    K.defer_list = c->m_cl.p; K.defer_n = c->d_scalars + 12;
+    HIPCHK(c, a5x_launch_keyspace(K, st));
+  }
+  A5xModeLaunch M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx, rfast);
+  if (rfast) {  // k_mode_count only over the words the probe left to the mode engine
+    M.cl_list = c->m_cl.p;
+    M.cl_n = c->d_scalars + 12;
+  }
+  // -s / -s -r: radix positional words counted lane per word (k_mode_count_thread), the
+  // wave kernel only for the words it lists (an empty key makes "" a pattern of every word)
+  const bool mct = (mode == A5X_MODE_SUBALL || mode == A5X_MODE_SUBALL_REVERSE) && mx >= 0 &&
+                   !((const A5xMHdr*)c->mblob.data())->has_empty && !getenv("A5X_NO_MCT");
+  if (mct) {
+    if ((rc = grow(c, c->m_cl, nw + 1))) return rc;
+    M.cl_list = c->m_cl.p;
+    M.cl_n = c->d_scalars + 12;
+    HIPCHK(c, a5x_launch_mode_count_thread(M, st));
+  }
   HIPCHK(c, a5x_launch_mode_count(M, st));
   HIPCHK(c, a5x_launch_scan(c->count.p, c->m_nseg.p, nw, d_cand_off, c->m_seg_off.p, c->scan_tmp.p,
                             c->d_scalars + 2, st));
@@ -651,7 +735,7 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
       HIPCHK(c, hipMalloc((void**)&c->mgscr, (size_t)A5X_G_SLOTS * a5x_mode_gslot_bytes()));
     }
     c->m_nglob = c->h_scalars[7];
-    M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx);
+    M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx, rfast);
     HIPCHK(c, a5x_launch_mode_count_g(M, st));
     HIPCHK(c, a5x_launch_scan(c->count.p, c->m_nseg.p, nw, d_cand_off, c->m_seg_off.p, c->scan_tmp.p,
                               c->d_scalars + 2, st));
@@ -688,10 +772,15 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
       (rc = grow(c, c->m_seg_boff, items + 1)) || (rc = grow(c, c->m_tmp, items + 1)) ||
       (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(items + 1) + 16)))
     return rc;
-  M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx);
+  M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx, rfast);
   M.cand_off = d_cand_off;
   M.item_begin = 0;
   M.item_end = items;
+  if (rfast && B->total_cands) {  // chunk -> first word map for k_expand_fast
+    const uint64_t nchunks = (B->total_cands + c->chunk - 1) / c->chunk;
+    if ((rc = grow(c, c->chunk_w0, nchunks + 1))) return rc;
+    HIPCHK(c, a5x_launch_plan(d_cand_off, nw, c->chunk, c->chunk_w0.p, st));
+  }
   if (items) HIPCHK(c, a5x_launch_plan(c->m_seg_off.p, nw, 1, c->m_item_w.p, st));
   if (!lengths) {
     HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 16, hipMemcpyDeviceToHost, st));
@@ -764,7 +853,7 @@ int job_locate(a5x_ctx* c, const Job& J, const std::vector<uint64_t>& q, std::ve
   if ((rc = grow(c, c->loc_q, n)) || (rc = grow(c, c->loc_r, 3 * (size_t)n))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->loc_q.p, q.data(), 8 * (size_t)n, hipMemcpyHostToDevice, J.st));
   if (J.mode != A5X_MODE_DEFAULT) {
-    A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx);
+    A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, J.B.rfast);
     M.cand_off = J.B.cand_off;
     HIPCHK(c, a5x_launch_mode_locate(M, c->loc_q.p, n, c->loc_r.p, J.st));
     std::vector<uint64_t> t(3 * (size_t)n);
@@ -858,7 +947,7 @@ int job_launch(a5x_ctx* c, const Job& J, const Range& R, uint8_t* d_out, uint64_
     return fail(c, A5X_E_CAPACITY, "output needs %llu bytes, buffer has %llu", (unsigned long long)(R.b1 - R.b0),
                 (unsigned long long)out_cap);
   if (J.mode != A5X_MODE_DEFAULT) {
-    A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx);
+    A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, J.B.rfast);
     M.cand_off = J.B.cand_off;
     M.item_begin = R.i0;
     M.item_end = R.i1;
@@ -867,7 +956,27 @@ int job_launch(a5x_ctx* c, const Job& J, const Range& R, uint8_t* d_out, uint64_
     M.out = d_out;
     M.out_base = R.b0;
     M.out_cap = out_cap;
-    HIPCHK(c, a5x_launch_mode_items(M, 1, J.st));
+    if (!J.B.rfast) {
+      HIPCHK(c, a5x_launch_mode_items(M, 1, J.st));
+      return A5X_OK;
+    }
+    // -r FAST words: k_expand_fast on the job stream, the mode engine's items (disjoint
+    // output bytes) on the side stream, joined before the range completes
+    if (!c->sstream) HIPCHK(c, hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking));
+    if (!c->ev_fork) HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    if (!c->ev_join) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_fork, J.st));
+    HIPCHK(c, hipStreamWaitEvent(c->sstream, c->ev_fork, 0));
+    HIPCHK(c, a5x_launch_mode_items(M, 1, c->sstream));
+    A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
+    E.cand_begin = R.cb;
+    E.cand_end = R.ce;
+    E.out = d_out;
+    E.out_base = R.b0;
+    E.out_cap = out_cap;
+    HIPCHK(c, a5x_launch_expand(E, 0, J.st));
+    HIPCHK(c, hipEventRecord(c->ev_join, c->sstream));
+    HIPCHK(c, hipStreamWaitEvent(J.st, c->ev_join, 0));
     return A5X_OK;
   }
   const Batch& B = J.B;
@@ -995,7 +1104,7 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
     uint64_t nh = 0;
     float ms = 0;
     for (;;) {
-      A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx);
+      A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, J.B.rfast);
       const A5xDigLaunch D = dig_launch(c);
       M.cand_off = J.B.cand_off;
       M.item_begin = 0;
@@ -1007,6 +1116,15 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
       HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
       HIPCHK(c, hipEventRecord(c->ev[1], J.st));
       HIPCHK(c, a5x_launch_mode_items(M, 2, J.st));
+      if (J.B.rfast && tc) {  // -r FAST words: hashed in k_expand_fast_md5 / _ntlm's ring
+        A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
+        E.cand_begin = 0;
+        E.cand_end = tc;
+        E.dg_bitmap = D.bitmap; E.dg_bm_mask = D.bm_mask; E.dg_has_zero = D.has_zero_target;
+        E.dg_table = D.table; E.dg_tmask = D.tmask;
+        E.dg_hits = c->dg_hits.p; E.dg_hit_cap = (uint32_t)dev_hits; E.dg_nhits = c->d_scalars + 8;
+        HIPCHK(c, a5x_launch_expand(E, c->t_algo == A5X_ALGO_MD5 ? 3 : 5, J.st));
+      }
       HIPCHK(c, hipEventRecord(c->ev[2], J.st));
       HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, J.st));
       HIPCHK(c, hipStreamSynchronize(J.st));

@@ -203,7 +203,29 @@ struct KsArgs {
   u32* glob_list;  // pass G words (k_keyspace_wave -> k_keyspace_g)
   u32* glob_n;
   uint8_t* gscr;   // pass G scratch slots
+  int rmode;       // 1: -r FAST probe (k_keyspace_thread only; r_unit below): the other
+                   // words are appended to defer_list (for k_mode_count)
+  u32 rcmin;       // -r: max(min, 0) (0 or 1 for a FAST word)
+  u64* rnseg;      // -r: mode-engine items per FAST word (ceil(count / rseg))
+  u64 rseg;
 };
+
+// -r (processWordReverse, main.go:208-261) on the FAST path.  For a word whose match
+// positions are pairwise disjoint -- exactly the lone units of the position-synchronous
+// walk -- and whose every key's subs[0] keeps the key's length (the running offset of
+// main.go:251-256 then moves nothing), candidate = any subset of the positions replaced
+// by subs[0]: a unit of 2 choices (choice 0 = the key, choice 1 = subs[0], a5x_format.h)
+// per position.  The size window [min, max] cuts nothing when min <= 1 <= #positions <=
+// max; with min = 0 the all-keep word is candidate P - 1 of the FAST numbering
+// (index P wraps to the all-zero digits), so count = P - rcmin.  Every candidate has
+// L + 1 bytes.  Returns false when the unit does not qualify (the mode engine takes
+// the word).
+__device__ __forceinline__ bool r_unit(const Tab& T, Unit& U) {
+  const A5xKey key = T.keys[U.key];
+  if (key.nvals < 1 || T.ch[key.choice_base + 1].len != key.klen) return false;
+  U.R = 2; U.ml = key.klen; U.mnl = key.klen; U.spos = 0; U.sneg = 0; U.maxd = 0;
+  return true;
+}
 
 // Append the lanes with pred to list[*ctr ...] (one atomic per wave); returns the
 // lane's slot (valid where pred).  Every lane of the wave must call it.
@@ -290,7 +312,7 @@ __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const
 #endif
 template <bool COUNT, class PL>
 __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 Lmax, u32 bmax, const Tab& T,
-                                         PL& pl, CountAcc& A, bool& cplx, uint16_t* ulog = nullptr,
+                                         PL& pl, CountAcc& A, bool& cplx, bool rm, uint16_t* ulog = nullptr,
                                          u32* nlog = nullptr) {
   u32 cur_end = 0;
   for (u32 q = 0; q < Lmax; q++) {
@@ -320,7 +342,9 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
       } else if (nm == 1 && !cplx) {
         Unit U;
         lone_unit(T, q, kk, U);
-        if (U.R > KS_GCAP) {
+        if (rm && !r_unit(T, U)) {
+          cplx = true;
+        } else if (U.R > KS_GCAP) {
           cplx = true;
         } else {
           if (COUNT) count_unit(A, U);
@@ -395,7 +419,8 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     NullSink ns;
     Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
     u32 nlog = 0;
-    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, ulog, &nlog);
+    const bool rm = a.rmode != 0;
+    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, rm, ulog, &nlog);
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
     u32 f = 0;
@@ -408,6 +433,14 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     }
     if (trivial) f = A5X_WF_RADIX | A5X_WF_FAST;
     if (longw) f = A5X_WF_DEFER;
+    if (rm) {
+      // -r FAST words (r_unit): count = 2^n - rcmin, L + 1 bytes each; every other word
+      // (flags 0) is left to the mode engine (k_mode_count skips the FAST ones)
+      const bool rf = psk && !cplx && (f & A5X_WF_FAST) && !(f & A5X_WF_DEFER) && A.nunits > 0 && C.count > 0;
+      f = rf ? f : 0u;
+      C.count = rf ? A.P - a.rcmin : 0ull;
+      C.bytes = rf ? C.count * (u64)(L + 1) : 0ull;
+    }
     // ---- record sizes -> exclusive workgroup scan ----
     const bool fast = psk && !cplx && (f & A5X_WF_FAST) && C.count > 0;
     const u32 rs = fast ? ff_rsize(f) : 0u;
@@ -434,11 +467,12 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
           const u32 e = ulog[i * 256u];
           Unit U;
           lone_unit(T, e >> 10, e & 1023u, U);
+          if (rm) (void)r_unit(T, U);  // (qualified in the count pass)
           pb.unit(U);
         }
       }
       const bool walk = build && !replay;
-      if (!(KS_ABL & 1)) psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2);
+      if (!(KS_ABL & 1)) psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2, rm);
       if (build && !(KS_ABL & 1)) {
         pb.finish(L);
         pb.pick_balanced();
@@ -449,8 +483,21 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       }
     }
     if (fast && !build) {
-      // the tile's record budget is spent: the slow path takes the word
-      f = C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
+      // the tile's record budget is spent: the slow path takes the word (-r: the mode engine)
+      f = rm ? 0u : C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
+    }
+    if (rm) {
+      const bool kept = valid && (f & A5X_WF_FAST) != 0;
+      if (valid) {
+        a.count[w] = kept ? C.count : 0ull;
+        a.bytes[w] = kept ? C.bytes : 0ull;
+        a.flags[w] = kept ? f : 0u;
+        a.rnseg[w] = kept ? (C.count + a.rseg - 1) / a.rseg : 0ull;
+      }
+      const u32 mi = wave_append(valid && !kept, a.defer_n);  // the mode engine's words
+      if (valid && !kept) a.defer_list[mi] = (u32)w;
+      __syncthreads();
+      continue;
     }
     // ---- lists (one atomic per wave each) and per-word results ----
     const u32 ci = wave_append(cplx, a.cplx_list ? a.cplx_n : a.defer_n);
@@ -2108,9 +2155,10 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   a.rec = L.rec; a.roff = L.roff;
   a.cplx_list = L.cplx_list; a.cplx_n = L.cplx_n; a.cplx_cap = L.cplx_cap; a.cplx_base = L.cplx_base;
   a.glob_list = L.glob_list; a.glob_n = L.glob_n; a.gscr = L.gscr;
+  a.rmode = L.rmode; a.rcmin = L.rcmin; a.rnseg = L.rnseg; a.rseg = L.rseg;
   hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || L.rmode) return e;  // -r FAST probe: k_keyspace_thread only
   hipLaunchKernelGGL(k_keyspace_cplx, dim3(L.defer_blocks), dim3(256),
                      ((L.table_bytes + 15u) & ~15u) + 2 * 256 * FW_UMAXR * 8 + 256 * KC_SLOT, st, a);
   e = hipGetLastError();

@@ -32,6 +32,11 @@ struct A5xKsLaunch {
   uint32_t* glob_n;
   uint8_t* gscr;        // pass G scratch: gslots x a5x_gslot_bytes() (ring zeroed)
   uint32_t gslots;
+  int rmode;            // 1: -r FAST probe (k_keyspace_thread only, a5x_kernels.hip r_unit);
+                        // the other words are listed in defer_list / defer_n
+  uint32_t rcmin;       // -r: max(min, 0)
+  uint64_t* rnseg;      // -r: per FAST word, ceil(count / rseg) mode-engine items
+  uint64_t rseg;
 };
 
 struct A5xHitRaw;
@@ -131,6 +136,13 @@ struct A5xModeLaunch {
   uint32_t* glob_n;
   uint8_t* gscr;
   uint32_t gslots;
+  // -r FAST words (flags & A5X_WF_FAST, set by the k_keyspace_thread -r probe): counted
+  // there, their items sized L + 1 per candidate and expanded by k_expand_fast
+  int rfast;
+  // -s / -s -r lane-per-word keyspace (k_mode_count_thread): the words it leaves to the
+  // wave kernel k_mode_count (cl_list null: k_mode_count takes every word)
+  uint32_t* cl_list;
+  uint32_t* cl_n;
   // fused digest (op 2): every candidate hashed where it is built and probed against the
   // target set; hits as (word, candidate in word) -- see A5xDigLaunch
   int dg_algo;
@@ -144,6 +156,9 @@ struct A5xModeLaunch {
 size_t a5x_mode_lds(uint32_t mtab_bytes);
 uint64_t a5x_mode_gslot_bytes();
 hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st);
+// -s / -s -r: radix positional words counted lane per word; the others listed for
+// a5x_launch_mode_count (which then runs over L.cl_list)
+hipError_t a5x_launch_mode_count_thread(const A5xModeLaunch& L, hipStream_t st);
 hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st);
 // op 0: per-item output bytes (seg_bytes); op 1: expand items [item_begin, item_end);
 // op 2: fused digest of items [item_begin, item_end) (no length pass needed before it)

@@ -1337,6 +1337,10 @@ extern __shared__ __attribute__((aligned(16))) uint8_t m_dyn[];
 // per-word count, segments and flags of a set-up word
 template <class SL>
 __device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLaunch& a, u64 w) {
+  if (!SL::G && a.rfast && (a.flags[w] & A5X_WF_FAST)) {  // counted by the -r FAST probe
+    if (m_lane() == 0) a.nseg[w] = (a.count[w] + a.SEG - 1) / a.SEG;
+    return;
+  }
   const MInfo I = m_setup(S, T, a, w, false);
   const bool gw = I.bad == M_ERR_GWORD;  // (LDS pass only) routed to mode pass G
   if (m_lane() == 0) {
@@ -1365,11 +1369,117 @@ __device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLa
   m_err(a.err, gw ? 0u : I.bad);
 }
 
-// one wave per word: count, segments, per-word error flags
+// one wave per word (or per word of cl_list): count, segments, per-word error flags
 __global__ void __launch_bounds__(64) k_mode_count(A5xModeLaunch a) {
+  const u64 n = a.cl_list ? (u64)*a.cl_n : a.nw;
+  if (blockIdx.x >= n) return;  // (before staging the table)
   MLdsC& S = *(MLdsC*)m_dyn;
   const MT T = m_table(m_dyn + sizeof(MLdsC), a.mtab, a.mtab_bytes);
-  for (u64 w = blockIdx.x; w < a.nw; w += gridDim.x) m_count_word(S, T, a, w);
+  for (u64 i = blockIdx.x; i < n; i += gridDim.x) m_count_word(S, T, a, a.cl_list ? (u64)a.cl_list[i] : i);
+}
+
+// Lane-per-word keyspace of -s / -s -r (processWordSubstituteAll(Reverse), main.go:
+// 308-365, 369-440) for the words the wave kernel would find radix and positional:
+// every pattern present passes the static per-key checks of compile_mtable (A5xMKey.pad:
+// one codepoint, values of <= 15 valid UTF-8 bytes containing no key), <= MCT_PMAX
+// patterns, no size-window cut (min <= 1, max >= #patterns).  Then, with R_p = 1 +
+// (values of p) and P = prod R_p (< 2^27):  count = P - max(min, 0) and, each value of p
+// chosen in P / R_p leaves, bytes = count (L + 1) + sum_p occ_p (P / R_p) sum_v (|v| - |p|)
+// -- k_mode_count's results (m_setup + m_pos_setup + m_pos_prefix) for these words
+// without the wave's per-word setup.  Every other word goes to cl_list.
+#define MCT_SLOT 64  // per-lane word slot in LDS: words of <= MCT_SLOT - 8 bytes
+#define MCT_PMAX 16  // patterns per word (the positional engine's MP_PMAX)
+__global__ void __launch_bounds__(256) k_mode_count_thread(A5xModeLaunch a) {
+  const MT T = m_table(m_dyn, a.mtab, a.mtab_bytes);
+  const u32 tb = (a.mtab_bytes + 15u) & ~15u;
+  uint8_t* ws = m_dyn + tb + threadIdx.x * MCT_SLOT;
+  u32* pl = (u32*)(m_dyn + tb + blockDim.x * MCT_SLOT) + threadIdx.x;  // pattern j at pl[j * 256]
+  const bool sub = a.mode == A5X_MODE_SUBALL;
+  const u32 okbit = sub ? 1u : 2u, dsh = sub ? 8u : 20u;
+  const u32 cmin = a.mn > 0 ? (u32)a.mn : 0u;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const u64 nw_r = (a.nw + blockDim.x - 1) / blockDim.x * blockDim.x;  // every lane runs every pass
+  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nw_r; w += stride) {
+    const bool valid = w < a.nw;
+    u64 w0 = 0, L64 = 0;
+    if (valid) { w0 = a.woff[w]; L64 = a.woff[w + 1] - w0; }
+    bool dfr = !valid || L64 == 0 || L64 + 8 > MCT_SLOT || a.mx < 0 || cmin > 1;
+    const u32 L = dfr ? 0u : (u32)L64;
+    for (u32 q = 0; q < MCT_SLOT / 4; q++) {
+      u32 v = 0;
+      for (u32 b = 0; b < 4; b++)
+        if (4 * q + b < L) v |= (u32)a.words[w0 + 4 * q + b] << (8 * b);
+      ((u32*)ws)[q] = v;
+    }
+    u32 n = 0, nlit = 0, lend = 0;
+    for (u32 q = 0; q < L && !dfr; q++) {
+      const u32 b = ws[q], w4 = m_lds4(ws, q);
+      for (u32 k = T.bucket[b]; k < T.bucket[b + 1] && !dfr; k++) {
+        const A5xMKey K = T.keys[k];
+        if (q + K.klen > L) continue;
+        bool m;
+        if (K.klen <= 4) {
+          const u32 mask = K.klen == 4 ? ~0u : (1u << (8u * K.klen)) - 1u;
+          m = ((w4 ^ m_lds4(T.blob, K.key_off)) & mask) == 0;
+        } else {
+          m = true;
+          for (u32 i = 0; m && i < K.klen; i++) m = ws[q + i] == T.blob[K.key_off + i];
+        }
+        if (!m) continue;
+        if (!(K.pad & okbit)) { dfr = true; break; }  // (not one codepoint: never positional)
+        u32 j = 0;
+        while (j < n && (pl[j * 256] & 0xFFFFu) != k) j++;
+        if (j == n) {
+          if (n == MCT_PMAX) { dfr = true; break; }
+          pl[n * 256] = k | (1u << 16);
+          n++;
+        } else {
+          pl[j * 256] += 1u << 16;
+        }
+        nlit += (q - lend + 14u) / 15u;  // the literal run before this occurrence, in <= 15-byte chunks
+        lend = q + K.klen;               // (codepoint keys in a word never overlap)
+      }
+    }
+    nlit += (L - lend + 14u) / 15u;
+    if (n == 0 || (u32)a.mx < n) dfr = true;  // (no pattern, or a size-window cut: the DP)
+    u64 P = 1;
+    u32 npe = 0;
+    for (u32 j = 0; j < n && !dfr; j++) {
+      const A5xMKey K = T.keys[pl[j * 256] & 0xFFFFu];
+      const u32 R = 1u + (sub ? (u32)K.nvals : (K.nvals ? 1u : 0u));
+      P *= R;
+      npe += R;
+      if (P >= (1ull << 27)) dfr = true;
+    }
+    u64 count = 0, wb = ~0ull;
+    if (!dfr) {
+      count = P - cmin;
+      i64 extra = 0;
+      for (u32 j = 0; j < n; j++) {
+        const u32 e = pl[j * 256];
+        const A5xMKey K = T.keys[e & 0xFFFFu];
+        const u32 R = 1u + (sub ? (u32)K.nvals : (K.nvals ? 1u : 0u));
+        const int d = (int)((K.pad >> dsh) & 0xFFFu) - 2048;
+        extra += (i64)(e >> 16) * (i64)(P / R) * d;
+      }
+      const u64 bytes = (u64)((i64)(count * (u64)(L + 1)) + extra);
+      // m_pos_setup's table limits (entries of the patterns, then the literal chunks)
+      const bool pos = L <= A5X_M_LMAX && npe <= MP_NE && npe + nlit <= MP_NE;
+      if (pos && count > 0 && count <= a.SEG) wb = bytes | (MF_OFF ? 0ull : M_WB_FAST);
+      a.count[w] = count;
+      a.nseg[w] = (count + a.SEG - 1) / a.SEG;
+      a.flags[w] = 0;
+      a.wbytes[w] = wb;
+    }
+    const u64 dm = __ballot(dfr && valid);
+    if (dm) {
+      const u32 lane = m_lane(), leader = (u32)__builtin_ctzll(dm);
+      u32 base = 0;
+      if (lane == leader) base = atomicAdd(a.cl_n, (u32)__popcll(dm));
+      base = (u32)__shfl((int)base, (int)leader);
+      if (dfr && valid) a.cl_list[base + (u32)__popcll(dm & ((1ull << lane) - 1ull))] = (u32)w;
+    }
+  }
 }
 
 // mode pass G: one wave per HBM scratch slot over the listed words
@@ -1446,6 +1556,7 @@ constexpr uint8_t MI_POS = 1;       // positional: lengths done, ring expansion
 constexpr uint8_t MI_BUILD = 2;     // byte builder for the expansion, lengths done
 constexpr uint8_t MI_BUILD_LEN = 3; // byte builder for the lengths too
 constexpr uint8_t MI_FAST = 4;      // positional radix word: lengths done, piece engine
+constexpr uint8_t MI_SKIP = 5;      // -r FAST word (A5xModeLaunch::rfast): k_expand_fast writes it
 template <class SL>
 __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op) {
   const u64 w = a.item_w[i];
@@ -1520,16 +1631,34 @@ template <class SL>
 __device__ __forceinline__ void m_items(const A5xModeLaunch& a, int op, uint8_t route) {
   SL& S = *(SL*)m_dyn;
   const MT T = m_table(m_dyn + sizeof(SL), a.mtab, a.mtab_bytes);
-  for (u64 i = a.item_begin + blockIdx.x; i < a.item_end; i += gridDim.x) {
-    const u64 w = a.item_w[i];
-    if (a.flags[w] & A5X_WF_GLOB) continue;
-    if (route && a.item_fl[i] != route) continue;
-    if (op == 0 && !route && a.wbytes[w] != ~0ull) {  // sized by k_mode_count (one item)
-      const u64 wb = a.wbytes[w];
-      if (m_lane() == 0) { a.seg_bytes[i] = wb & ~M_WB_FAST; a.item_fl[i] = (wb & M_WB_FAST) ? MI_FAST : MI_POS; }
-      continue;
+  // 64 items per step, filtered lane-parallel (pass-G words, -r FAST words, other routes,
+  // closed-form sizes); the wave then runs the items that need it one after the other
+  const u32 lane = m_lane();
+  for (u64 b0 = a.item_begin + (u64)blockIdx.x * 64; b0 < a.item_end; b0 += (u64)gridDim.x * 64) {
+    const u64 i = b0 + lane;
+    bool take = false;
+    if (i < a.item_end) {
+      const u64 w = a.item_w[i];
+      const u32 fl = a.flags[w];
+      if (fl & A5X_WF_GLOB) {
+      } else if (a.rfast && (fl & A5X_WF_FAST)) {  // every candidate L + 1 bytes (r_unit)
+        if (op == 0 && !route) {
+          const u64 cnt = a.cand_off[w + 1] - a.cand_off[w], t0 = (i - a.seg_off[w]) * a.SEG;
+          const u64 nc = cnt - t0 < a.SEG ? cnt - t0 : a.SEG;
+          a.seg_bytes[i] = nc * (a.woff[w + 1] - a.woff[w] + 1);
+          a.item_fl[i] = MI_SKIP;
+        }
+      } else if (route) {
+        take = a.item_fl[i] == route;
+      } else if (op == 0 && a.wbytes[w] != ~0ull) {  // sized by k_mode_count (one item)
+        const u64 wb = a.wbytes[w];
+        a.seg_bytes[i] = wb & ~M_WB_FAST;
+        a.item_fl[i] = (wb & M_WB_FAST) ? MI_FAST : MI_POS;
+      } else {
+        take = true;
+      }
     }
-    m_item(S, T, a, i, op);
+    for (u64 m = __ballot(take); m; m &= m - 1) m_item(S, T, a, b0 + (u64)__builtin_ctzll(m), op);
   }
 }
 __global__ void __launch_bounds__(64) k_mode_items_len(A5xModeLaunch a) { m_items<MLdsC>(a, 0, 0); }
@@ -1632,6 +1761,12 @@ hipError_t a5x_launch_mode_count(const A5xModeLaunch& L, hipStream_t st) {
   return hipGetLastError();
 }
 
+hipError_t a5x_launch_mode_count_thread(const A5xModeLaunch& L, hipStream_t st) {
+  const size_t lds = ((L.mtab_bytes + 15u) & ~15u) + 256 * (MCT_SLOT + 4 * MCT_PMAX);
+  hipLaunchKernelGGL(k_mode_count_thread, dim3(m_grid((L.nw + 255) / 256, 2048)), dim3(256), lds, st, L);
+  return hipGetLastError();
+}
+
 hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st) {
   hipLaunchKernelGGL(k_mode_count_g, dim3(L.gslots), dim3(64), (L.mtab_bytes + 15u) & ~15u, st, L);
   return hipGetLastError();
@@ -1639,7 +1774,7 @@ hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st) {
 
 hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st) {
   if (L.item_end <= L.item_begin) return hipSuccess;
-  const dim3 g(m_grid(L.item_end - L.item_begin, M_GRID_MAX));
+  const dim3 g(m_grid((L.item_end - L.item_begin + 63) / 64, M_GRID_MAX));  // (m_items: 64 items a step)
   if (op == 0) {
     hipLaunchKernelGGL(k_mode_items_len, g, dim3(64), m_lds<MLdsC>(L.mtab_bytes), st, L);
     if (L.mode != A5X_MODE_REVERSE)

@@ -541,7 +541,8 @@ A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk, u32 balanced_cap 
 // pieces nb with FB_RMAX^nb >= P, then about P^(1 / nb) with slack for the
 // discreteness of the small pieces' R (slack8 in 1/8 units; 0: no balanced grouping).
 #ifndef FB_BAL_SLACK8
-#define FB_BAL_SLACK8 10
+#define FB_BAL_SLACK8 0  // off: measured on C3 (A/B, one box) the balanced grouping left the
+                         // expansion at 8.78-8.80 ms and cost the keyspace 0.54 ms (3.14 -> 3.68)
 #endif
 A5X_HD u32 fb_balanced_cap(u64 P, u32 slack8 = FB_BAL_SLACK8) {
   if (!slack8 || P <= FB_RMAX) return 0;
