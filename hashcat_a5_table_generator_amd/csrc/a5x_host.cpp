@@ -113,7 +113,7 @@ struct a5x_ctx {
   DevBuf<uint32_t> flags, defer, chunk_w0, slow_list, big_list, roff, cplx;
   DevBuf<uint64_t> segs;  // slow / BIG segment items
   DevBuf<uint32_t> glob;  // pass G word list (words beyond the pass-B LDS budget)
-  DevBuf<uint32_t> m_cl;  // -s / -s -r: words k_mode_count_thread leaves to k_mode_count
+  DevBuf<uint32_t> m_cl, m_cl2;  // mode-engine word lists (FAST probe -> k_mode_count_thread -> k_mode_count)
   uint8_t* gscr = nullptr;  // pass G scratch: A5X_G_SLOTS x a5x_gslot_bytes(), allocated on first use
   DevBuf<uint64_t> rec;  // FAST plan records (keyspace tiles of FW_TILE_REC u64)
   uint32_t* d_scalars = nullptr;  // [0] defer_n, [1] nbig, [2] err, [3] nslow, [4] cplx_n, [5] slow segs, [6] BIG segs, [16..31] guard record
@@ -218,6 +218,44 @@ int parse_table_into(a5x_ctx* c, Table& t, const uint8_t* d, size_t n) {
 }
 
 // Compile the map into the device table blob of a5x_format.h.
+// Static per-key facts of the -s / -s -r positional engines (k_mode_count_thread, the
+// -s / -s -r FAST probe of k_keyspace_thread): bit 0 / 1 = the key passes m_pos_setup's
+// positional checks in -s / -s -r for ANY word (one codepoint, ASCII if one byte; <= 14
+// values (-s) or subs[0] (-s -r) of <= 15 valid UTF-8 bytes containing no key at all -- a
+// superset of "no later pattern"); bits 8-19 / 20-31 = sum over those values of
+// (len - klen) + 2048.
+uint32_t key_pos_facts(const Table& t, const std::string& k, const std::vector<std::string>& vs) {
+  if (t.keys.size() > 1024) return 0;  // (the containment test is O(keys^2))
+  auto valid_utf8 = [](const std::string& v) {
+    for (size_t i = 0; i < v.size();) {
+      int sz = 0;
+      const int r = a5x::gosem::decode_rune((const uint8_t*)v.data() + i, v.size() - i, &sz);
+      if (r == a5x::gosem::kRuneError && sz == 1) return false;
+      i += (size_t)sz;
+    }
+    return true;
+  };
+  auto has_key = [&](const std::string& v) {
+    for (const std::string& kj : t.keys)
+      if (!kj.empty() && v.find(kj) != std::string::npos) return true;
+    return false;
+  };
+  int sz = 0;
+  const int r0 = k.empty() ? 0 : a5x::gosem::decode_rune((const uint8_t*)k.data(), k.size(), &sz);
+  const bool cp = k.size() >= 1 && k.size() <= 4 && sz == (int)k.size() && !(r0 == a5x::gosem::kRuneError && sz == 1) &&
+                  !(sz == 1 && (uint8_t)k[0] >= 0x80);
+  auto vok = [&](const std::string& v) { return v.size() <= 15 && valid_utf8(v) && !has_key(v); };
+  bool ok2 = cp && vs.size() <= 14, ok3 = cp;
+  int d2 = 0, d3 = 0;
+  for (size_t v = 0; v < vs.size(); v++) {
+    const bool o = vok(vs[v]);
+    ok2 = ok2 && o;
+    if (v == 0) { ok3 = ok3 && o; d3 = (int)vs[0].size() - (int)k.size(); }
+    d2 += (int)vs[v].size() - (int)k.size();
+  }
+  return (ok2 ? 1u : 0u) | (ok3 ? 2u : 0u) | ((uint32_t)(d2 + 2048) & 0xFFFu) << 8 | ((uint32_t)(d3 + 2048) & 0xFFFu) << 20;
+}
+
 int compile_table(a5x_ctx* c) {
   const Table& t = c->table;
   std::vector<uint32_t> order;
@@ -257,6 +295,7 @@ int compile_table(a5x_ctx* c) {
       return fail(c, A5X_E_UNSUPPORTED, "table key/value list too large for the device table");
     A5xKey key;
     memset(&key, 0, sizeof key);
+    key.pad0 = (uint16_t)(key_pos_facts(t, k, vs) & 3u);  // -s / -s -r FAST probe (r_unit)
     key.klen = (uint16_t)k.size();
     key.nvals = (uint16_t)vs.size();
     key.choice_base = (uint32_t)ch.size();
@@ -531,47 +570,9 @@ int compile_mtable(a5x_ctx* c) {
     }
     keys.push_back(K);
   }
-  // Static per-key facts for the lane-per-word -s / -s -r keyspace (k_mode_count_thread):
-  // bit 0 / 1 = the key passes m_pos_setup's positional checks in -s / -s -r for ANY
-  // word (one codepoint, ASCII if one byte; <= 14 values (-s) or subs[0] (-s -r) of <= 15
-  // valid UTF-8 bytes containing no key at all -- a superset of "no later pattern");
-  // bits 8-19 / 20-31 = sum over those values of (len - klen) + 2048.
-  {
-    auto valid_utf8 = [](const std::string& v) {
-      for (size_t i = 0; i < v.size();) {
-        int sz = 0;
-        const int r = a5x::gosem::decode_rune((const uint8_t*)v.data() + i, v.size() - i, &sz);
-        if (r == a5x::gosem::kRuneError && sz == 1) return false;
-        i += (size_t)sz;
-      }
-      return true;
-    };
-    auto has_key = [&](const std::string& v) {
-      for (uint32_t j : order)
-        if (!t.keys[j].empty() && v.find(t.keys[j]) != std::string::npos) return true;
-      return false;
-    };
-    const bool small = order.size() <= 1024;  // (the containment test is O(keys^2))
-    for (size_t i = 0; i < order.size(); i++) {
-      const std::string& k = t.keys[order[i]];
-      const auto& vs = t.vals[order[i]];
-      int sz = 0;
-      const int r0 = k.empty() ? 0 : a5x::gosem::decode_rune((const uint8_t*)k.data(), k.size(), &sz);
-      const bool cp = small && k.size() >= 1 && k.size() <= 4 && sz == (int)k.size() &&
-                      !(r0 == a5x::gosem::kRuneError && sz == 1) && !(sz == 1 && (uint8_t)k[0] >= 0x80);
-      auto vok = [&](const std::string& v) { return v.size() <= 15 && valid_utf8(v) && !has_key(v); };
-      bool ok2 = cp && vs.size() <= 14, ok3 = cp;
-      int d2 = 0, d3 = 0;
-      for (size_t v = 0; v < vs.size(); v++) {
-        const bool o = vok(vs[v]);
-        ok2 = ok2 && o;
-        if (v == 0) { ok3 = ok3 && o; d3 = (int)vs[0].size() - (int)k.size(); }
-        d2 += (int)vs[v].size() - (int)k.size();
-      }
-      keys[i].pad = (ok2 ? 1u : 0u) | (ok3 ? 2u : 0u) | ((uint32_t)(d2 + 2048) & 0xFFFu) << 8 |
-                    ((uint32_t)(d3 + 2048) & 0xFFFu) << 20;
-    }
-  }
+  // static per-key facts (key_pos_facts) for the lane-per-word -s / -s -r keyspace
+  for (size_t i = 0; i < order.size(); i++)
+    keys[i].pad = key_pos_facts(t, t.keys[order[i]], t.vals[order[i]]);
   bucket[0] = (uint16_t)has_empty;
   for (int b = 0; b < 256; b++) bucket[b + 1] += bucket[b];
   auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -623,6 +624,7 @@ A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_
   A5xModeLaunch M;
   memset(&M, 0, sizeof M);
   M.rfast = rfast ? 1 : 0;
+  if (rfast) { M.rec = c->rec.p; M.roff = c->roff.p; }
   M.mtab = c->d_mtab; M.mtab_bytes = c->mtab_bytes; M.words = d_words; M.woff = d_woff; M.nw = nw;
   M.mode = mode; M.mn = mn; M.mx = mx; M.SEG = c->mseg;
   M.count = c->count.p; M.nseg = c->m_nseg.p; M.flags = c->flags.p;
@@ -681,17 +683,26 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     c->m_items = 0;
     return A5X_OK;
   }
-  // -r words with pairwise disjoint positions whose subs[0] keep the key lengths go to the
-  // FAST path (a5x_kernels.hip r_unit): the default keyspace kernel probes them (count,
-  // bytes, plan record; flags & A5X_WF_FAST), k_mode_count and the length pass skip them,
+  // FAST probe (a5x_kernels.hip mode_unit): -r words with pairwise disjoint positions whose
+  // subs[0] keep the key lengths, -s / -s -r words whose every pattern occurs once and is
+  // statically positional, go to the FAST path: the default keyspace kernel plans them
+  // (count, bytes, record; flags & A5X_WF_FAST), the mode-engine kernels skip them, and
   // k_expand_fast (k_expand_fast_md5 / _ntlm in the fused digest) writes them beside the
-  // mode engine's items, so every path numbers a word's candidates the same way.
-  bool rfast = mode == A5X_MODE_REVERSE && mx >= 1 && mn <= 1 && !getenv("A5X_NO_RFAST");
+  // mode engine's items -- every path numbers a word's candidates the same way.  The other
+  // words are listed for the mode engine.  (An empty key makes "" a pattern of every -s word.)
+  const bool has_empty = ((const A5xMHdr*)c->mblob.data())->has_empty != 0;
+  bool rfast = mx >= 1 && mn <= 1 && !getenv("A5X_NO_RFAST") &&
+               (mode == A5X_MODE_REVERSE || ((mode == A5X_MODE_SUBALL || mode == A5X_MODE_SUBALL_REVERSE) && !has_empty));
   if (rfast && upload_table(c) != A5X_OK) {  // (a table the default engine refuses: mode engine only)
     rfast = false;
     c->err.clear();
   }
   B->rfast = rfast;
+  // -s / -s -r: radix positional words counted lane per word (k_mode_count_thread) over the
+  // words the probe left; the wave kernel k_mode_count only for the words it lists
+  const bool mct = (mode == A5X_MODE_SUBALL || mode == A5X_MODE_SUBALL_REVERSE) && mx >= 0 && !has_empty &&
+                   !getenv("A5X_NO_MCT");
+  if ((rfast || mct) && ((rc = grow(c, c->m_cl, nw + 1)) || (rc = grow(c, c->m_cl2, nw + 1)))) return rc;
   if (rfast) {
     if ((rc = grow(c, c->roff, nw + 1)) ||
         (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC + 2)))
@@ -701,25 +712,20 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     K.table = c->d_table; K.table_bytes = c->table_bytes; K.words = d_words; K.woff = d_woff; K.nw = nw;
     K.mn = mn; K.mx = mx; K.count = c->count.p; K.bytes = c->bytes.p; K.flags = c->flags.p;
     K.err = c->d_scalars + 2; K.rec = c->rec.p; K.roff = c->roff.p;
-    K.rmode = 1; K.rcmin = mn > 0 ? 1u : 0u; K.rnseg = c->m_nseg.p; K.rseg = c->mseg;
-    if ((rc = grow(c, c->m_cl, nw + 1))) return rc;
+    K.rmode = mode; K.rcmin = mn > 0 ? 1u : 0u; K.rnseg = c->m_nseg.p; K.rseg = c->mseg;
     K.defer_list = c->m_cl.p; K.defer_n = c->d_scalars + 12;
     HIPCHK(c, a5x_launch_keyspace(K, st));
   }
   A5xModeLaunch M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx, rfast);
-  if (rfast) {  // k_mode_count only over the words the probe left to the mode engine
-    M.cl_list = c->m_cl.p;
-    M.cl_n = c->d_scalars + 12;
-  }
-  // -s / -s -r: radix positional words counted lane per word (k_mode_count_thread), the
-  // wave kernel only for the words it lists (an empty key makes "" a pattern of every word)
-  const bool mct = (mode == A5X_MODE_SUBALL || mode == A5X_MODE_SUBALL_REVERSE) && mx >= 0 &&
-                   !((const A5xMHdr*)c->mblob.data())->has_empty && !getenv("A5X_NO_MCT");
   if (mct) {
-    if ((rc = grow(c, c->m_cl, nw + 1))) return rc;
+    M.in_list = rfast ? c->m_cl.p : nullptr;
+    M.in_n = rfast ? c->d_scalars + 12 : nullptr;
+    M.cl_list = rfast ? c->m_cl2.p : c->m_cl.p;
+    M.cl_n = c->d_scalars + (rfast ? 13 : 12);
+    HIPCHK(c, a5x_launch_mode_count_thread(M, st));
+  } else if (rfast) {  // k_mode_count only over the words the probe left to the mode engine
     M.cl_list = c->m_cl.p;
     M.cl_n = c->d_scalars + 12;
-    HIPCHK(c, a5x_launch_mode_count_thread(M, st));
   }
   HIPCHK(c, a5x_launch_mode_count(M, st));
   HIPCHK(c, a5x_launch_scan(c->count.p, c->m_nseg.p, nw, d_cand_off, c->m_seg_off.p, c->scan_tmp.p,

@@ -203,27 +203,46 @@ struct KsArgs {
   u32* glob_list;  // pass G words (k_keyspace_wave -> k_keyspace_g)
   u32* glob_n;
   uint8_t* gscr;   // pass G scratch slots
-  int rmode;       // 1: -r FAST probe (k_keyspace_thread only; r_unit below): the other
-                   // words are appended to defer_list (for k_mode_count)
+  int rmode;       // 1 / 2 / 3: -r / -s / -s -r FAST probe (k_keyspace_thread only;
+                   // mode_unit below): the other words are appended to defer_list
   u32 rcmin;       // -r: max(min, 0) (0 or 1 for a FAST word)
   u64* rnseg;      // -r: mode-engine items per FAST word (ceil(count / rseg))
   u64 rseg;
 };
 
-// -r (processWordReverse, main.go:208-261) on the FAST path.  For a word whose match
-// positions are pairwise disjoint -- exactly the lone units of the position-synchronous
-// walk -- and whose every key's subs[0] keeps the key's length (the running offset of
-// main.go:251-256 then moves nothing), candidate = any subset of the positions replaced
-// by subs[0]: a unit of 2 choices (choice 0 = the key, choice 1 = subs[0], a5x_format.h)
-// per position.  The size window [min, max] cuts nothing when min <= 1 <= #positions <=
-// max; with min = 0 the all-keep word is candidate P - 1 of the FAST numbering
-// (index P wraps to the all-zero digits), so count = P - rcmin.  Every candidate has
-// L + 1 bytes.  Returns false when the unit does not qualify (the mode engine takes
-// the word).
-__device__ __forceinline__ bool r_unit(const Tab& T, Unit& U) {
+// -r / -s / -s -r on the FAST path (the mode-engine probe of k_keyspace_thread, rmode =
+// 1 / 2 / 3).  The lone units of the position-synchronous walk are the word's match
+// positions when those are pairwise disjoint.
+//   -r (processWordReverse, main.go:208-261): every key's subs[0] keeps the key's length
+//      (the running offset of main.go:251-256 then moves nothing); candidate = any subset
+//      of the positions replaced by subs[0]: a unit of 2 choices (choice 0 = the key,
+//      choice 1 = subs[0], a5x_format.h) per position.
+//   -s / -s -r (main.go:308-365, 369-440): every pattern occurs once in the word and
+//      passes the static positional checks (A5xKey.pad0, key_pos_facts: one codepoint,
+//      values containing no key), so sequential ReplaceAll = replacing each occurrence:
+//      a unit of 1 + values (-s) or 2 (-s -r: subs[0]) choices per pattern.  seen: the
+//      patterns met so far (key index mod 64; a collision is taken for a repeat).
+// The size window cuts nothing when min <= 1 and max >= #units; count = P - min (min 0:
+// the all-keep word is index P of the FAST numbering, whose digits wrap to zero).
+// Returns false when the unit does not qualify (the mode engine takes the word).
+__device__ __forceinline__ bool mode_unit(const Tab& T, Unit& U, int rmode, u64& seen, bool check) {
   const A5xKey key = T.keys[U.key];
-  if (key.nvals < 1 || T.ch[key.choice_base + 1].len != key.klen) return false;
-  U.R = 2; U.ml = key.klen; U.mnl = key.klen; U.spos = 0; U.sneg = 0; U.maxd = 0;
+  if (rmode == 1) {
+    if (key.nvals < 1 || T.ch[key.choice_base + 1].len != key.klen) return false;
+    U.R = 2; U.ml = key.klen; U.mnl = key.klen; U.spos = 0; U.sneg = 0; U.maxd = 0;
+    return true;
+  }
+  if (check) {
+    if (!(key.pad0 & (rmode == 2 ? 1u : 2u)) || key.nvals < 1) return false;
+    const u64 bit = 1ull << (U.key & 63u);
+    if (seen & bit) return false;
+    seen |= bit;
+  }
+  if (rmode == 3) {  // subs[0] only
+    const u32 vl = T.ch[key.choice_base + 1].len, kl = key.klen;
+    U.R = 2; U.ml = max(kl, vl); U.mnl = min(kl, vl);
+    U.spos = vl > kl ? vl - kl : 0u; U.sneg = kl > vl ? kl - vl : 0u; U.maxd = (int)vl - (int)kl;
+  }
   return true;
 }
 
@@ -312,9 +331,10 @@ __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const
 #endif
 template <bool COUNT, class PL>
 __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 Lmax, u32 bmax, const Tab& T,
-                                         PL& pl, CountAcc& A, bool& cplx, bool rm, uint16_t* ulog = nullptr,
+                                         PL& pl, CountAcc& A, bool& cplx, int rmode, uint16_t* ulog = nullptr,
                                          u32* nlog = nullptr) {
   u32 cur_end = 0;
+  u64 seen = 0;
   for (u32 q = 0; q < Lmax; q++) {
     const bool act = act0 && q < L && !cplx;
     if (act) {
@@ -342,7 +362,7 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
       } else if (nm == 1 && !cplx) {
         Unit U;
         lone_unit(T, q, kk, U);
-        if (rm && !r_unit(T, U)) {
+        if (rmode && !mode_unit(T, U, rmode, seen, true)) {
           cplx = true;
         } else if (U.R > KS_GCAP) {
           cplx = true;
@@ -420,7 +440,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
     u32 nlog = 0;
     const bool rm = a.rmode != 0;
-    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, rm, ulog, &nlog);
+    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, a.rmode, ulog, &nlog);
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
     u32 f = 0;
@@ -434,12 +454,15 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     if (trivial) f = A5X_WF_RADIX | A5X_WF_FAST;
     if (longw) f = A5X_WF_DEFER;
     if (rm) {
-      // -r FAST words (r_unit): count = 2^n - rcmin, L + 1 bytes each; every other word
-      // (flags 0) is left to the mode engine (k_mode_count skips the FAST ones)
-      const bool rf = psk && !cplx && (f & A5X_WF_FAST) && !(f & A5X_WF_DEFER) && A.nunits > 0 && C.count > 0;
+      // mode FAST words (mode_unit): count = P - rcmin, the all-keep word's L + 1 bytes
+      // added when min = 0; -s / -s -r words only as one mode-engine item (the length pass
+      // takes their bytes whole); every other word (flags 0) is left to the mode engine
+      const u64 cnt = A.P - a.rcmin;
+      const bool rf = psk && !cplx && (f & A5X_WF_FAST) && !(f & A5X_WF_DEFER) && A.nunits > 0 && C.count > 0 &&
+                      (a.rmode == 1 || cnt <= a.rseg);
       f = rf ? f : 0u;
-      C.count = rf ? A.P - a.rcmin : 0ull;
-      C.bytes = rf ? C.count * (u64)(L + 1) : 0ull;
+      C.bytes = rf ? C.bytes + (a.rcmin ? 0ull : (u64)(L + 1)) : 0ull;
+      C.count = rf ? cnt : 0ull;
     }
     // ---- record sizes -> exclusive workgroup scan ----
     const bool fast = psk && !cplx && (f & A5X_WF_FAST) && C.count > 0;
@@ -467,12 +490,13 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
           const u32 e = ulog[i * 256u];
           Unit U;
           lone_unit(T, e >> 10, e & 1023u, U);
-          if (rm) (void)r_unit(T, U);  // (qualified in the count pass)
+          u64 seen = 0;
+          if (rm) (void)mode_unit(T, U, a.rmode, seen, false);  // (qualified in the count pass)
           pb.unit(U);
         }
       }
       const bool walk = build && !replay;
-      if (!(KS_ABL & 1)) psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2, rm);
+      if (!(KS_ABL & 1)) psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2, a.rmode);
       if (build && !(KS_ABL & 1)) {
         pb.finish(L);
         pb.pick_balanced();
@@ -1402,6 +1426,9 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #ifndef FX_NOOR
 #define FX_OR         // OR placement into a zeroed ring (a5x_fx6.h fx7_round)
 #endif
+#ifndef FX_DABL
+#define FX_DABL 0     // fused-digest ablations (variant builds, wrong hits): 1 no MD rounds, 2 no probe
+#endif
 #ifndef FX_AB
 #define FX_AB 0       // 1: fx8_put (alignbyte shifts, per-window scalar slot counts; A/B: 1 % slower)
 #endif
@@ -1625,9 +1652,18 @@ struct FxDigest {
       const bool on = c < lr.nc;
       if (!__builtin_amdgcn_ballot_w64(on)) break;  // runs are filled from candidate 0
       u32 d[4];
+#if FX_DABL & 1  // (ablation: no MD rounds -- a cheap stand-in digest)
+      d[0] = off * 0x9E3779B9u + l; d[1] = d[0] ^ 0x85EBCA6Bu; d[2] = d[0] * 3u; d[3] = d[1] + c;
+#else
       if constexpr (MD5) md_lds<true>(base, off, on ? l - 1u : 0u, d);  // the candidate without its '\n'
       else ntlm_lds(base, off, on ? l - 1u : 0u, d);
-      if (on && md_probe(a->dg_bitmap, a->dg_bm_mask, a->dg_table, a->dg_tmask, a->dg_has_zero != 0, d)) {
+#endif
+#if FX_DABL & 2  // (ablation: no target probe -- the digest kept live by a never-true test)
+      const bool hit = (d[0] ^ d[1] ^ d[2] ^ d[3]) == 0x7A5A5A5Au && d[0] == 0x13579BDFu;
+#else
+      const bool hit = md_probe(a->dg_bitmap, a->dg_bm_mask, a->dg_table, a->dg_tmask, a->dg_has_zero != 0, d);
+#endif
+      if (on && hit) {
         const u32 h = atomicAdd(a->dg_nhits, 1u);
         if (h < a->dg_hit_cap) {
           A5xHitRaw r;

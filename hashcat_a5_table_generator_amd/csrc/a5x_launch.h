@@ -32,7 +32,7 @@ struct A5xKsLaunch {
   uint32_t* glob_n;
   uint8_t* gscr;        // pass G scratch: gslots x a5x_gslot_bytes() (ring zeroed)
   uint32_t gslots;
-  int rmode;            // 1: -r FAST probe (k_keyspace_thread only, a5x_kernels.hip r_unit);
+  int rmode;            // 1 / 2 / 3: -r / -s / -s -r FAST probe (k_keyspace_thread only, mode_unit);
                         // the other words are listed in defer_list / defer_n
   uint32_t rcmin;       // -r: max(min, 0)
   uint64_t* rnseg;      // -r: per FAST word, ceil(count / rseg) mode-engine items
@@ -143,6 +143,10 @@ struct A5xModeLaunch {
   // wave kernel k_mode_count (cl_list null: k_mode_count takes every word)
   uint32_t* cl_list;
   uint32_t* cl_n;
+  const uint32_t* in_list;  // k_mode_count_thread's words (null: all; else the probe's list)
+  const uint32_t* in_n;
+  const uint64_t* rec;      // FAST plan records / offsets (k_mode_locate inside -s FAST words)
+  const uint32_t* roff;
   // fused digest (op 2): every candidate hashed where it is built and probed against the
   // target set; hits as (word, candidate in word) -- see A5xDigLaunch
   int dg_algo;

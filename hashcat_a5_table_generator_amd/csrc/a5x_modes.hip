@@ -1398,9 +1398,11 @@ __global__ void __launch_bounds__(256) k_mode_count_thread(A5xModeLaunch a) {
   const u32 okbit = sub ? 1u : 2u, dsh = sub ? 8u : 20u;
   const u32 cmin = a.mn > 0 ? (u32)a.mn : 0u;
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  const u64 nw_r = (a.nw + blockDim.x - 1) / blockDim.x * blockDim.x;  // every lane runs every pass
-  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nw_r; w += stride) {
-    const bool valid = w < a.nw;
+  const u64 nin = a.in_list ? (u64)*a.in_n : a.nw;  // (in_list: the words the FAST probe left)
+  const u64 nw_r = (nin + blockDim.x - 1) / blockDim.x * blockDim.x;  // every lane runs every pass
+  for (u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x; x < nw_r; x += stride) {
+    const bool valid = x < nin;
+    const u64 w = !valid ? 0 : a.in_list ? (u64)a.in_list[x] : x;
     u64 w0 = 0, L64 = 0;
     if (valid) { w0 = a.woff[w]; L64 = a.woff[w + 1] - w0; }
     bool dfr = !valid || L64 == 0 || L64 + 8 > MCT_SLOT || a.mx < 0 || cmin > 1;
@@ -1641,11 +1643,12 @@ __device__ __forceinline__ void m_items(const A5xModeLaunch& a, int op, uint8_t 
       const u64 w = a.item_w[i];
       const u32 fl = a.flags[w];
       if (fl & A5X_WF_GLOB) {
-      } else if (a.rfast && (fl & A5X_WF_FAST)) {  // every candidate L + 1 bytes (r_unit)
+      } else if (a.rfast && (fl & A5X_WF_FAST)) {  // k_expand_fast writes it (mode_unit)
         if (op == 0 && !route) {
+          // -r: every candidate L + 1 bytes; -s / -s -r: one item, sized by the probe
           const u64 cnt = a.cand_off[w + 1] - a.cand_off[w], t0 = (i - a.seg_off[w]) * a.SEG;
           const u64 nc = cnt - t0 < a.SEG ? cnt - t0 : a.SEG;
-          a.seg_bytes[i] = nc * (a.woff[w + 1] - a.woff[w] + 1);
+          a.seg_bytes[i] = a.mode == A5X_MODE_REVERSE ? nc * (a.woff[w + 1] - a.woff[w] + 1) : a.wbytes[w];
           a.item_fl[i] = MI_SKIP;
         }
       } else if (route) {
@@ -1703,6 +1706,33 @@ __device__ void m_locate(SL& S, const MT& T, const A5xModeLaunch& a, const u64* 
   const u64 t0 = (local / a.SEG) * a.SEG;
   const u32 r = (u32)(local - t0);
   u64 pre = 0;
+  if (!SL::G && r && a.rfast && (a.flags[w] & A5X_WF_FAST)) {
+    // a FAST word (k_expand_fast numbering): -r candidates are all L + 1 bytes; -s / -s -r
+    // (one item): candidates [0, r) summed from the word's plan record, lanes over them
+    if (a.mode == A5X_MODE_REVERSE) {
+      pre = (u64)r * (a.woff[w + 1] - a.woff[w] + 1);
+    } else {
+      const u64* rec = a.rec + a.roff[w];
+      const u32 np = (u32)rec[0] & 15u;
+      u64 sum = 0;
+      for (u32 cnd = m_lane(); cnd < r; cnd += 64) {
+        u32 n = cnd + 1, len = 0;
+        for (u32 p = 0; p < np; p++) {
+          const u64 G = rec[1 + p];
+          const u32 R = ((u32)(G >> 40) & 31u) + 1u, eb = (u32)(G >> 32) & 255u;
+          const u32 d = n % R;
+          n /= R;
+          len += (u32)(rec[1 + np + eb + d] >> 56) & 7u;
+        }
+        sum += len;
+      }
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) sum += (u64)__shfl_xor((long long)sum, dd, 64);
+      pre = sum;
+    }
+    if (m_lane() == 0) { out[3 * q] = item; out[3 * q + 1] = r; out[3 * q + 2] = a.seg_boff[item] + pre; }
+    return;
+  }
   if (r) {
     const MInfo I = m_setup(S, T, a, w);
     if (I.bad || I.count != a.cand_off[w + 1] - a.cand_off[w]) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }

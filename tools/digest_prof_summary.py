@@ -10,6 +10,35 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import digest_src_sha  # noqa: E402
 
+
+def breakdown(algos):
+    """tools/gpu.sh dabl: VALU wave instructions per candidate of k_expand_fast_<algo> in the
+    product build and the FX_DABL variants (1 no MD rounds, 2 no probe, 3 neither) ->
+    MD rounds = full - dabl1, probe = full - dabl2, expansion + ring = dabl3."""
+    out = os.path.join(ROOT, "gpurun_out")
+    for algo in algos.split():
+        per = {}
+        for v in ("cur", "dabl1", "dabl2", "dabl3"):
+            f = glob.glob(os.path.join(out, "dabl_%s_%s" % (algo, v), "run_counter_collection.csv"))
+            valu = sum(float(r["Counter_Value"]) for r in csv.DictReader(open(f[0])) if r["Counter_Name"] == "SQ_INSTS_VALU")
+            cands = None
+            for line in open(os.path.join(out, "dabl_%s_%s.log" % (algo, v))):
+                if line.startswith("{"):
+                    cands = json.loads(line)["config"]["candidates_per_gpu_step"]
+            per[v] = valu * 64 / cands  # int lane-ops per candidate
+        res = {"algo": algo, "kernel": "k_expand_fast_" + algo, "kernel_src_sha": digest_src_sha(),
+               "int_ops_per_cand": per["cur"], "md_rounds": per["cur"] - per["dabl1"],
+               "probe": per["cur"] - per["dabl2"], "expansion_ring_and_loop": per["dabl3"],
+               "variants": per,
+               "note": "SQ_INSTS_VALU x 64 / candidates of one C5 step (2M words, 1M targets); FX_DABL variant builds: "
+                       "1 = MD rounds replaced by a 4-op stand-in, 2 = probe replaced by a never-true test, 3 = both"}
+        json.dump(res, open(os.path.join(out, "digest_breakdown_%s_c5.json" % algo), "w"), indent=1)
+        print(json.dumps(res))
+
+
+if sys.argv[1] == "breakdown":
+    breakdown(sys.argv[2])
+    sys.exit(0)
 algo, words = sys.argv[1], int(sys.argv[2])
 kname = sys.argv[3] if len(sys.argv) > 3 else "k_digest_stream"
 out = os.path.join(ROOT, "gpurun_out")
@@ -45,8 +74,8 @@ res = {
     "active_valu_per_wave_cycle": sum(c1.get("SQ_ACTIVE_INST_VALU", [0])) / max(1.0, sum(c1.get("SQ_WAVE_CYCLES", [1]))),
     "kernel_avg_us": float(dig["AverageNs"]) / 1e3 if dig else None,
     "kernel_calls": int(dig["Calls"]) if dig else None,
-    "note": "SQ_INSTS_VALU summed over the k_digest_stream dispatches of one step (1 step, 0 warmup; the "
-            "planted-target setup adds ~1e6 candidates); int_ops = wave instructions x 64 lanes",
+    "note": "SQ_INSTS_VALU summed over the %s dispatches of one step (1 step, 0 warmup; the "
+            "planted-target setup adds ~1e6 candidates); int_ops = wave instructions x 64 lanes" % kname,
 }
 json.dump(res, open(os.path.join(out, "pmc_digest_%s_%s_c5.json" % (algo, kname)), "w"), indent=1)
 print(json.dumps(res))

@@ -15,7 +15,9 @@
 #   pmc         PMC counter groups, one pass each (PMC="group\ngroup", KRE, BENCH_ARGS)
 #   digestprof  fused-digest kernel stats + VALU counters [ALGOS, KRE, WORDS]
 #   stamps      per-phase cycle stamps (diagnostic build _build_diag) [WL, SW]
-#   final       test + C3 bench/prof/traffic + C4 + C2a + fused digests + C5 modes + stdout path
+#   final       test + C3 bench (+ steady state, CPU baseline)/prof/traffic + C4 + C2a
+#   final2      fused digests (+ dabl op breakdown) + C5 modes (+ rocprof) + stdout path
+#   dabl        fused-digest VALU per candidate, product vs FX_DABL variant builds [ALGOS, WORDS]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 2
@@ -136,27 +138,48 @@ step_digestprof() {
   done
 }
 
+step_dabl() {  # fused-digest op breakdown: VALU instructions per candidate with MD rounds / probe ablated
+  local W=${WORDS:-2000000}
+  for A in ${ALGOS:-md5 ntlm}; do
+    for v in cur dabl1 dabl2 dabl3; do
+      local lib=""
+      [ $v != cur ] && lib=$R/hashcat_a5_table_generator_amd/_build_$v/liba5x.so
+      ( cd /tmp && export TMPDIR=/tmp && A5X_LIB_PATH=$lib timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES \
+          --kernel-include-regex k_expand_fast_$A -d $R/gpurun_out/dabl_${A}_$v -o run --output-format csv -- \
+          python3 $R/bench.py --digest $A --workload c5 --words $W --no-cpu-baseline --targets 1000000 --steps 1 --warmup 0 \
+          > $R/gpurun_out/dabl_${A}_$v.log 2>&1 ) || { echo "dabl $A $v failed"; tail -5 gpurun_out/dabl_${A}_$v.log; return 18; }
+    done
+  done
+  python3 tools/digest_prof_summary.py breakdown "${ALGOS:-md5 ntlm}"
+}
+
 step_stamps() {
   timeout -k 10 120 python tools/stamps.py ${WL:-c3} ${SW:-2000000} > gpurun_out/stamps_$T.txt 2>&1 \
     || { tail -5 gpurun_out/stamps_$T.txt; return 17; }
   cat gpurun_out/stamps_$T.txt
 }
 
-step_final() {
+step_final() {  # part 1: tests, the headline C3 line and its evidence, C4, C2a, steady state
   TT=900 step_test || return $?
   NAME=_c3 BENCH_ARGS="" step_bench || return $?
-  BENCH_ARGS="" step_prof || return $?
+  BENCH_ARGS="--steady-batches 0" step_prof || return $?
   WL=c3 step_traffic || return $?
-  NAME=_c3_steady BENCH_ARGS="--steady-batches 4 --no-cpu-baseline" step_bench || return $?
-  NAME=_c4 BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --workload c4 --words 12500000" step_bench || return $?
-  NAME=_c2a BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --workload c2a --words 1000000" step_bench || return $?
+  NAME=_c4 BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --workload c4 --words 12500000 --steady-batches 0" step_bench || return $?
+  NAME=_c2a BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --workload c2a --words 1000000 --steady-batches 0" step_bench || return $?
+}
+
+step_final2() {  # part 2: fused digests (+ op breakdown), the -r / -s / -s -r lines and profiles, stdout path
   ALGOS="md5 ntlm" step_digestprof || return $?
   for alg in md5 ntlm; do
     NAME=_digest_$alg BENCH_ARGS="--digest $alg --workload c5 --words 2000000 --targets 1000000 --steps 3 --warmup 1" \
       step_bench || return $?
   done
+  step_dabl || return $?
   for m in 1 2 3; do
     NAME=_c5_mode$m BENCH_ARGS="--mode $m --workload c5 --steps 3 --warmup 1 --no-cpu-baseline" step_bench || return $?
+  done
+  for m in 1 2; do
+    TAG=${T}_m$m BENCH_ARGS="--mode $m --workload c5 --steady-batches 0" STEPS=2 step_prof || return $?
   done
   NAME=_stdout BENCH_ARGS="--stdout --no-cpu-baseline" step_bench || return $?
 }
