@@ -416,7 +416,8 @@ struct Batch {  // device-side per-batch state after keyspace
   uint64_t total_cands = 0, total_bytes = 0;
   uint32_t nbig = 0, nslow = 0;
   uint32_t nglob = 0;  // pass G words (on the BIG list, expanded by k_expand_g)
-  bool rfast = false;  // -r: FAST words probed by k_keyspace_thread (expanded by k_expand_fast)
+  bool rfast = false;  // -r / -s / -s -r: FAST words probed by k_keyspace_thread (k_expand_fast)
+  uint64_t nmode = 0;  // -r / -s / -s -r: words left to the mode engine (0: no mode-item launch)
   const uint64_t* cand_off = nullptr;
   const uint64_t* byte_off = nullptr;
 };
@@ -732,8 +733,9 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
                             c->d_scalars + 2, st));
   HIPCHK(c, hipMemcpyAsync(c->h_totals, d_cand_off + nw, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipMemcpyAsync(c->h_totals + 1, c->m_seg_off.p + nw, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  B->nmode = rfast ? c->h_scalars[12] : nw;
   if (c->h_scalars[2] == 0 && c->h_scalars[7] > 0) {
     // mode pass G: words longer than the LDS engines take are counted in HBM scratch
     // slots (their counts were 0 in the first scan), then the scan runs again
@@ -973,7 +975,7 @@ int job_launch(a5x_ctx* c, const Job& J, const Range& R, uint8_t* d_out, uint64_
     if (!c->ev_join) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     HIPCHK(c, hipEventRecord(c->ev_fork, J.st));
     HIPCHK(c, hipStreamWaitEvent(c->sstream, c->ev_fork, 0));
-    HIPCHK(c, a5x_launch_mode_items(M, 1, c->sstream));
+    if (J.B.nmode) HIPCHK(c, a5x_launch_mode_items(M, 1, c->sstream));  // (every word FAST: none)
     A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
     E.cand_begin = R.cb;
     E.cand_end = R.ce;
@@ -1121,7 +1123,7 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
       M.dg_hits = c->dg_hits.p; M.dg_hit_cap = (uint32_t)dev_hits; M.dg_nhits = c->d_scalars + 8;
       HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
       HIPCHK(c, hipEventRecord(c->ev[1], J.st));
-      HIPCHK(c, a5x_launch_mode_items(M, 2, J.st));
+      if (J.B.nmode) HIPCHK(c, a5x_launch_mode_items(M, 2, J.st));
       if (J.B.rfast && tc) {  // -r FAST words: hashed in k_expand_fast_md5 / _ntlm's ring
         A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
         E.cand_begin = 0;

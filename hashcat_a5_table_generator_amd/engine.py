@@ -234,7 +234,12 @@ class Context:
     def expand_digest_device(self, d_words: int, d_offs: int, n_words: int, mode: int = MODE_DEFAULT, mn: int = 0,
                              mx: int = 15, scratch_bytes: int = 0, hit_cap: int = 1 << 16,
                              stream: int = 0) -> Tuple[List[Tuple[int, int, bytes]], dict]:
-        arr = (_lib.Hit * max(1, hit_cap))()
+        # (one hit buffer per context, grown on demand: a fresh 1M-entry ctypes array costs
+        # milliseconds of host zeroing per call)
+        buf = getattr(self, "_hit_buf", None)
+        if buf is None or len(buf) < max(1, hit_cap):
+            buf = self._hit_buf = (_lib.Hit * max(1, hit_cap))()
+        arr = buf
         nh = ctypes.c_uint64()
         st = Stats()
         self._chk(self._L.a5x_expand_digest_device(self.h, d_words, d_offs, n_words, mode, mn, mx, scratch_bytes,

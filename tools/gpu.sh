@@ -144,7 +144,7 @@ step_dabl() {  # fused-digest op breakdown: VALU instructions per candidate with
     for v in cur dabl1 dabl2 dabl3; do
       local lib=""
       [ $v != cur ] && lib=$R/hashcat_a5_table_generator_amd/_build_$v/liba5x.so
-      ( cd /tmp && export TMPDIR=/tmp && A5X_LIB_PATH=$lib timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES \
+      ( cd /tmp && export TMPDIR=/tmp && A5X_BENCH_NO_HITCHECK=1 A5X_LIB_PATH=$lib timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES \
           --kernel-include-regex k_expand_fast_$A -d $R/gpurun_out/dabl_${A}_$v -o run --output-format csv -- \
           python3 $R/bench.py --digest $A --workload c5 --words $W --no-cpu-baseline --targets 1000000 --steps 1 --warmup 0 \
           > $R/gpurun_out/dabl_${A}_$v.log 2>&1 ) || { echo "dabl $A $v failed"; tail -5 gpurun_out/dabl_${A}_$v.log; return 18; }
@@ -178,9 +178,11 @@ step_final2() {  # part 2: fused digests (+ op breakdown), the -r / -s / -s -r l
   for m in 1 2 3; do
     NAME=_c5_mode$m BENCH_ARGS="--mode $m --workload c5 --steps 3 --warmup 1 --no-cpu-baseline" step_bench || return $?
   done
+  local T0=$T
   for m in 1 2; do
-    TAG=${T}_m$m BENCH_ARGS="--mode $m --workload c5 --steady-batches 0" STEPS=2 step_prof || return $?
+    T=${T0}_m$m; BENCH_ARGS="--mode $m --workload c5 --steady-batches 0" STEPS=2 step_prof || { T=$T0; return 13; }
   done
+  T=$T0
   NAME=_stdout BENCH_ARGS="--stdout --no-cpu-baseline" step_bench || return $?
 }
 
