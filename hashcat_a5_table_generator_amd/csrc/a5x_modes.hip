@@ -86,11 +86,18 @@ constexpr u32 MP_VMAX = 14;   // values per pattern (selector 1 + v <= 15)
 constexpr u32 MP_RING = 16 + 64 * A5X_M_CBUF + 48;
 // radix words (MInfo::radix), piece expansion (m_fast_expand): the multi-token pieces'
 // entries follow the token entries (ent[MP_NE ..]); pieces of one word
-constexpr u32 MF_NPE = 256;
-constexpr u32 MF_ZE = MP_NE + MF_NPE - 1;  // the empty entry
-constexpr u32 MF_PMAX = A5X_M_LMAX + 2;
+#ifndef MF_NPE
+#define MF_NPE 128           // multi-token piece entries per word (the piece layout's LDS; 256: C5 -s 10 % slower, 9 vs 11 waves per CU)
+#endif
+#ifndef MF_NE
+#define MF_NE 128            // token entries of the piece layout (MP_NE elsewhere): words needing more
+                             // are routed to the token ring (m_pos_setup's entry count, S.nent)
+#endif
+#ifndef MF_TCAP
+#define MF_TCAP 48           // tokens (and so pieces) per word in the piece layout; more: the token ring
+#endif
 #ifndef MF_RING
-#define MF_RING 4096         // the piece engine's ring (runs that do not fit wait a round)
+#define MF_RING 3072         // the piece engine's ring (runs that do not fit wait a round; 4096: C5 -s 7 % slower)
 #endif
 #ifndef MF_K
 #define MF_K 2               // leaves per lane run (odometer steps between them; C5: 2 < 4 < 8)
@@ -104,22 +111,26 @@ constexpr u32 MF_PMAX = A5X_M_LMAX + 2;
 #ifndef MF_EMAX
 #define MF_EMAX 64           // entries of one multi-token piece
 #endif
-template <u32 LMAX, u32 CBUF, u32 NBUF = 2 * 64 * (CBUF + 4), u32 DPN = A5X_M_DPMAX, u32 NPE = 0>
+template <u32 LMAX, u32 CBUF, u32 NBUF = 2 * 64 * (CBUF + 4), u32 DPN = A5X_M_DPMAX, u32 NPE = 0, u32 NE = MP_NE,
+          u32 TC = A5X_M_LMAX + 2>
 struct MLdsT {
+  static constexpr u32 TCAP = TC;              // tokens per word
+  static constexpr u32 N_E = NE;               // token entries (patterns' choices, literal chunks)
+  static constexpr u32 ZE = NE + NPE - 1;      // the piece layout's empty entry
   static constexpr u32 L_MAX = LMAX, STRIDE = CBUF + 4, CMAXLEN = CBUF - 1;
   static constexpr bool G = LMAX > A5X_M_LMAX;
   static constexpr bool BUILDER = NBUF >= 2 * 64 * STRIDE, RING = NBUF >= MP_RING;
   static constexpr bool FAST = NPE > 0;  // piece engine layout: no DP table (radix words only)
   u64 dp[DPN ? DPN : 1];
-  uint4 ent[MP_NE + NPE];
-  uint4 pdesc[NPE ? MF_PMAX : 1];  // pieces: entry base (bias folded) | selector shifts | strides | sources
-  u32 tok[A5X_M_LMAX + 2];   // entry base | (pattern index + 1) << 16 (0: literal chunk)
+  uint4 ent[NE + NPE];
+  uint4 pdesc[NPE ? TC : 1];  // pieces: entry base (bias folded) | selector shifts | strides | sources
+  u32 tok[TC];               // entry base | (pattern index + 1) << 16 (0: literal chunk)
   uint8_t mpi[A5X_M_LMAX];   // pattern index + 1 matched at byte q (0: none)
   uint8_t pb[MP_PMAX], occ[MP_PMAX];
-  uint8_t elen[MP_NE + NPE]; // entry lengths
+  uint8_t elen[NE + NPE];    // entry lengths
   u32 rmag[MP_PMAX];         // radix mode: magic of R_r = 1 + values of pattern r
   uint8_t rr[MP_PMAX];       // R_r
-  u32 ntok, radix, shift;
+  u32 ntok, radix, shift, nent;  // (nent: token entries m_pos_setup used)
   u32 bitmap[A5X_MTAB_KEYS_MAX / 32];
   alignas(16) uint8_t word[LMAX + 16];
   uint16_t pat[64];          // key index per sorted pattern (-s) / per position (-r)
@@ -130,7 +141,7 @@ struct MLdsT {
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF> MLds;                // byte builder (general words)
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MP_RING> MLdsR;      // positional expansion
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, 16> MLdsC;           // counts, closed-form lengths
-typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MF_RING + 48, 0, MF_NPE> MLdsF;  // piece expansion (radix words)
+typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MF_RING + 48, 0, MF_NPE, MF_NE, MF_TCAP> MLdsF;  // piece expansion (radix words)
 typedef MLdsT<A5X_MG_LMAX, A5X_MG_CBUF> MLdsG;             // mode pass G (HBM)
 
 // wave sync over the word state: LDS, or (pass G) HBM written and read by the wave's own
@@ -618,7 +629,7 @@ __device__ u32 m_rpos_setup(SL& S, const MT& T, const MInfo& I) {
   const u32 tinc = m_incl_scan(ntk), cinc = m_incl_scan(nch);
   const u32 nt = (u32)__builtin_amdgcn_readlane((int)tinc, 63);
   const u32 nlit = (u32)__builtin_amdgcn_readlane((int)cinc, 63);
-  const bool over = 2 * n + nlit > MP_NE;
+  const bool over = 2 * n + nlit > SL::N_E || nt > SL::TCAP;
   if (!over && lane <= n) {
     const u32 t = tinc - ntk, e = 2 * n + cinc - nch;
     for (u32 c = 0; c < nch; c++) {
@@ -635,6 +646,7 @@ __device__ u32 m_rpos_setup(SL& S, const MT& T, const MInfo& I) {
   }
   if (lane == 0) {
     S.ntok = over ? 0u : nt;
+    S.nent = 2 * n + nlit;
     S.radix = 0;
   }
   m_sync<SL>();
@@ -672,7 +684,7 @@ __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode, bool ch
   if (__ballot(!ok)) return 0;
   const u32 incl = m_incl_scan(ne);
   const u32 npe = (u32)__builtin_amdgcn_readlane((int)incl, 63);
-  if (npe > MP_NE) return 0;
+  if (npe > SL::N_E) return 0;
   M_WAVE_SYNC();
   if (lane < n) {  // pattern entries: [keep, value 0, value 1, ...]
     const u32 b = incl - ne;
@@ -749,7 +761,7 @@ __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode, bool ch
     const u64 tb = __ballot(tstart), lb = __ballot(lstart);
     const u32 ti = nt + (u32)__popcll(tb & ((1ull << lane) - 1ull));
     const u32 li = nlit + (u32)__popcll(lb & ((1ull << lane) - 1ull));
-    if (tstart) {
+    if (tstart && ti < SL::TCAP) {
       S.elen[ti] = (uint8_t)q;
       S.tok[ti] = m ? (S.pb[m - 1] | (m << 16)) : (npe + li);
     }
@@ -761,7 +773,7 @@ __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode, bool ch
     nlit += (u32)__popcll(lb);
     rs_carry = (u32)__builtin_amdgcn_readlane((int)rs, 63);
   }
-  const bool over = npe + nlit > MP_NE;
+  const bool over = npe + nlit > SL::N_E || nt > SL::TCAP;
   if (lane < n) S.occ[lane] = (uint8_t)occ;
   M_WAVE_SYNC();
   if (!over) {  // literal chunk entries: bytes [q, next token start)
@@ -778,6 +790,7 @@ __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode, bool ch
   }
   if (lane == 0) {
     S.ntok = over ? 0u : nt;
+    S.nent = npe + nlit;
     // radix mode: no effective size window (min <= 1, max >= #patterns) -- the leaves are
     // every per-pattern choice vector (minus the all-keep one when min = 1), enumerated
     // as the mixed radix over patterns (pattern 0 least significant, digit 0 = keep);
@@ -792,7 +805,7 @@ __device__ u32 m_pos_setup(SL& S, const MT& T, const MInfo& I, int mode, bool ch
     S.rr[lane] = (uint8_t)R;
     S.rmag[lane] = R > 1 ? (u32)((((u64)1 << 32) + R - 1) / R) : 0u;
   }
-  for (u32 e = lane; e < MP_NE; e += 64) S.elen[e] = (uint8_t)(S.ent[e].w >> 24);
+  for (u32 e = lane; e < SL::N_E; e += 64) S.elen[e] = (uint8_t)(S.ent[e].w >> 24);
   M_WAVE_SYNC();
   return (u32)__builtin_amdgcn_readfirstlane((int)S.ntok);
 }
@@ -1013,7 +1026,7 @@ __device__ u32 m_piece_setup_serial(SL& S, const MInfo& I, int mode, u32 ntok, u
     if (k1 == k + 1) {
       base = S.tok[k] & 0xFFFFu;  // one token: its own entries, indexed by its digit
     } else {
-      base = MP_NE + pe;
+      base = SL::N_E + pe;
       for (u32 e = lane; e < E; e += 64) {
         const u32 d0 = e % R0, d1 = (e / R0) % R1, d2 = e / (R0 * R1);
         u64 lo = 0, hi = 0;
@@ -1041,8 +1054,8 @@ __device__ u32 m_piece_setup_serial(SL& S, const MInfo& I, int mode, u32 ntok, u
     k = k1;
   }
   if (lane == 0) {  // the empty entry (leaves past a run's end)
-    S.ent[MF_ZE] = make_uint4(0, 0, 0, 0);
-    S.elen[MF_ZE] = 0;
+    S.ent[SL::ZE] = make_uint4(0, 0, 0, 0);
+    S.elen[SL::ZE] = 0;
   }
   m_sync<SL>();
   return np;
@@ -1095,7 +1108,7 @@ __device__ u32 m_piece_setup(SL& S, const MInfo& I, int mode, u32 ntok, u64& bia
       k1++;
     }
     const bool multi = k1 > k + 1;
-    const u32 base = multi ? MP_NE + pe : (u32)__builtin_amdgcn_readlane((int)teb, (int)k);
+    const u32 base = multi ? SL::N_E + pe : (u32)__builtin_amdgcn_readlane((int)teb, (int)k);
     if (lane == np) {
       pk0 = k; pk1 = k1; psrc = s0 | (s1 << 8) | (s2 << 16); pR = R0 | (R1 << 8) | (R2 << 16);
       pE = multi ? E : 0u; pbase = base; pns = ns; pml = ml;
@@ -1120,13 +1133,13 @@ __device__ u32 m_piece_setup(SL& S, const MInfo& I, int mode, u32 ntok, u64& bia
     const u32 g = g0 + lane;
     u32 p = 0;
     for (u32 q = 0; q < np; q++) {
-      const u32 bq = (u32)__builtin_amdgcn_readlane((int)pbase, (int)q) - MP_NE;
+      const u32 bq = (u32)__builtin_amdgcn_readlane((int)pbase, (int)q) - SL::N_E;
       const u32 eq = (u32)__builtin_amdgcn_readlane((int)pE, (int)q);
       p = (eq && g >= bq && g < bq + eq) ? q : p;
     }
     const u32 k0 = (u32)__shfl((int)pk0, (int)p), k1 = (u32)__shfl((int)pk1, (int)p);
     const u32 src = (u32)__shfl((int)psrc, (int)p), Rp = (u32)__shfl((int)pR, (int)p);
-    const u32 e = g - ((u32)__shfl((int)pbase, (int)p) - MP_NE);
+    const u32 e = g - ((u32)__shfl((int)pbase, (int)p) - SL::N_E);
     if (g < pe) {
       const u32 R0 = Rp & 255u, R1 = (Rp >> 8) & 255u;
       const u32 s0 = src & 255u, s1 = (src >> 8) & 255u;
@@ -1138,13 +1151,13 @@ __device__ u32 m_piece_setup(SL& S, const MInfo& I, int mode, u32 ntok, u64& bia
         const u32 dg = !pi ? 0u : pi == s0 ? d0 : pi == s1 ? d1 : d2;
         m_cat(lo, hi, off, S.ent[(d & 0xFFFFu) + dg]);
       }
-      S.ent[MP_NE + g] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, ((u32)(hi >> 32) & 0xFFFFFFu) | (off << 24));
-      S.elen[MP_NE + g] = (uint8_t)off;
+      S.ent[SL::N_E + g] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, ((u32)(hi >> 32) & 0xFFFFFFu) | (off << 24));
+      S.elen[SL::N_E + g] = (uint8_t)off;
     }
   }
   if (lane == 0) {  // the empty entry (leaves past a run's end)
-    S.ent[MF_ZE] = make_uint4(0, 0, 0, 0);
-    S.elen[MF_ZE] = 0;
+    S.ent[SL::ZE] = make_uint4(0, 0, 0, 0);
+    S.elen[SL::ZE] = 0;
   }
   m_sync<SL>();
   return np;
@@ -1215,7 +1228,7 @@ __device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64
       for (u32 p = 0; p < np; p++) {
         const uint4 pd = S.pdesc[p];
 #pragma unroll
-        for (int c = 0; c < MF_K; c++) clen[c] += S.elen[(u32)c < nc ? m_piece_ix(pd, sel[c]) : MF_ZE];
+        for (int c = 0; c < MF_K; c++) clen[c] += S.elen[(u32)c < nc ? m_piece_ix(pd, sel[c]) : SL::ZE];
       }
     }
 #pragma unroll
@@ -1235,7 +1248,7 @@ __device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64
         const uint4 pd = S.pdesc[p];
         const u32 nsl = (u32)__builtin_amdgcn_readfirstlane((int)(pd.w >> 8));
 #pragma unroll
-        for (int c = 0; c < MF_K; c++) fx8_put(S.ent[(u32)c < nc ? m_piece_ix(pd, sel[c]) : MF_ZE], P1[c], nsl);
+        for (int c = 0; c < MF_K; c++) fx8_put(S.ent[(u32)c < nc ? m_piece_ix(pd, sel[c]) : SL::ZE], P1[c], nsl);
       }
 #pragma unroll
       for (int c = 0; c < MF_K; c++) fx8_put((u32)c < nc ? nl : make_uint4(0, 0, 0, 0), P1[c], 2u);
@@ -1362,7 +1375,7 @@ __device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLa
       const u32 ntok = m_pos_setup(S, T, I, a.mode);
       if (ntok && a.mode == A5X_MODE_REVERSE) wb = I.count * (u64)(I.L + 1);
       else if (ntok && S.radix) wb = m_pos_prefix(S, I, I.count) - m_pos_prefix(S, I, 0);
-      if (wb != ~0ull && I.radix && !MF_OFF) wb |= M_WB_FAST;
+      if (wb != ~0ull && I.radix && !MF_OFF && S.nent <= MF_NE && ntok <= MF_TCAP) wb |= M_WB_FAST;
     }
     if (m_lane() == 0) a.wbytes[w] = wb;
   }
@@ -1413,7 +1426,7 @@ __global__ void __launch_bounds__(256) k_mode_count_thread(A5xModeLaunch a) {
         if (4 * q + b < L) v |= (u32)a.words[w0 + 4 * q + b] << (8 * b);
       ((u32*)ws)[q] = v;
     }
-    u32 n = 0, nlit = 0, lend = 0;
+    u32 n = 0, nlit = 0, lend = 0, nocc = 0;
     for (u32 q = 0; q < L && !dfr; q++) {
       const u32 b = ws[q], w4 = m_lds4(ws, q);
       for (u32 k = T.bucket[b]; k < T.bucket[b + 1] && !dfr; k++) {
@@ -1438,6 +1451,7 @@ __global__ void __launch_bounds__(256) k_mode_count_thread(A5xModeLaunch a) {
         } else {
           pl[j * 256] += 1u << 16;
         }
+        nocc++;
         nlit += (q - lend + 14u) / 15u;  // the literal run before this occurrence, in <= 15-byte chunks
         lend = q + K.klen;               // (codepoint keys in a word never overlap)
       }
@@ -1467,7 +1481,8 @@ __global__ void __launch_bounds__(256) k_mode_count_thread(A5xModeLaunch a) {
       const u64 bytes = (u64)((i64)(count * (u64)(L + 1)) + extra);
       // m_pos_setup's table limits (entries of the patterns, then the literal chunks)
       const bool pos = L <= A5X_M_LMAX && npe <= MP_NE && npe + nlit <= MP_NE;
-      if (pos && count > 0 && count <= a.SEG) wb = bytes | (MF_OFF ? 0ull : M_WB_FAST);
+      if (pos && count > 0 && count <= a.SEG)
+        wb = bytes | (MF_OFF || npe + nlit > MF_NE || nocc + nlit > MF_TCAP ? 0ull : M_WB_FAST);
       a.count[w] = count;
       a.nseg[w] = (count + a.SEG - 1) / a.SEG;
       a.flags[w] = 0;
@@ -1610,7 +1625,8 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
       return;
     }
     if (m_lane() == 0)
-      a.item_fl[i] = ntok ? (I.radix && !MF_OFF ? MI_FAST : MI_POS) : a.mode == A5X_MODE_REVERSE ? MI_BUILD : MI_BUILD_LEN;
+      a.item_fl[i] = ntok ? (I.radix && !MF_OFF && S.nent <= MF_NE && ntok <= MF_TCAP ? MI_FAST : MI_POS)
+                          : a.mode == A5X_MODE_REVERSE ? MI_BUILD : MI_BUILD_LEN;
     if (!ntok && a.mode != A5X_MODE_REVERSE) return;  // lengths need the byte builder
     if (ntok && S.radix) {  // op 0, radix mode: closed form, no candidate is visited
       const u64 run = m_pos_prefix(S, I, t0 + nc) - m_pos_prefix(S, I, t0);
