@@ -69,7 +69,8 @@ constexpr u32 M_ERR_LIMIT = 1u << 6;  // word beyond the mode-engine limits
 constexpr u32 M_ERR_PANIC = 1u << 7;  // -r slice-bounds panic (main.go:255)
 constexpr u32 M_ERR_CLEN = 1u << 8;   // a candidate longer than the lane buffer
 constexpr u32 M_ERR_GWORD = 1u << 30; // (not an error) word longer than A5X_M_LMAX: mode pass G
-constexpr u64 M_WB_FAST = 1ull << 62;  // k_mode_count's wbytes of a single-item word: route MI_FAST
+constexpr u64 M_WB_FAST = 1ull << 62;   // k_mode_count's wbytes of a single-item word: route MI_FAST
+constexpr u64 M_WB_FAST2 = 1ull << 61;  // ... route MI_FAST2 (the piece layout with room for more entries)
 
 
 // positional -s / -s -r words (m_pos_setup): entries (a5x_ring.h) and the token list
@@ -90,8 +91,12 @@ constexpr u32 MP_RING = 16 + 64 * A5X_M_CBUF + 48;
 #define MF_NPE 128           // multi-token piece entries per word (the piece layout's LDS; 256: C5 -s 10 % slower, 9 vs 11 waves per CU)
 #endif
 #ifndef MF_NE
-#define MF_NE 128            // token entries of the piece layout (MP_NE elsewhere): words needing more
-                             // are routed to the token ring (m_pos_setup's entry count, S.nent)
+#define MF_NE 64             // token entries of the small piece layout (MLdsF, 14 waves per CU);
+                             // MF_NE2 in the large one (MLdsF2); words needing more entries (m_pos_setup's
+                             // count, S.nent) run on the token ring.  C5 -s: 128 in MLdsF -> 15 % slower
+#endif
+#ifndef MF_NE2
+#define MF_NE2 128
 #endif
 #ifndef MF_TCAP
 #define MF_TCAP 48           // tokens (and so pieces) per word in the piece layout; more: the token ring
@@ -141,7 +146,8 @@ struct MLdsT {
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF> MLds;                // byte builder (general words)
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MP_RING> MLdsR;      // positional expansion
 typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, 16> MLdsC;           // counts, closed-form lengths
-typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MF_RING + 48, 0, MF_NPE, MF_NE, MF_TCAP> MLdsF;  // piece expansion (radix words)
+typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MF_RING + 48, 0, MF_NPE, MF_NE, MF_TCAP> MLdsF;    // piece expansion (radix words)
+typedef MLdsT<A5X_M_LMAX, A5X_M_CBUF, MF_RING + 48, 0, MF_NPE, MF_NE2, MF_TCAP> MLdsF2;  // ... with more token entries
 typedef MLdsT<A5X_MG_LMAX, A5X_MG_CBUF> MLdsG;             // mode pass G (HBM)
 
 // wave sync over the word state: LDS, or (pass G) HBM written and read by the wave's own
@@ -1375,7 +1381,8 @@ __device__ __forceinline__ void m_count_word(SL& S, const MT& T, const A5xModeLa
       const u32 ntok = m_pos_setup(S, T, I, a.mode);
       if (ntok && a.mode == A5X_MODE_REVERSE) wb = I.count * (u64)(I.L + 1);
       else if (ntok && S.radix) wb = m_pos_prefix(S, I, I.count) - m_pos_prefix(S, I, 0);
-      if (wb != ~0ull && I.radix && !MF_OFF && S.nent <= MF_NE && ntok <= MF_TCAP) wb |= M_WB_FAST;
+      if (wb != ~0ull && I.radix && !MF_OFF && ntok <= MF_TCAP)
+        wb |= S.nent <= MF_NE ? M_WB_FAST : S.nent <= MF_NE2 ? M_WB_FAST2 : 0ull;
     }
     if (m_lane() == 0) a.wbytes[w] = wb;
   }
@@ -1482,7 +1489,8 @@ __global__ void __launch_bounds__(256) k_mode_count_thread(A5xModeLaunch a) {
       // m_pos_setup's table limits (entries of the patterns, then the literal chunks)
       const bool pos = L <= A5X_M_LMAX && npe <= MP_NE && npe + nlit <= MP_NE;
       if (pos && count > 0 && count <= a.SEG)
-        wb = bytes | (MF_OFF || npe + nlit > MF_NE || nocc + nlit > MF_TCAP ? 0ull : M_WB_FAST);
+        wb = bytes | (MF_OFF || nocc + nlit > MF_TCAP ? 0ull
+                      : npe + nlit <= MF_NE ? M_WB_FAST : npe + nlit <= MF_NE2 ? M_WB_FAST2 : 0ull);
       a.count[w] = count;
       a.nseg[w] = (count + a.SEG - 1) / a.SEG;
       a.flags[w] = 0;
@@ -1573,6 +1581,7 @@ constexpr uint8_t MI_POS = 1;       // positional: lengths done, ring expansion
 constexpr uint8_t MI_BUILD = 2;     // byte builder for the expansion, lengths done
 constexpr uint8_t MI_BUILD_LEN = 3; // byte builder for the lengths too
 constexpr uint8_t MI_FAST = 4;      // positional radix word: lengths done, piece engine
+constexpr uint8_t MI_FAST2 = 6;     // ... in the piece layout with more token entries (MLdsF2)
 constexpr uint8_t MI_SKIP = 5;      // -r FAST word (A5xModeLaunch::rfast): k_expand_fast writes it
 template <class SL>
 __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op) {
@@ -1625,7 +1634,8 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
       return;
     }
     if (m_lane() == 0)
-      a.item_fl[i] = ntok ? (I.radix && !MF_OFF && S.nent <= MF_NE && ntok <= MF_TCAP ? MI_FAST : MI_POS)
+      a.item_fl[i] = ntok ? (I.radix && !MF_OFF && ntok <= MF_TCAP && S.nent <= MF_NE2
+                                 ? (S.nent <= MF_NE ? MI_FAST : MI_FAST2) : MI_POS)
                           : a.mode == A5X_MODE_REVERSE ? MI_BUILD : MI_BUILD_LEN;
     if (!ntok && a.mode != A5X_MODE_REVERSE) return;  // lengths need the byte builder
     if (ntok && S.radix) {  // op 0, radix mode: closed form, no candidate is visited
@@ -1671,8 +1681,8 @@ __device__ __forceinline__ void m_items(const A5xModeLaunch& a, int op, uint8_t 
         take = a.item_fl[i] == route;
       } else if (op == 0 && a.wbytes[w] != ~0ull) {  // sized by k_mode_count (one item)
         const u64 wb = a.wbytes[w];
-        a.seg_bytes[i] = wb & ~M_WB_FAST;
-        a.item_fl[i] = (wb & M_WB_FAST) ? MI_FAST : MI_POS;
+        a.seg_bytes[i] = wb & ~(M_WB_FAST | M_WB_FAST2);
+        a.item_fl[i] = (wb & M_WB_FAST) ? MI_FAST : (wb & M_WB_FAST2) ? MI_FAST2 : MI_POS;
       } else {
         take = true;
       }
@@ -1685,6 +1695,7 @@ __global__ void __launch_bounds__(64) k_mode_items_len_b(A5xModeLaunch a) { m_it
 __global__ void __launch_bounds__(64) k_mode_items_pos(A5xModeLaunch a) { m_items<MLdsR>(a, 1, MI_POS); }
 __global__ void __launch_bounds__(64) k_mode_items_b(A5xModeLaunch a) { m_items<MLds>(a, 1, MI_BUILD); }
 __global__ void __launch_bounds__(64) k_mode_items_fast(A5xModeLaunch a) { m_items<MLdsF>(a, 1, MI_FAST); }
+__global__ void __launch_bounds__(64) k_mode_items_fast2(A5xModeLaunch a) { m_items<MLdsF2>(a, 1, MI_FAST2); }
 __global__ void __launch_bounds__(64) k_mode_digest_pos(A5xModeLaunch a) { m_items<MLdsR>(a, 2, 0); }
 __global__ void __launch_bounds__(64) k_mode_digest_b(A5xModeLaunch a) { m_items<MLds>(a, 2, MI_BUILD); }
 
@@ -1827,6 +1838,7 @@ hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st)
       hipLaunchKernelGGL(k_mode_items_len_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   } else if (op == 1) {
     hipLaunchKernelGGL(k_mode_items_fast, g, dim3(64), m_lds<MLdsF>(L.mtab_bytes), st, L);
+    hipLaunchKernelGGL(k_mode_items_fast2, g, dim3(64), m_lds<MLdsF2>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_items_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_items_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   } else {
