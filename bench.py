@@ -288,7 +288,7 @@ def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
     expand, hash and probe in one kernel, so the stage time is the expansion time.  The
     step's time is accounted as keyspace + stage (+ two-pass digest) + the rest (host)."""
     fused = ms_dig < 1e-3
-    kernel = (f"k_expand_fast_{args.digest}" if args.mode == 0 else "k_mode_digest_pos") if fused else "k_digest_stream"
+    kernel = (f"k_expand_fast_{args.digest}" if args.mode == 0 else "k_mode_digest_*") if fused else "k_digest_stream"
     ms_stage = ms_exp if fused else ms_dig
     prof = digest_profile(args.digest, args.words, kernel)
     peak = 256 * 4 * 32 * 2.4e9 / 1e12  # Tops/s

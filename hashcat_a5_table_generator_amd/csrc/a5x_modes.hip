@@ -1198,13 +1198,19 @@ __device__ __forceinline__ u64 m_fast_step(u64 sel, bool rev, u64 biasm) {
   return y | (biasm & (nf >= 16 ? ~0ull : (1ull << (4 * nf)) - 1ull));
 }
 
+__device__ __forceinline__ void m_digest_probe(const A5xModeLaunch& a, const uint8_t* base, u32 off, u32 len, bool on,
+                                               u64 w, u64 t);
+
 // Expand leaves [tb, te) of the radix word set up in S (pieces from m_piece_setup);
 // the first one's bytes start at a.out + pos0.  A round: 64 runs of MF_K leaves,
 // lengths -> wave scan -> the runs that fit the ring OR-place their pieces (piece-major:
 // one descriptor read per piece per run) -> complete 16-B blocks streamed out.
-template <class SL>
+// DIG (fused digest, op 2): the leaves are placed without their newline, every lane
+// hashes its run's leaves where they lie in the ring and probes the target set (hits
+// as (word w, leaf)), and the round's bytes are zeroed instead of streamed.
+template <class SL, bool DIG = false>
 __device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64 tb, u64 te, u64 pos0, u32 np,
-                              u64 biasm, u32& err) {
+                              u64 biasm, u32& err, u64 w = 0) {
   const u32 lane = m_lane();
   uint4* r4 = (uint4*)&S.buf[0];
   constexpr u32 RB = sizeof(S.buf) / 16;
@@ -1229,7 +1235,7 @@ __device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64
     for (int c = 1; c < MF_K; c++) sel[c] = m_fast_step(sel[c - 1], rev, biasm);
     u32 clen[MF_K], len = 0;
 #pragma unroll
-    for (int c = 0; c < MF_K; c++) clen[c] = (u32)c < nc ? (rev ? Lc : 1u) : 0u;
+    for (int c = 0; c < MF_K; c++) clen[c] = (u32)c < nc ? (rev ? Lc : 1u) - (DIG ? 1u : 0u) : 0u;
     if (!rev) {  // (leaves past the run read the empty entry: no per-leaf branches)
       for (u32 p = 0; p < np; p++) {
         const uint4 pd = S.pdesc[p];
@@ -1256,12 +1262,27 @@ __device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64
 #pragma unroll
         for (int c = 0; c < MF_K; c++) fx8_put(S.ent[(u32)c < nc ? m_piece_ix(pd, sel[c]) : SL::ZE], P1[c], nsl);
       }
+      if (!DIG) {
 #pragma unroll
-      for (int c = 0; c < MF_K; c++) fx8_put((u32)c < nc ? nl : make_uint4(0, 0, 0, 0), P1[c], 2u);
+        for (int c = 0; c < MF_K; c++) fx8_put((u32)c < nc ? nl : make_uint4(0, 0, 0, 0), P1[c], 2u);
+      }
     }
     pos += tot;
     rr += nact;
     M_WAVE_SYNC();
+    if constexpr (DIG) {  // hash the round's leaves in the ring, then zero its bytes
+      u32 off = used + incl - len;
+#pragma unroll
+      for (int c = 0; c < MF_K; c++) {
+        m_digest_probe(a, (const uint8_t*)r4, off, clen[c], fit && (u32)c < nc, w, t + c);
+        off += clen[c];
+      }
+      M_WAVE_SYNC();
+      for (u32 b = lane; b < (tot + 31u) / 16u && b < RB; b += 64) r4[b] = make_uint4(0, 0, 0, 0);
+      pos = B = 0;
+      M_WAVE_SYNC();
+      continue;
+    }
     const u32 nb = (u32)((pos - B) >> 4);
     if (B + 16ull * nb > a.out_cap) { err |= M_ERR_GUARD; return; }
     for (u32 b = lane; b < nb; b += 64) {
@@ -1593,13 +1614,18 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
   const MInfo I = m_setup(S, T, a, w);
   if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
   u32 err = 0, ntok = 0;
-  if constexpr (SL::FAST) {  // op 1 of MI_FAST items (the only route here)
-    ntok = op == 1 ? ((MF_ABL & 4) ? 1u : m_pos_setup(S, T, I, a.mode, false)) : 0u;
+  if constexpr (SL::FAST) {  // op 1 / op 2 (fused digest) of MI_FAST / MI_FAST2 items
+    ntok = op != 0 ? ((MF_ABL & 4) ? 1u : m_pos_setup(S, T, I, a.mode, false)) : 0u;
     if (!ntok) {
       err |= M_ERR_STATE;
     } else {
       u64 biasm = 0;
       const u32 np = (MF_ABL & 2) ? 0u : m_piece_setup(S, I, a.mode, ntok, biasm);
+      if (op == 2) {
+        m_fast_expand<SL, true>(S, I, a, t0, t0 + nc, 0, np, biasm, err, w);
+        m_err(a.err, m_wave_or(err));
+        return;
+      }
       const u64 rb = a.cand_begin > cw0 ? a.cand_begin - cw0 : 0;
       const u64 re = a.cand_end - cw0 < t0 + nc ? a.cand_end - cw0 : t0 + nc;  // (cand_end > cw0 here)
       const u64 tb = rb > t0 ? rb : t0;
@@ -1677,6 +1703,13 @@ __device__ __forceinline__ void m_items(const A5xModeLaunch& a, int op, uint8_t 
           a.seg_bytes[i] = a.mode == A5X_MODE_REVERSE ? nc * (a.woff[w + 1] - a.woff[w] + 1) : a.wbytes[w];
           a.item_fl[i] = MI_SKIP;
         }
+      } else if (op == 2) {
+        // fused digest: single-item words routed to a piece layout by k_mode_count (wbytes
+        // flags) go to that layout's kernel, every other item to k_mode_digest_pos (route
+        // 0), which marks the byte builder's (MI_BUILD) for k_mode_digest_b
+        const u64 wb = a.wbytes[w];
+        const uint8_t wr = wb == ~0ull ? 0 : (wb & M_WB_FAST) ? MI_FAST : (wb & M_WB_FAST2) ? MI_FAST2 : 0;
+        take = route == MI_BUILD ? wr == 0 && a.item_fl[i] == MI_BUILD : route ? wr == route : wr == 0;
       } else if (route) {
         take = a.item_fl[i] == route;
       } else if (op == 0 && a.wbytes[w] != ~0ull) {  // sized by k_mode_count (one item)
@@ -1697,6 +1730,8 @@ __global__ void __launch_bounds__(64) k_mode_items_b(A5xModeLaunch a) { m_items<
 __global__ void __launch_bounds__(64) k_mode_items_fast(A5xModeLaunch a) { m_items<MLdsF>(a, 1, MI_FAST); }
 __global__ void __launch_bounds__(64) k_mode_items_fast2(A5xModeLaunch a) { m_items<MLdsF2>(a, 1, MI_FAST2); }
 __global__ void __launch_bounds__(64) k_mode_digest_pos(A5xModeLaunch a) { m_items<MLdsR>(a, 2, 0); }
+__global__ void __launch_bounds__(64) k_mode_digest_fast(A5xModeLaunch a) { m_items<MLdsF>(a, 2, MI_FAST); }
+__global__ void __launch_bounds__(64) k_mode_digest_fast2(A5xModeLaunch a) { m_items<MLdsF2>(a, 2, MI_FAST2); }
 __global__ void __launch_bounds__(64) k_mode_digest_b(A5xModeLaunch a) { m_items<MLds>(a, 2, MI_BUILD); }
 
 // the items of the listed pass-G words inside [item_begin, item_end), dealt to the slots
@@ -1842,6 +1877,8 @@ hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st)
     hipLaunchKernelGGL(k_mode_items_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_items_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   } else {
+    hipLaunchKernelGGL(k_mode_digest_fast, g, dim3(64), m_lds<MLdsF>(L.mtab_bytes), st, L);
+    hipLaunchKernelGGL(k_mode_digest_fast2, g, dim3(64), m_lds<MLdsF2>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_digest_pos, g, dim3(64), m_lds<MLdsR>(L.mtab_bytes), st, L);
     hipLaunchKernelGGL(k_mode_digest_b, g, dim3(64), m_lds<MLds>(L.mtab_bytes), st, L);
   }
