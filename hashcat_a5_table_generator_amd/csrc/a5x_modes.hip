@@ -98,6 +98,9 @@ constexpr u32 MP_RING = 16 + 64 * A5X_M_CBUF + 48;
 #ifndef MF_NE2
 #define MF_NE2 128
 #endif
+#ifndef M_PREFETCH
+#define M_PREFETCH 1         // m_items: the next item's metadata and word bytes loaded under the current item
+#endif
 #ifndef MF_TCAP
 #define MF_TCAP 48           // tokens (and so pieces) per word in the piece layout; more: the token ring
 #endif
@@ -210,6 +213,12 @@ __device__ __forceinline__ u64 m_uniform64(u64 x) {
   return ((u64)hi << 32) | lo;
 }
 
+__device__ __forceinline__ u64 m_readlane64(u64 x, u32 l) {
+  const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)x, (int)l);
+  const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(x >> 32), (int)l);
+  return ((u64)hi << 32) | lo;
+}
+
 __device__ __forceinline__ MT m_table(uint8_t* lds, const uint8_t* g, u32 bytes) {
   // stage the mode table (16-B granules, the blob is 16-B padded by the host)
   const uint4* src = (const uint4*)g;
@@ -299,23 +308,38 @@ __device__ u32 m_replace_all(const uint8_t* src, u32 n, const uint8_t* p, u32 pl
   return o;
 }
 
+// An item's word metadata and bytes, loaded by m_items while the wave still runs the
+// previous item (the per-item chain of dependent global loads off the critical path):
+// w0 / w1 = woff[w], woff[w + 1]; c0 / c1 = cand_off[w], cand_off[w + 1]; s0 = seg_off[w];
+// b0 / b1 = word bytes lane and lane + 64.
+struct MPre {
+  u64 w0, w1, c0, c1, s0;
+  u32 b0, b1;
+};
+
 // Per-word setup (wave-uniform result): word -> LDS, the pattern / position list,
 // the DP table and the count.
 // dp = false: a radix word's count in closed form, no DP table (callers that never
 // unrank a leaf through it: k_mode_count)
 template <class SL>
-__device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w, bool dp = true) {
+__device__ MInfo m_setup(SL& S, const MT& T, const A5xModeLaunch& a, u64 w, bool dp = true,
+                         const MPre* pre = nullptr) {
   const u32 lane = m_lane();
   MInfo I;
   I.L = I.n = I.cmin = I.cmax = I.cols = 0;
   I.count = 0;
   I.bad = 0;
-  const u64 w0 = a.woff[w], w1 = a.woff[w + 1];
+  const u64 w0 = pre ? pre->w0 : a.woff[w], w1 = pre ? pre->w1 : a.woff[w + 1];
   if (w1 - w0 > SL::L_MAX) { I.bad = w1 - w0 <= A5X_MG_LMAX ? M_ERR_GWORD : M_ERR_LIMIT; return I; }
   const u32 L = (u32)(w1 - w0);
   I.L = L;
   m_sync<SL>();  // previous item's readers of S are done
-  for (u32 i = lane; i < L; i += 64) S.word[i] = a.words[w0 + i];
+  if (pre) {
+    if (lane < L) S.word[lane] = (uint8_t)pre->b0;
+    if (lane + 64 < L) S.word[lane + 64] = (uint8_t)pre->b1;
+  } else {
+    for (u32 i = lane; i < L; i += 64) S.word[i] = a.words[w0 + i];
+  }
   m_sync<SL>();
   u32 n = 0;
   if (a.mode == A5X_MODE_REVERSE) {
@@ -1605,13 +1629,13 @@ constexpr uint8_t MI_FAST = 4;      // positional radix word: lengths done, piec
 constexpr uint8_t MI_FAST2 = 6;     // ... in the piece layout with more token entries (MLdsF2)
 constexpr uint8_t MI_SKIP = 5;      // -r FAST word (A5xModeLaunch::rfast): k_expand_fast writes it
 template <class SL>
-__device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op) {
+__device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op, const MPre* pre = nullptr) {
   const u64 w = a.item_w[i];
-  const u64 cw0 = a.cand_off[w], cnt = a.cand_off[w + 1] - cw0;
-  const u64 t0 = (i - a.seg_off[w]) * a.SEG;
+  const u64 cw0 = pre ? pre->c0 : a.cand_off[w], cnt = (pre ? pre->c1 : a.cand_off[w + 1]) - cw0;
+  const u64 t0 = (i - (pre ? pre->s0 : a.seg_off[w])) * a.SEG;
   if (t0 >= cnt) { m_err(a.err, M_ERR_STATE); return; }
   const u32 nc = (u32)min(a.SEG, cnt - t0);
-  const MInfo I = m_setup(S, T, a, w);
+  const MInfo I = m_setup(S, T, a, w, true, pre);
   if (I.bad || I.count != cnt) { m_err(a.err, I.bad ? I.bad : M_ERR_STATE); return; }
   u32 err = 0, ntok = 0;
   if constexpr (SL::FAST) {  // op 1 / op 2 (fused digest) of MI_FAST / MI_FAST2 items
@@ -1720,7 +1744,36 @@ __device__ __forceinline__ void m_items(const A5xModeLaunch& a, int op, uint8_t 
         take = true;
       }
     }
-    for (u64 m = __ballot(take); m; m &= m - 1) m_item(S, T, a, b0 + (u64)__builtin_ctzll(m), op);
+    // the taken items' metadata, all loads together; each item's word bytes are loaded
+    // while the wave runs the item before it
+    u64 lw0 = 0, lw1 = 0, lc0 = 0, lc1 = 0, ls0 = 0;
+    if (take) {
+      const u64 w = a.item_w[i];
+      lw0 = a.woff[w]; lw1 = a.woff[w + 1];
+      lc0 = a.cand_off[w]; lc1 = a.cand_off[w + 1]; ls0 = a.seg_off[w];
+    }
+    u64 m = __ballot(take);
+    auto meta = [&](u32 l, MPre& P) {
+      P.w0 = m_readlane64(lw0, l); P.w1 = m_readlane64(lw1, l);
+      P.c0 = m_readlane64(lc0, l); P.c1 = m_readlane64(lc1, l); P.s0 = m_readlane64(ls0, l);
+      const u64 L = P.w1 - P.w0;
+      P.b0 = (L <= A5X_M_LMAX && lane < L) ? a.words[P.w0 + lane] : 0u;
+      P.b1 = (L <= A5X_M_LMAX && lane + 64 < L) ? a.words[P.w0 + lane + 64] : 0u;
+    };
+    if (!M_PREFETCH) {
+      for (; m; m &= m - 1) m_item(S, T, a, b0 + (u64)__builtin_ctzll(m), op);
+      continue;
+    }
+    MPre cur;
+    if (m) meta((u32)__builtin_ctzll(m), cur);
+    while (m) {
+      const u32 l = (u32)__builtin_ctzll(m);
+      m &= m - 1;
+      MPre nxt;
+      if (m) meta((u32)__builtin_ctzll(m), nxt);  // (consumed after this item: latency hidden)
+      m_item(S, T, a, b0 + l, op, &cur);
+      cur = nxt;
+    }
   }
 }
 __global__ void __launch_bounds__(64) k_mode_items_len(A5xModeLaunch a) { m_items<MLdsC>(a, 0, 0); }
