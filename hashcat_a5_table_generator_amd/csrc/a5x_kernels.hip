@@ -293,7 +293,9 @@ struct LWord {
   }
 };
 
+#ifndef KS_WB
 #define KS_WB 8192  // tile word bytes staged in LDS (larger tiles read global memory)
+#endif
 
 template <class W>
 __device__ __forceinline__ u32 ks_classify(const W& wd, u64 L64, const Tab& T, const KsArgs& a, WordClass& C) {
