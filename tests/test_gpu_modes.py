@@ -196,3 +196,39 @@ def test_reverse_negative_min_window():
     cnt, byt = c.keyspace(data, offs, 1, -3, -4)
     assert int(cnt.sum()) == 0 and int(byt.sum()) == 0
     c.close()
+
+
+@pytest.mark.parametrize("wl,tabs", [("c5", ["greek-hebrew"]), ("c3", ["czech", "german"])])
+@pytest.mark.parametrize("mode,mn", [(1, 0), (1, 1), (2, 0), (3, 1)])
+def test_mode_hits_regenerate_their_plains(wl, tabs, mode, mn):
+    """Every path numbers a word's candidates the same way: hits of the fused -r / -s /
+    -s -r digest (FAST-probe words in k_expand_fast_md5, piece-engine and token-ring words
+    in the mode kernels) come back through a5x_format_hits -- which regenerates each plain
+    from (word, candidate) on the expansion path (locate inside FAST words included) -- as
+    plains whose MD5 is the reported digest, every planted (word, candidate) found."""
+    import binascii
+    from hashcat_a5_table_generator_amd import Context, DeviceBuffer, pack_words, synth
+    _, (data, offs) = synth.global_words(wl, 0, 3000, seed=0xE5 + mode)
+    words = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in range(len(offs) - 1)]
+    rng = np.random.default_rng(11 + mode)
+    with Context(0) as ctx:
+        ctx.load_tables([table_path(t) for t in tabs])
+        cands = ctx.expand_words(words, mode, mn, 15)
+        planted = {}
+        for w in rng.choice(len(words), size=200, replace=False):
+            if cands[w]:
+                c = cands[w][int(rng.integers(0, len(cands[w])))]
+                planted[hashlib.md5(c).digest()] = c
+        ctx.set_targets(0, b"".join(planted))
+        d, o = pack_words(words)
+        dw, do = DeviceBuffer.from_array(ctx, d), DeviceBuffer.from_array(ctx, o)
+        hits, _ = ctx.expand_digest_device(dw.ptr, do.ptr, len(words), mode, mn, 15, hit_cap=1 << 14)
+        text = ctx.format_hits(d, o, hits, mode, mn, 15)
+    seen = set()
+    for line in text.split(b"\n")[:-1]:
+        hx, plain = line.split(b":", 1)
+        if plain.startswith(b"$HEX[") and plain.endswith(b"]"):
+            plain = binascii.unhexlify(plain[5:-1])
+        assert hashlib.md5(plain).hexdigest().encode() == hx, line
+        seen.add(bytes.fromhex(hx.decode()))
+    assert set(planted) <= seen
