@@ -1428,6 +1428,9 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #ifndef FX_NOOR
 #define FX_OR         // OR placement into a zeroed ring (a5x_fx6.h fx7_round)
 #endif
+#ifndef FX_HOLESKIP
+#define FX_HOLESKIP 0 // 1: skip a run of hole words in one window step (A/B: C5 -s -1 %, C3 +0.8 %: off)
+#endif
 #ifndef FX_DABL
 #define FX_DABL 0     // fused-digest ablations (variant builds, wrong hits): 1 no MD rounds, 2 no probe
 #endif
@@ -1812,14 +1815,31 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     const u64 badm = __ballot(!ok);
     u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
     STAMP(0);
-    if (k == 0) {
-      // word w is a hole here (slow / BIG) or empty
+#if !FX_HOLESKIP
+    if (k == 0) {  // (A/B: one hole word per step)
       const u64 w0c1 = uniform64(c1);
       if (w0c1 > g && w0c1 != ~0ull) {
         if (!DIG) fx_close(R, ring, a);
         g = min(w0c1, g1);
       }
       w++;
+      M = fx_meta(a, w);
+      continue;
+    }
+#endif
+    if (k == 0) {
+      // word w is a hole here (slow / BIG / a mode-engine word) or empty: skip every loaded
+      // word before the next FAST word with candidates in one step (holes come in runs
+      // when the mode engines share the batch)
+      const u64 fmk = __ballot(fast && hasc);
+      const u64 vmk = __ballot(c0 != ~0ull);
+      const u32 ns = fmk ? (u32)__builtin_ctzll(fmk) : (vmk ? 64u - (u32)__builtin_clzll(vmk) : 1u);
+      const u64 cend = uniform64(shfl_u64(c1, (int)(ns ? ns - 1u : 0u)));
+      if (cend > g && cend != ~0ull) {
+        if (!DIG) fx_close(R, ring, a);
+        g = min(cend, g1);
+      }
+      w += ns ? ns : 1u;
       M = fx_meta(a, w);
       continue;
     }
