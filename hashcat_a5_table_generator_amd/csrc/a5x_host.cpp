@@ -135,7 +135,8 @@ struct a5x_ctx {
   // k_expand_fast (disjoint output bytes), joined back before the range completes
   hipStream_t sstream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  uint64_t seg = 1024;        // candidates per per-word-path segment (a radix round there costs ~64x a FAST one)
+  uint64_t seg = 512;         // candidates per per-word-path segment (a radix round there costs ~64x a FAST one;
+                              // C3 A/B: 512 / 256 -1 %, 4096 +8 %, 16384 +44 % -- the slow words run beside k_expand_fast)
   uint64_t chunk = 8192;      // candidates per expand wave (sweep on C3: 8192 < 16384 < 32768 ms)
   uint32_t waves_per_block = 4;
   uint32_t waves_per_block_fast = 1;
