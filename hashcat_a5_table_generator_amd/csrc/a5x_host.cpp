@@ -1394,7 +1394,8 @@ int a5x_create(int device, a5x_ctx** out) {
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_MSEG")) c->mseg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_SEG")) c->seg = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
-  if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
+  // (k_expand_slow is built for <= 256 threads per workgroup: __launch_bounds__(256))
+  if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(4u, (unsigned)atoi(e)));
   if (const char* e = getenv("A5X_FAST_WAVES")) c->waves_per_block_fast = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   *out = c;
   return A5X_OK;

@@ -2311,7 +2311,10 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   const u64 c0 = L.cand_begin / L.CH, c1 = (L.cand_end + L.CH - 1) / L.CH;
   const u64 nchunks = c1 - c0;
   if (nchunks == 0) return hipSuccess;
-  const u32 waves = kind == 0 ? L.waves_per_block_fast : L.waves_per_block;
+  u32 waves = kind == 0 ? L.waves_per_block_fast : L.waves_per_block;
+  // (A5X_WAVES beyond what the layout fits in a workgroup's 64 KiB of dynamic LDS: fewer waves)
+  const int lk = kind == 1 ? 1 : kind == 2 ? 2 : 0;
+  while (waves > 1 && a5x_expand_lds(L.table_bytes, lk, waves) > 65536) waves--;
   const u64 nb = (nchunks + waves - 1) / waves;
   if (kind == 0)
     hipLaunchKernelGGL(k_expand_fast, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);
