@@ -58,10 +58,13 @@ def _digests(dump):
     return parts[0][0], parts[-1][1], np.concatenate([p[2] for p in parts])
 
 
-def test_two_ranks_expand_equals_one_rank(tmp_path):
-    """C3 words: 2 ranks x 30k words per rank == 1 rank x 60k words, per-word digests."""
-    r2 = _bench(2, ["--workload", "c3", "--words", "30000"], tmp_path / "w2")
-    r1 = _bench(1, ["--workload", "c3", "--words", "60000"], tmp_path / "w1")
+@pytest.mark.parametrize("wl,mode", [("c3", 0), ("c5", 1), ("c5", 3)])
+def test_two_ranks_expand_equals_one_rank(tmp_path, wl, mode):
+    """2 ranks x 30k words per rank == 1 rank x 60k words, per-word digests: C3 in the
+    default mode, C5 in -r (FAST-probe words) and -s -r (piece engine + FAST probe)."""
+    args = ["--workload", wl, "--mode", str(mode), "--steady-batches", "0"]
+    r2 = _bench(2, args + ["--words", "30000"], tmp_path / "w2")
+    r1 = _bench(1, args + ["--words", "60000"], tmp_path / "w1")
     a0, a1, d2 = _digests(tmp_path / "w2")
     b0, b1, d1 = _digests(tmp_path / "w1")
     assert (a0, a1) == (b0, b1) == (0, 60000)
