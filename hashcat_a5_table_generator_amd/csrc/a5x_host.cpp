@@ -97,6 +97,8 @@ struct a5x_ctx {
   DevBuf<uint8_t> hy_words;
   uint8_t* mgscr = nullptr;   // mode pass G scratch: A5X_G_SLOTS x a5x_mode_gslot_bytes(), on first use
   uint64_t mseg = 4096;  // candidates per mode-engine item (C5 -r: most words one item, sized by k_mode_count)
+  uint64_t rov_need = 0;  // -r/-s FAST probe: overflow slots a previous batch needed (k_keyspace_rprobe)
+  uint64_t cplx_need = 0;  // default mode: complex-word record slots a previous batch needed
   // fused digest + lookup (a5x_digest.hip)
   int t_algo = -1;
   uint64_t n_targets = 0;
@@ -410,7 +412,8 @@ int decode_dev_err(a5x_ctx* c, uint32_t e) {
 }
 
 // words with overlapping keys (or other irregular shapes) whose FAST records go to
-// fixed slots after the tile regions: at most this many per batch (the rest: slow path)
+// fixed slots after the tile regions: this many slots at first (a batch with more complex
+// words grows them and runs its keyspace again, run_keyspace)
 uint32_t ks_cplx_cap(uint64_t nw) { return (uint32_t)std::min<uint64_t>(nw / 16 + 1024, 1u << 22); }
 
 struct Batch {  // device-side per-batch state after keyspace
@@ -429,12 +432,18 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   int rc;
   if ((rc = upload_table(c))) return rc;
   if (nw > 0xffffffffull) return fail(c, A5X_E_ARG, "batch of %llu words (max 2^32-1)", (unsigned long long)nw);
+  // FAST record slots of the complex words (k_keyspace_cplx): enough for every one of them,
+  // so whether a word is FAST (and how its candidates are numbered) never depends on how
+  // many complex words share its batch; u32 record offsets bound the whole record area
+  const uint64_t ccap = std::min<uint64_t>(nw + 1, std::max<uint64_t>(ks_cplx_cap(nw), c->cplx_need));
+  if (((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC + ccap * FW_RMAX > 0xffffffffull)
+    return fail(c, A5X_E_ARG, "batch of %llu words is too large for one call (FAST record index; split it)",
+                (unsigned long long)nw);
   if ((rc = grow(c, c->count, nw + 1)) || (rc = grow(c, c->bytes, nw + 1)) || (rc = grow(c, c->flags, nw + 1)) ||
       (rc = grow(c, c->defer, nw + 1)) || (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(nw + 1) + 16)) ||
       (rc = grow(c, c->roff, nw + 1)) || (rc = grow(c, c->cplx, nw + 1)) ||
       (rc = grow(c, c->slow_list, nw + 1)) || (rc = grow(c, c->big_list, nw + 1)) || (rc = grow(c, c->glob, nw + 1)) ||
-      (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC +
-                                (uint64_t)ks_cplx_cap(nw) * FW_RMAX + 2)))
+      (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC + ccap * FW_RMAX + 2)))
     return rc;
   if (!d_cand_off) {
     if ((rc = grow(c, c->cand_off, nw + 1))) return rc;
@@ -455,7 +464,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
     K.nslow = c->d_scalars + 3;
     K.slow_list = c->slow_list.p; K.big_list = c->big_list.p;
     K.rec = c->rec.p; K.roff = c->roff.p;
-    K.cplx_list = c->cplx.p; K.cplx_n = c->d_scalars + 4; K.cplx_cap = ks_cplx_cap(nw);
+    K.cplx_list = c->cplx.p; K.cplx_n = c->d_scalars + 4; K.cplx_cap = (uint32_t)ccap;
     K.cplx_base = ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC;
     K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nw, (uint64_t)c->cus * 4));
     K.glob_list = c->glob.p; K.glob_n = c->d_scalars + 7;
@@ -471,6 +480,11 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
   }
   HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  if (nw > 0 && c->h_scalars[4] > ccap) {
+    // more complex words than record slots: room for all of them, and the keyspace again
+    c->cplx_need = c->h_scalars[4];
+    return run_keyspace(c, d_words, d_woff, nw, mn, mx, d_cand_off, d_byte_off, st, B, timed);
+  }
   if (nw > 0 && c->h_scalars[2] == 0 && c->h_scalars[7] > 0) {
     // pass G: words beyond the pass-B LDS budget are sized in HBM scratch slots (their
     // counts were 0 in the first scan), then the scan runs again
@@ -705,9 +719,15 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   const bool mct = (mode == A5X_MODE_SUBALL || mode == A5X_MODE_SUBALL_REVERSE) && mx >= 0 && !has_empty &&
                    !getenv("A5X_NO_MCT");
   if ((rfast || mct) && ((rc = grow(c, c->m_cl, nw + 1)) || (rc = grow(c, c->m_cl2, nw + 1)))) return rc;
+  // (the probe's overflow slots: words a keyspace tile could not decide, k_keyspace_rprobe)
+  const uint64_t rtiles = ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC;
+  const uint64_t rcap = std::min<uint64_t>(nw, std::max<uint64_t>(ks_cplx_cap(nw), c->rov_need));
   if (rfast) {
-    if ((rc = grow(c, c->roff, nw + 1)) ||
-        (rc = grow(c, c->rec, ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC + 2)))
+    if (rtiles + rcap * FW_RMAX > 0xffffffffull)  // (u32 record offsets)
+      return fail(c, A5X_E_ARG, "batch of %llu words is too large for one -r/-s call (FAST record index)",
+                  (unsigned long long)nw);
+    if ((rc = grow(c, c->roff, nw + 1)) || (rc = grow(c, c->cplx, nw + 1)) ||
+        (rc = grow(c, c->rec, rtiles + rcap * FW_RMAX + 2)))
       return rc;
     A5xKsLaunch K;
     memset(&K, 0, sizeof K);
@@ -716,6 +736,8 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     K.err = c->d_scalars + 2; K.rec = c->rec.p; K.roff = c->roff.p;
     K.rmode = mode; K.rcmin = mn > 0 ? 1u : 0u; K.rnseg = c->m_nseg.p; K.rseg = c->mseg;
     K.defer_list = c->m_cl.p; K.defer_n = c->d_scalars + 12;
+    K.cplx_list = c->cplx.p; K.cplx_n = c->d_scalars + 14; K.cplx_cap = (uint32_t)rcap; K.cplx_base = rtiles;
+    K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nw + 255) / 256, (uint64_t)c->cus * 2));
     HIPCHK(c, a5x_launch_keyspace(K, st));
   }
   A5xModeLaunch M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx, rfast);
@@ -736,6 +758,12 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   HIPCHK(c, hipMemcpyAsync(c->h_totals + 1, c->m_seg_off.p + nw, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, 64, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  if (rfast && c->h_scalars[14] > rcap) {
+    // more undecided words than overflow slots: grow to fit them all and run again (the
+    // undecided tail was left uncounted, so nothing of this pass is used)
+    c->rov_need = c->h_scalars[14];
+    return run_keyspace_mode(c, d_words, d_woff, nw, mode, mn, mx, d_cand_off, d_byte_off, st, B, timed, lengths);
+  }
   B->nmode = rfast ? c->h_scalars[12] : nw;
   if (c->h_scalars[2] == 0 && c->h_scalars[7] > 0) {
     // mode pass G: words longer than the LDS engines take are counted in HBM scratch
@@ -1394,8 +1422,8 @@ int a5x_create(int device, a5x_ctx** out) {
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_MSEG")) c->mseg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_SEG")) c->seg = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
-  // (k_expand_slow is built for <= 256 threads per workgroup: __launch_bounds__(256))
-  if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(4u, (unsigned)atoi(e)));
+  // (tuning knobs; a5x_launch_expand clamps each launch to the kernel's compiled launch bound)
+  if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   if (const char* e = getenv("A5X_FAST_WAVES")) c->waves_per_block_fast = std::max(1u, std::min(16u, (unsigned)atoi(e)));
   *out = c;
   return A5X_OK;

@@ -513,15 +513,22 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       f = rm ? 0u : C.clusters ? A5X_WF_DEFER : (f & (A5X_WF_RADIX | A5X_WF_BIN));
     }
     if (rm) {
-      const bool kept = valid && (f & A5X_WF_FAST) != 0;
+      // Whether a word is FAST must not depend on its tile (hit numbering, FAST order vs the
+      // mode engine's, is per word: a5x_format_hits re-runs a sub-batch, shards re-tile): a
+      // word of an unstaged tile, or one past the tile's record budget, is listed for
+      // k_keyspace_rprobe, which probes it alone and plans it into a fixed overflow slot.
+      const bool rov = (valid && !longw && !trivial && !staged) || (fast && !build);
+      const bool kept = valid && !rov && (f & A5X_WF_FAST) != 0;
       if (valid) {
         a.count[w] = kept ? C.count : 0ull;
         a.bytes[w] = kept ? C.bytes : 0ull;
         a.flags[w] = kept ? f : 0u;
         a.rnseg[w] = kept ? (C.count + a.rseg - 1) / a.rseg : 0ull;
       }
-      const u32 mi = wave_append(valid && !kept, a.defer_n);  // the mode engine's words
-      if (valid && !kept) a.defer_list[mi] = (u32)w;
+      const u32 ri = wave_append(rov, a.cplx_n);
+      if (rov) a.cplx_list[ri] = (u32)w;
+      const u32 mi = wave_append(valid && !kept && !rov, a.defer_n);  // the mode engine's words
+      if (valid && !kept && !rov) a.defer_list[mi] = (u32)w;
       __syncthreads();
       continue;
     }
@@ -540,6 +547,88 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       a.flags[w] = f;
     }
     __syncthreads();  // wb / wsum are rewritten by the next tile
+  }
+}
+
+#define RP_SLOT 80  // k_keyspace_rprobe: per-lane LDS word slot (words <= A5X_LMAX_A bytes + over-read)
+
+// The -r / -s / -s -r FAST probe of the words k_keyspace_thread could not decide inside
+// its tile (an unstaged tile, or the tile's record budget spent), one lane per listed
+// word with the word copied to the lane's own LDS slot: the same count walk, mode_unit
+// qualification, closed form and plan as there, so a word is FAST (and numbered in FAST
+// order) whatever batch it is in.  Records go to slot i of cplx_base; a list longer
+// than cplx_cap leaves its tail undecided (count 0) and the host reruns the keyspace
+// with room for all (a5x_host.cpp run_keyspace_mode).
+__global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const u32 tb = (a.table_bytes + 15u) & ~15u;
+  u64* gbuf = (u64*)(smem + tb);                           // 256 x KS_GCAP open-group entries
+  uint8_t* slots = smem + tb + 256 * KS_GCAP * 8;          // 256 x RP_SLOT word bytes
+  load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  const u32 bmax = T.hdr->max_bucket;
+  const u32 tid = threadIdx.x;
+  const u32 n = *a.cplx_n;
+  for (u32 b0 = blockIdx.x * 256u; b0 < n; b0 += gridDim.x * 256u) {
+    const u32 i = b0 + tid;
+    const bool valid = i < n && i < a.cplx_cap;
+    const u64 w = valid ? a.cplx_list[i] : 0ull;
+    const u64 s = valid ? a.woff[w] : 0ull;
+    const u32 L = valid ? (u32)(a.woff[w + 1] - s) : 0u;  // <= A5X_LMAX_A (longer words never listed)
+    u32* sl = (u32*)(slots + tid * RP_SLOT);
+    for (u32 q = 0; q < RP_SLOT / 4; q++) {
+      u32 v = 0;
+      for (u32 bb = 0; bb < 4; bb++)
+        if (4 * q + bb < L) v |= (u32)a.words[s + 4 * q + bb] << (8 * bb);
+      sl[q] = v;
+    }
+    LWord lw;
+    lw.base = slots; lw.off = tid * RP_SLOT;
+    CountAcc A;
+    count_init(A, L);
+    NullSink ns;
+    Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
+    bool cplx = false;
+    psk_walk<true>(lw, L, valid, wave_max_u32(L), bmax, T, pl, A, cplx, a.rmode);
+    WordClass C;
+    C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
+    u32 f = 0;
+    if (valid && !cplx) {
+      pl.finish(L);
+      C = classify_finish(A, pl.P, L, a.mn, a.mx, A5X_RING_A - 16);
+      f = C.flags;
+      if (C.ovf) atomicOr(a.err, A5X_DERR_OVF);
+      if ((f & A5X_WF_DEFER) || !(f & (A5X_WF_FAST | A5X_WF_RADIX | A5X_WF_ERR_OVF))) f = A5X_WF_DEFER;
+    }
+    const u64 cnt = A.P - a.rcmin;
+    const bool rf = valid && !cplx && (f & A5X_WF_FAST) && !(f & A5X_WF_DEFER) && A.nunits > 0 && C.count > 0 &&
+                    (a.rmode == 1 || cnt <= a.rseg);
+    u64* rec = a.rec + a.cplx_base + (u64)i * FW_RMAX;
+    {
+      DevRecSink sk;
+      sk.g = gbuf + tid; sk.c = sk.g; sk.rec = rec; sk.np = ff_np(f);
+      Planner<true, LWord, DevRecSink, KS_GCAP> pb(lw, T, sk, rf ? fb_balanced_cap(C.count + 1) : 0u);
+      CountAcc A2;
+      bool c2 = false;
+      psk_walk<false>(lw, L, rf, wave_max_u32(rf ? L : 0u), bmax, T, pb, A2, c2, a.rmode);
+      if (rf) {
+        pb.finish(L);
+        pb.pick_balanced();
+        const Plan& P = pb.P;
+        rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
+        if (c2 || !P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
+        a.roff[w] = (u32)(a.cplx_base + (u64)i * FW_RMAX);
+      }
+    }
+    if (valid) {
+      a.count[w] = rf ? cnt : 0ull;
+      a.bytes[w] = rf ? C.bytes + (a.rcmin ? 0ull : (u64)(L + 1)) : 0ull;
+      a.flags[w] = rf ? f : 0u;
+      a.rnseg[w] = rf ? (cnt + a.rseg - 1) / a.rseg : 0ull;
+    }
+    const u32 mi = wave_append(valid && !rf, a.defer_n);  // the mode engine's words
+    if (valid && !rf) a.defer_list[mi] = (u32)w;
   }
 }
 
@@ -2216,7 +2305,12 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   a.rmode = L.rmode; a.rcmin = L.rcmin; a.rnseg = L.rnseg; a.rseg = L.rseg;
   hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || L.rmode) return e;  // -r FAST probe: k_keyspace_thread only
+  if (e != hipSuccess) return e;
+  if (L.rmode) {  // -r / -s / -s -r FAST probe: k_keyspace_thread + the words it listed
+    hipLaunchKernelGGL(k_keyspace_rprobe, dim3(L.defer_blocks), dim3(256), a5x_keyspace_rprobe_lds(L.table_bytes), st,
+                       a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_keyspace_cplx, dim3(L.defer_blocks), dim3(256),
                      ((L.table_bytes + 15u) & ~15u) + 2 * 256 * FW_UMAXR * 8 + 256 * KC_SLOT, st, a);
   e = hipGetLastError();
@@ -2241,6 +2335,10 @@ hipError_t a5x_launch_keyspace_g(const A5xKsLaunch& L, hipStream_t st) {
 
 size_t a5x_keyspace_thread_lds(u32 table_bytes) {
   return ((table_bytes + 15u) & ~15u) + FW_TILE * KS_GCAP * 8 + 64 + KS_WB + 32 + FW_TILE * KS_ULOG * 2;
+}
+
+size_t a5x_keyspace_rprobe_lds(u32 table_bytes) {
+  return ((table_bytes + 15u) & ~15u) + 256 * KS_GCAP * 8 + 256 * RP_SLOT;
 }
 
 size_t a5x_keyspace_wave_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + sizeof(LdsB); }
@@ -2305,6 +2403,13 @@ size_t a5x_expand_lds(u32 table_bytes, int kind, u32 waves) {
   return waves * ((FX_RING + FX_TRASH + sizeof(FXWin) + 15u) & ~(size_t)15u);
 }
 
+// waves per workgroup a kernel admits: its compiled maxThreadsPerBlock / 64 (>= 1)
+u32 a5x_max_waves(const void* fn) {
+  hipFuncAttributes at;
+  if (hipFuncGetAttributes(&at, fn) != hipSuccess || at.maxThreadsPerBlock < 64) return 1u;
+  return (u32)at.maxThreadsPerBlock / 64u;
+}
+
 // kind 0: k_expand_fast, 1: k_expand_slow, 2: k_expand_b, 3 / 5: k_expand_fast_md5 / _ntlm (fused digest)
 hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   ExpArgs a = exp_args(L);
@@ -2315,6 +2420,13 @@ hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st) {
   // (A5X_WAVES beyond what the layout fits in a workgroup's 64 KiB of dynamic LDS: fewer waves)
   const int lk = kind == 1 ? 1 : kind == 2 ? 2 : 0;
   while (waves > 1 && a5x_expand_lds(L.table_bytes, lk, waves) > 65536) waves--;
+  // ... and never more threads than the kernel was compiled for (its __launch_bounds__):
+  // a larger workgroup fails to launch ("unspecified launch failure")
+  const void* fn = kind == 0 ? (const void*)k_expand_fast : kind == 3 ? (const void*)k_expand_fast_md5
+                 : kind == 5 ? (const void*)k_expand_fast_ntlm : kind == 1 ? (const void*)k_expand_slow
+                 : kind == 2 ? (const void*)k_expand_b : (const void*)k_expand_g;
+  const u32 wmax = a5x_max_waves(fn);
+  if (waves > wmax) waves = wmax;
   const u64 nb = (nchunks + waves - 1) / waves;
   if (kind == 0)
     hipLaunchKernelGGL(k_expand_fast, dim3((u32)nb), dim3(64 * waves), a5x_expand_lds(L.table_bytes, 0, waves), st, a);
@@ -2374,6 +2486,8 @@ hipError_t a5x_set_kernel_attrs() {
   e = hipFuncSetAttribute((const void*)k_keyspace_thread, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_keyspace_cplx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_keyspace_rprobe, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_locate, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;

@@ -32,8 +32,9 @@ struct A5xKsLaunch {
   uint32_t* glob_n;
   uint8_t* gscr;        // pass G scratch: gslots x a5x_gslot_bytes() (ring zeroed)
   uint32_t gslots;
-  int rmode;            // 1 / 2 / 3: -r / -s / -s -r FAST probe (k_keyspace_thread only, mode_unit);
-                        // the other words are listed in defer_list / defer_n
+  int rmode;            // 1 / 2 / 3: -r / -s / -s -r FAST probe (k_keyspace_thread, mode_unit, then
+                        // k_keyspace_rprobe over the words a tile could not decide: cplx_list,
+                        // records in cplx slots); the other words are listed in defer_list / defer_n
   uint32_t rcmin;       // -r: max(min, 0)
   uint64_t* rnseg;      // -r: per FAST word, ceil(count / rseg) mode-engine items
   uint64_t rseg;
@@ -88,6 +89,7 @@ int a5x_read_stamps(unsigned long long* out16, int reset);
 hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st);
 size_t a5x_keyspace_wave_lds(uint32_t table_bytes);
 size_t a5x_keyspace_thread_lds(uint32_t table_bytes);
+size_t a5x_keyspace_rprobe_lds(uint32_t table_bytes);
 uint64_t a5x_scan_tmp_elems(uint64_t n);
 hipError_t a5x_launch_scan(const uint64_t* ca, const uint64_t* cb, uint64_t n, uint64_t* outa, uint64_t* outb,
                            uint64_t* tmp, uint32_t* err, hipStream_t st);

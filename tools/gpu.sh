@@ -51,7 +51,7 @@ PY
 
 step_test() {
   timeout -k 10 ${TT:-600} python -u -m pytest ${TESTS:-tests/} -v -m gpu -x ${K:+-k "$K"} --timeout ${TTO:-200} \
-    --timeout-method thread > gpurun_out/test_$T.log 2>&1
+    --timeout-method thread -rA --junitxml gpurun_out/junit_$T.xml > gpurun_out/test_$T.log 2>&1
   local rc=$?
   echo "pytest rc=$rc"; tail -2 gpurun_out/test_$T.log
   [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/test_$T.log | head -8; return 10; }
