@@ -128,29 +128,40 @@ PARALLELISM = ("partition: one global list of words_per_gpu x {world} words, spl
                "no data-path collective")
 
 
-def shard_for_rank(args, D, ctx):
+def shard_for_rank(args, D, ctx, intra_word=True):
     """This rank's shard of ONE global list of words_per_gpu x N words (north_star (e),
-    main.go:70-95 data parallelism): every rank keyspaces an equal word-count block,
-    and the balanced split by output bytes (a5x_partition semantics) comes from one
-    all-gather of block totals + one all-reduce(MIN) (dist.distributed_split).  Returns
-    (tables, data, offs, (w0, w1))."""
+    main.go:70-95 data parallelism): every rank keyspaces an equal word-count block, and
+    the balanced split by output bytes comes from one all-gather of block totals + one
+    all-reduce(MIN).  intra_word: the split points are candidates, found
+    exactly on the device (a5x_split_device / a5x_locate_device), so a word larger than a
+    rank's share is cut inside (dist.candidate_split); else word boundaries
+    (dist.distributed_split, a5x_partition semantics: the fused-digest path).
+    Returns (tables, data, offs, (w0, w1), (cand_begin, cand_count)) -- candidates of the
+    local batch [w0, w1); (0, None) = all of them."""
     from hashcat_a5_table_generator_amd import DeviceBuffer, dist as hd, synth
     n_total = args.words * D.world
     b0, b1 = hd.block_bounds(n_total, D.world, D.rank)
     tables, (bd, bo) = synth.global_words(args.workload, b0, b1, seed=SEED)
     if D.world == 1:
-        return tables, bd, bo, (0, n_total)
+        return tables, bd, bo, (0, n_total), (0, None)
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw, do = DeviceBuffer.from_array(ctx, bd), DeviceBuffer.from_array(ctx, bo)
     lp = DeviceBuffer(ctx, (b1 - b0 + 1) * 8)
-    ctx.keyspace_device(dw.ptr, do.ptr, b1 - b0, args.mode, args.min, args.max, d_byte_off=lp.ptr)
-    split = hd.distributed_split(D.dist, lp.to_array(np.uint64, count=b1 - b0 + 1), b0, n_total, D.world, D.backend)
+    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, b1 - b0, args.mode, args.min, args.max, d_byte_off=lp.ptr)
+    if intra_word:
+        def split_fn(targets):
+            g, w, c = ctx.split_device(dw.ptr, do.ptr, b1 - b0, targets, args.mode, args.min, args.max)
+            return g, w, c, ctx.locate_device(dw.ptr, do.ptr, b1 - b0, g, args.mode, args.min, args.max)
+        split = hd.candidate_split(D.dist, tc, tb, b0, n_total, D.world, split_fn, D.backend)
+        w0, w1, c0, ncand, _, nbytes = hd.shard_of(split, D.rank)
+    else:
+        ws = hd.distributed_split(D.dist, lp.to_array(np.uint64, count=b1 - b0 + 1), b0, n_total, D.world, D.backend)
+        w0, w1, c0, ncand = int(ws[D.rank]), int(ws[D.rank + 1]), 0, None
     for b in (dw, do, lp):
         b.free()
     ctx.clear_table()
-    w0, w1 = int(split[D.rank]), int(split[D.rank + 1])
     _, (data, offs) = synth.global_words(args.workload, w0, w1, seed=SEED)
-    return tables, data, offs, (w0, w1)
+    return tables, data, offs, (w0, w1), (c0, ncand)
 
 
 def kernel_src_sha() -> str:
@@ -298,11 +309,14 @@ def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
          "ms_step_unaccounted": ms_step - ms_ks - ms_exp - (0.0 if fused else ms_dig),
          "digest_cand_per_s": tc / (ms_stage * 1e-3), "achieved": None, "frac": None, "profile": None}
     if prof:
-        ach = prof["int_ops_per_cand"] * tc / (ms_stage * 1e-3) / 1e12
-        r.update(achieved=ach, frac=ach / peak, int_ops_per_cand=prof["int_ops_per_cand"],
-                 valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"),
-                 profile=f"{prof['_file']} (kernel_src_sha {prof['kernel_src_sha'][:12]}"
+        r.update(profile=f"{prof['_file']} (kernel_src_sha {prof['kernel_src_sha'][:12]}"
                          f"{'' if prof['_sha_match'] else ', an earlier source revision'})")
+        if prof["_sha_match"]:  # int ops per candidate count only for the sources they were measured on
+            ach = prof["int_ops_per_cand"] * tc / (ms_stage * 1e-3) / 1e12
+            r.update(achieved=ach, frac=ach / peak, int_ops_per_cand=prof["int_ops_per_cand"],
+                     valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"))
+        else:
+            r.update(frac_from_stale_profile=True, stale_int_ops_per_cand=prof["int_ops_per_cand"])
     return r
 
 
@@ -359,7 +373,8 @@ def run_digest(args, D):
     from hashcat_a5_table_generator_amd import ALGO_MD5, ALGO_NTLM, Context, DeviceBuffer, dist as hd, synth
     algo = ALGO_MD5 if args.digest == "md5" else ALGO_NTLM
     ctx = Context(D.device)
-    tables, data, offs, (w0, w1) = shard_for_rank(args, D, ctx)
+    # (word-granular shards: a5x_expand_digest_device takes whole batches)
+    tables, data, offs, (w0, w1), _ = shard_for_rank(args, D, ctx, intra_word=False)
     n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)
@@ -582,18 +597,24 @@ def main():
     from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
 
     ctx = Context(D.device)
-    tables, data, offs, (w0, w1) = shard_for_rank(args, D, ctx)
+    tables, data, offs, (w0, w1), (cb, ncand) = shard_for_rank(args, D, ctx)
     n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)
     do = DeviceBuffer.from_array(ctx, offs)
-    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max)
-    log(f"rank {D.rank}: {ctx.device_name}: words [{w0}, {w1}) -> {tc} candidates, {tb / 1e9:.2f} GB")
+    tc_all, tb_all = ctx.keyspace_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max)
+    ce = tc_all if ncand is None else cb + ncand
+    rb, re_ = (0, tb_all) if (cb, ce) == (0, tc_all) else \
+        (int(x) for x in ctx.locate_device(dw.ptr, do.ptr, n, [cb, ce], args.mode, args.min, args.max))
+    tc, tb = ce - cb, re_ - rb  # this rank's candidates / bytes (the shard may cut words)
+    log(f"rank {D.rank}: {ctx.device_name}: words [{w0}, {w1}) candidates [{cb}, {ce}) of the local batch -> "
+        f"{tc} candidates, {tb / 1e9:.2f} GB")
     out = DeviceBuffer(ctx, max(tb, 16))
     boff = DeviceBuffer(ctx, (n + 1) * 8)
 
     def step():
-        return ctx.expand_device(dw.ptr, do.ptr, n, out.ptr, tb, args.mode, args.min, args.max, d_byte_off=boff.ptr)
+        return ctx.expand_device(dw.ptr, do.ptr, n, out.ptr, tb, args.mode, args.min, args.max, cand_begin=cb,
+                                 cand_end=ce, d_byte_off=boff.ptr)
 
     for _ in range(args.warmup):
         step()
@@ -606,18 +627,28 @@ def main():
     dt = time.perf_counter() - t0
     dt_max = D.reduce(dt, "max")
     cands_all = D.reduce(float(tc) * args.steps, "sum")
+    bytes_per_rank = [tb] if D.world == 1 else \
+        [int(x) for x in __import__("hashcat_a5_table_generator_amd.dist", fromlist=["x"]).allgather_u64(
+            D.dist, [tb], D.backend)[:, 0]]
     ms_exp = float(np.mean([s["ms_expand"] for s in stats]))
     ms_ks = float(np.mean([s["ms_keyspace"] for s in stats]))
     launches = stats[-1]["expand_launches"]
     ms_exp_max = D.reduce(ms_exp, "max")
 
     if args.verify or args.dump:
+        # per-word digests of this rank's bytes [rb, re_) of the local stream (a cut word:
+        # the part this rank wrote; digests are sums, so the parts add up across ranks)
+        bo_h = boff.to_array(np.uint64, count=n + 1)
+        cut = DeviceBuffer.from_array(ctx, (np.clip(bo_h, rb, re_) - np.uint64(rb)).astype(np.uint64))
         dig = DeviceBuffer(ctx, n * 32)
-        ctx.digest_device(out.ptr, boff.ptr, 0, n, dig.ptr)
+        ctx.digest_device(out.ptr, cut.ptr, 0, n, dig.ptr)
         got = dig.to_array(np.uint64).reshape(n, 4)
+        cut.free()
         if args.dump:  # this rank's shard: per-word digests of words [w0, w1) of the global list
             os.makedirs(args.dump, exist_ok=True)
             np.save(os.path.join(args.dump, f"digest_{w0}_{w1}.npy"), got)
+    if args.verify and (cb, ce) != (0, tc_all):
+        raise SystemExit("--verify checks whole batches (one rank); the multi-rank check is tests/test_gpu_dist.py")
     if args.verify:
         from oracle import c_oracle as co
         want = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables]
@@ -656,6 +687,7 @@ def main():
                 "words_per_gpu": n,
                 "candidates_per_gpu_step": tc,
                 "bytes_per_gpu_step": tb,
+                "bytes_per_rank": bytes_per_rank,
                 "table_min": args.min,
                 "table_max": args.max,
                 "mode": MODE_NAMES[args.mode],

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -114,18 +115,39 @@ struct Turn {
   }
 };
 
+// host timeline (A5X_CLI_TIMELINE=1): milliseconds since main() per event, to stderr
+static const auto g_t0 = std::chrono::steady_clock::now();
+static bool g_tl = false;
+static double ms_now() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_t0).count();
+}
+#define TL(...)                                \
+  do {                                         \
+    if (g_tl) {                                \
+      fprintf(stderr, "[tl %9.2f] ", ms_now()); \
+      fprintf(stderr, __VA_ARGS__);            \
+      fputc('\n', stderr);                     \
+    }                                          \
+  } while (0)
+
 struct SinkCtx {
   Turn* t;
   uint64_t k;
   bool waited;
+  const std::atomic<int>* failed;  // a failed earlier batch: write nothing more
+  uint64_t bytes;
 };
 
 static int sink_ordered(void* user, const uint8_t* data, size_t len) {
   SinkCtx* s = (SinkCtx*)user;
   if (!s->waited) {
+    TL("batch %llu: first range ready, waiting for its turn", (unsigned long long)s->k);
     s->t->wait(s->k);
+    TL("batch %llu: streaming", (unsigned long long)s->k);
     s->waited = true;
   }
+  if (s->failed->load()) return 1;
+  s->bytes += len;
   return fwrite(data, 1, len, stdout) == len ? 0 : 1;
 }
 
@@ -248,8 +270,11 @@ int main(int argc, char** argv) {
   if (tables.empty()) { fprintf(stderr, "a5_generator: error: missing flags: --table-files=TABLE-FILES,...\n"); usage(stderr); return 80; }
   if (dict.empty()) { fprintf(stderr, "a5_generator: error: expected \"<dict-file>\"\n"); usage(stderr); return 80; }
 
+  g_tl = getenv("A5X_CLI_TIMELINE") != nullptr;
+  TL("main");
   a5x_ctx* ctx = nullptr;
   int rc = a5x_create(device, &ctx);
+  TL("context 1 created");
   if (rc) { fprintf(stderr, "a5_generator: no usable GPU (a5x_create=%d)\n", rc); return 1; }
   for (auto& t : tables) {
     rc = a5x_load_table_file(ctx, t.c_str());
@@ -285,6 +310,7 @@ int main(int argc, char** argv) {
       fclose(f);
       return 1;
     }
+    TL("context 2 ready");
     a5x_ctx* cx[2] = {ctx, ctx2};
     Turn turn;
     std::mutex qmu;
@@ -307,10 +333,13 @@ int main(int argc, char** argv) {
         const uint64_t k = job.first;
         auto& words = job.second.first;
         auto& off = job.second.second;
-        SinkCtx sc{&turn, k, false};
-        const int r = failed.load() ? 0 : a5x_expand(cx[w], words.data(), off.data(), off.size() - 1, mode, tmin,
-                                                     tmax, sink_ordered, &sc, nullptr);
+        SinkCtx sc{&turn, k, false, &failed, 0};
+        TL("batch %llu: ctx %d starts (%zu words)", (unsigned long long)k, w, off.size() - 1);
+        int r = failed.load() ? 0 : a5x_expand(cx[w], words.data(), off.data(), off.size() - 1, mode, tmin,
+                                               tmax, sink_ordered, &sc, nullptr);
         if (!sc.waited) turn.wait(k);  // (a batch with no output still takes its turn)
+        if (r == A5X_E_SINK && failed.load()) r = 0;  // stopped by an earlier batch's failure
+        TL("batch %llu: done, %llu bytes", (unsigned long long)k, (unsigned long long)sc.bytes);
         int zero = 0;
         if (r && failed.compare_exchange_strong(zero, r)) emsg = a5x_last_error(cx[w]);
         turn.done(k);
@@ -321,6 +350,7 @@ int main(int argc, char** argv) {
       std::vector<uint8_t> words;
       std::vector<uint64_t> off;
       if (!ds.next(words, off, B, BB)) break;
+      TL("batch %llu read (%zu words)", (unsigned long long)k, off.size() - 1);
       std::unique_lock<std::mutex> l(qmu);
       qcv.wait(l, [&] { return q[k & 1].empty() || failed.load(); });  // one batch ahead per context
       if (failed.load()) break;
@@ -337,9 +367,11 @@ int main(int argc, char** argv) {
     rc = failed.load();
     fclose(f);
     fflush(stdout);
+    TL("all batches written");
     if (rc) fprintf(stderr, "a5_generator: %s\n", emsg.c_str());
     a5x_destroy(ctx2);
     a5x_destroy(ctx);
+    TL("contexts destroyed");
     return rc ? 2 : 0;
   }
   std::vector<uint8_t> words;

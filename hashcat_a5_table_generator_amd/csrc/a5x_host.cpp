@@ -1653,6 +1653,86 @@ int a5x_expand_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   return A5X_OK;
 }
 
+int a5x_locate_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn,
+                      int mx, const uint64_t* cands, uint64_t n, uint64_t* byte_off_out, void* stream) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!d_words || !d_woff)) || (n && (!cands || !byte_off_out))) return A5X_E_ARG;
+  if (n > 0xffffffffull) return fail(c, A5X_E_ARG, "too many queries");
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  Job J;
+  job_open(c, J, d_words, d_woff, nw, mode, mn, mx, stream ? (hipStream_t)stream : c->stream);
+  if ((rc = job_prepare(c, J, nullptr, nullptr, false))) return rc;
+  std::vector<uint64_t> q(n), res;
+  for (uint64_t i = 0; i < n; i++) q[i] = std::min(cands[i], J.B.total_cands);
+  if ((rc = job_locate(c, J, q, res))) return rc;
+  for (uint64_t i = 0; i < n; i++) byte_off_out[i] = res[3 * i];
+  return A5X_OK;
+}
+
+int a5x_split_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn,
+                     int mx, const uint64_t* targets, uint32_t nt, uint64_t* cand_out, uint64_t* word_out,
+                     uint64_t* ciw_out, void* stream) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!d_words || !d_woff)) || (nt && (!targets || !cand_out || !word_out || !ciw_out)))
+    return A5X_E_ARG;
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  Job J;
+  job_open(c, J, d_words, d_woff, nw, mode, mn, mx, stream ? (hipStream_t)stream : c->stream);
+  if ((rc = job_prepare(c, J, nullptr, nullptr, false))) return rc;
+  const uint64_t T = J.B.total_cands, TB = J.B.total_bytes;
+  // lockstep binary searches: lo[i] < answer <= hi[i], byte(g) = first byte of candidate g
+  std::vector<uint64_t> lo(nt), hi(nt), res;
+  for (uint32_t i = 0; i < nt; i++) {
+    if (targets[i] > TB) return fail(c, A5X_E_ARG, "byte target %llu past the batch's %llu bytes",
+                                     (unsigned long long)targets[i], (unsigned long long)TB);
+    lo[i] = ~0ull;  // "-1": byte(-1) < every target
+    hi[i] = T;      // byte(T) = TB >= every target
+  }
+  for (int it = 0; it < 70; it++) {
+    std::vector<uint64_t> q;
+    std::vector<uint32_t> who;
+    for (uint32_t i = 0; i < nt; i++)
+      if (hi[i] - (lo[i] + 1) > 0) {  // candidates lo+1 .. hi-1 still open
+        q.push_back(lo[i] + 1 + (hi[i] - lo[i] - 1) / 2);
+        who.push_back(i);
+      }
+    if (q.empty()) break;
+    if ((rc = job_locate(c, J, q, res))) return rc;
+    for (size_t k = 0; k < q.size(); k++) {
+      const uint32_t i = who[k];
+      if (res[3 * k] >= targets[i]) hi[i] = q[k];
+      else lo[i] = q[k];
+    }
+  }
+  // the word of each split candidate: binary search over the candidate offsets
+  const uint64_t* co = J.B.cand_off;
+  auto cand_at = [&](uint64_t w, uint64_t* v) -> int {
+    HIPCHK(c, hipMemcpyAsync(v, co + w, 8, hipMemcpyDeviceToHost, J.st));
+    HIPCHK(c, hipStreamSynchronize(J.st));
+    return A5X_OK;
+  };
+  for (uint32_t i = 0; i < nt; i++) {
+    cand_out[i] = hi[i];
+    if (hi[i] >= T) { word_out[i] = nw; ciw_out[i] = 0; continue; }
+    uint64_t a = 0, b = nw;  // cand_off[a] <= g < cand_off[b]
+    while (b - a > 1) {
+      const uint64_t m = a + (b - a) / 2;
+      uint64_t v = 0;
+      if ((rc = cand_at(m, &v))) return rc;
+      if (v <= hi[i]) a = m; else b = m;
+    }
+    uint64_t base = 0;
+    if ((rc = cand_at(a, &base))) return rc;
+    word_out[i] = a;
+    ciw_out[i] = hi[i] - base;
+  }
+  return A5X_OK;
+}
+
 int a5x_digest_device(a5x_ctx* c, const uint8_t* d_out, const uint64_t* d_byte_off, uint64_t out_base, uint64_t nw,
                       uint64_t* d_digest, void* stream) {
   if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");

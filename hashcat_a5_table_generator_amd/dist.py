@@ -53,6 +53,52 @@ def distributed_split(dist, local_prefix: np.ndarray, b0: int, n: int, world: in
     return allreduce_min_u64(dist, cand, backend)
 
 
+INF_U63 = (1 << 63) - 1
+
+
+def candidate_split(dist, block_cands: int, block_bytes: int, b0: int, n: int, world: int, split_fn,
+                    backend: str = "nccl") -> np.ndarray:
+    """Balanced split of ONE global candidate stream at CANDIDATE granularity (SURVEY 8(e)
+    e1: split points are (word, intra-word index)): the reference serialises a word on one
+    goroutine (main.go:77-93), so a word larger than a rank's share would cap a word-only
+    split; here such a word is cut inside.
+
+    Rank r holds the keyspace of its equal-count block [b0, b1) (``block_cands`` /
+    ``block_bytes`` totals).  One all-gather of the block totals gives the global bases;
+    the owner of byte target t_r = total * r // W (the block whose bytes hold it) finds the
+    first candidate starting at or after t_r with ``split_fn(local_targets) -> (g, w, c, b)``
+    (block-local candidate, word, candidate in word, first byte: ``Context.split_device`` +
+    ``locate_device`` on the GPU) and one all-reduce(MIN) shares the answers.
+
+    Returns a (4, W + 1) u64 array: global candidate g_r, global word w_r, candidate in that
+    word c_r and global byte b_r of every split; rank r's shard is candidates [g_r, g_r+1),
+    i.e. words w_r .. w_r+1 (the last one only when c_r+1 > 0) from candidate c_r of w_r."""
+    tot = allgather_u64(dist, [block_cands, block_bytes], backend)  # (world, 2)
+    rank = dist_rank(dist)
+    cbase, bbase = int(tot[:rank, 0].sum()), int(tot[:rank, 1].sum())
+    T, TB = int(tot[:, 0].sum()), int(tot[:, 1].sum())
+    out = np.full((4, world + 1), INF_U63, dtype=np.uint64)
+    out[:, 0] = 0
+    out[:, world] = (T, n, 0, TB)
+    mine = [r for r in range(1, world) if TB and bbase <= TB * r // world < bbase + block_bytes]
+    if mine:
+        g, w, c, b = split_fn(np.array([TB * r // world - bbase for r in mine], dtype=np.uint64))
+        for k, r in enumerate(mine):
+            out[:, r] = (cbase + int(g[k]), b0 + int(w[k]), int(c[k]), bbase + int(b[k]))
+    if not TB:  # no output at all: every split at the end
+        out[:, 1:world] = np.array([[T], [n], [0], [TB]], dtype=np.uint64)
+    return allreduce_min_u64(dist, out.reshape(-1), backend).reshape(4, world + 1)
+
+
+def shard_of(split: np.ndarray, rank: int):
+    """Rank's shard from ``candidate_split``: (first word, end word (exclusive), candidate
+    in the first word where the shard starts, candidates, first global byte, bytes)."""
+    g0, g1 = int(split[0, rank]), int(split[0, rank + 1])
+    w0, c0 = int(split[1, rank]), int(split[2, rank])
+    w1 = int(split[1, rank + 1]) + (1 if int(split[2, rank + 1]) > 0 else 0)
+    return w0, max(w1, w0), c0, g1 - g0, int(split[3, rank]), int(split[3, rank + 1]) - int(split[3, rank])
+
+
 def dist_rank(dist) -> int:
     return dist.get_rank() if dist is not None and dist.is_initialized() else 0
 

@@ -282,6 +282,27 @@ class Context:
                                               stream or None))
         return tc.value, tb.value
 
+    def locate_device(self, d_words: int, d_offs: int, n_words: int, cands, mode: int = MODE_DEFAULT, mn: int = 0,
+                      mx: int = 15, stream: int = 0) -> np.ndarray:
+        """Output byte offsets of global candidate indices (``a5x_locate_device``)."""
+        q = np.ascontiguousarray(cands, dtype=np.uint64)
+        out = np.zeros(max(1, q.size), dtype=np.uint64)
+        self._chk(self._L.a5x_locate_device(self.h, d_words, d_offs, n_words, mode, mn, mx,
+                                            q.ctypes.data if q.size else None, q.size, out.ctypes.data,
+                                            stream or None))
+        return out[: q.size]
+
+    def split_device(self, d_words: int, d_offs: int, n_words: int, byte_targets, mode: int = MODE_DEFAULT,
+                     mn: int = 0, mx: int = 15, stream: int = 0) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(global candidate, word, candidate in word) of the first candidate starting at or
+        after each byte target (``a5x_split_device``: intra-word split points)."""
+        t = np.ascontiguousarray(byte_targets, dtype=np.uint64)
+        g, w, c = (np.zeros(max(1, t.size), dtype=np.uint64) for _ in range(3))
+        self._chk(self._L.a5x_split_device(self.h, d_words, d_offs, n_words, mode, mn, mx,
+                                           t.ctypes.data if t.size else None, t.size, g.ctypes.data, w.ctypes.data,
+                                           c.ctypes.data, stream or None))
+        return g[: t.size], w[: t.size], c[: t.size]
+
     def digest_device(self, d_out: int, d_byte_off: int, out_base: int, n_words: int, d_digest: int,
                       stream: int = 0) -> None:
         self._chk(self._L.a5x_digest_device(self.h, d_out, d_byte_off, out_base, n_words, d_digest,

@@ -52,6 +52,19 @@ def words_greek(n: int, lmin: int = 6, lmax: int = 12, seed: int = 0x5A5) -> Tup
     return _pack(letters * 2, data)
 
 
+def words_az_huge(n: int, lmin: int = 10, lmax: int = 10, seed: int = 0x5A5, every: int = 20000,
+                  huge: int = 24) -> Tuple[np.ndarray, np.ndarray]:
+    """C4's length-10 [a-z] words with every ``every``-th word (by position in the block)
+    ``huge`` letters long: 2^huge - 1 candidates under qwerty-cyrillic, one word larger than a
+    rank's share (the intra-word split of SURVEY 8(e) e1)."""
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(lmin, lmax + 1, size=n, dtype=np.int64)
+    lengths[every // 3::every] = huge
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", dtype=np.uint8)
+    data = alpha[rng.integers(0, len(alpha), size=int(lengths.sum()), dtype=np.int64)]
+    return _pack(lengths, data)
+
+
 CONFIGS = {
     # name: (tables, generator, kwargs, description)
     "c1": (["qwerty-azerty"], words_az09, {"lmin": 6, "lmax": 12},
@@ -64,6 +77,8 @@ CONFIGS = {
            "czech+german x synthetic [a-z] words len U[6,12] (configs[2])"),
     "c4": (["qwerty-cyrillic"], words_az, {"lmin": 10, "lmax": 10},
            "qwerty-cyrillic x synthetic [a-z] words len 10 (configs[3], 1023 cand/word)"),
+    "c4h": (["qwerty-cyrillic"], words_az_huge, {"lmin": 10, "lmax": 10},
+            "qwerty-cyrillic x C4 words with a 24-letter word every 20000 (intra-word shard split test)"),
     "c5": (["greek-hebrew"], words_greek, {"lmin": 6, "lmax": 12},
            "greek-hebrew x synthetic Greek words len U[6,12] (configs[4] expansion stage)"),
 }

@@ -196,6 +196,24 @@ A5X_API int a5x_format_hits(a5x_ctx* ctx, const uint8_t* words, const uint64_t* 
                             int mode, int min, int max, const a5x_hit* hits, uint64_t n_hits, a5x_sink_fn sink,
                             void* user);
 
+/* Output byte offset, in the batch's full "cand\n" stream, of each global candidate index
+ * cands[i] (cands[i] = the batch's total candidates gives its total bytes; larger: clamped).
+ * Device-resident words; the keyspace runs once per call.  Candidate numbering is the one
+ * a5x_expand_device's [cand_begin, cand_end) uses. */
+A5X_API int a5x_locate_device(a5x_ctx* ctx, const uint8_t* d_words, const uint64_t* d_word_off, uint64_t n_words,
+                              int mode, int min, int max, const uint64_t* cands, uint64_t n, uint64_t* byte_off_out,
+                              void* stream);
+/* Candidate-granular split points for byte targets (a word larger than
+ * a rank's share is cut inside, where the reference serialises it on one goroutine,
+ * main.go:77-93): for each byte_targets[i] (<= the batch's total bytes), cand_out[i] =
+ * the first global candidate whose first output byte is >= the target (the total
+ * candidates when none), word_out[i] = the word holding it (n_words when none) and
+ * cand_in_word_out[i] = its index inside that word.  Exact (binary search over
+ * a5x_locate_device's offsets); the keyspace runs once per call. */
+A5X_API int a5x_split_device(a5x_ctx* ctx, const uint8_t* d_words, const uint64_t* d_word_off, uint64_t n_words,
+                             int mode, int min, int max, const uint64_t* byte_targets, uint32_t n_targets,
+                             uint64_t* cand_out, uint64_t* word_out, uint64_t* cand_in_word_out, void* stream);
+
 /* ---- multi-GPU partition --------------------------------------- */
 /* Balanced split of [0, total) for `parts` ranks from an inclusive/exclusive
  * prefix (n+1 entries, e.g. per-word byte offsets): split[r] = first word of

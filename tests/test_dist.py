@@ -182,3 +182,84 @@ def test_hit_gather_global_word_indices(tmp_path, world):
     its shard to the global list, arrive on rank 0 in rank order (empty ranks included)."""
     res = _run_ranks(tmp_path, GATHER_WORKER.format(root=ROOT), world)
     assert all(r["ok"] for r in res), res
+
+
+HUGE_WORKER = r"""
+import hashlib, os, sys, json
+sys.path.insert(0, {root!r})
+import numpy as np
+from hashcat_a5_table_generator_amd import dist as D
+from oracle import c_oracle as co
+dist, rank, world, _ = D.init_from_env("gloo")
+# ONE global list: length-10 [a-z] words and three 20-letter words (2^20 - 1 candidates,
+# ~32 MB each under qwerty-cyrillic: each larger than a rank's share of the ~110 MB)
+rng = np.random.default_rng(3)
+words = [bytes(rng.integers(97, 123, size=10, dtype=np.uint8)) for _ in range(600)]
+for k, at in enumerate((5, 250, 251)):
+    words.insert(at, bytes(rng.integers(97, 123, size=20, dtype=np.uint8)))
+n = len(words)
+t = co.CTable([os.path.join({root!r}, "tests", "golden", "tables", "qwerty-cyrillic.table")])
+
+def stream(ws):
+    # the oracle's stream of words ws and the first byte of every candidate (its own,
+    # deterministic candidate order stands in for the device's in this CPU test)
+    data, offs = co.pack_words(ws)
+    out, wb = t.expand_batch(data, offs, 0, 0, 15)
+    buf = np.frombuffer(out, dtype=np.uint8)
+    nl = np.flatnonzero(buf == 10)
+    starts = np.concatenate([[0], nl[:-1] + 1]).astype(np.uint64)
+    cnt = np.zeros(len(ws) + 1, dtype=np.int64)
+    pos, k = 0, 0
+    for i, b in enumerate(wb):  # candidates per word from the per-word bytes
+        e = pos + int(b)
+        k2 = int(np.searchsorted(starts, np.uint64(e), side="left"))
+        cnt[i + 1] = cnt[i] + (k2 - k)
+        pos, k = e, k2
+    return out, starts, cnt
+
+b0, b1 = D.block_bounds(n, world, rank)
+out, starts, cnt = stream(words[b0:b1])
+
+def split_fn(targets):
+    g = np.searchsorted(starts, targets, side="left").astype(np.uint64)
+    w = np.searchsorted(cnt, g.astype(np.int64), side="right") - 1
+    w = np.minimum(w, b1 - b0)
+    c = g.astype(np.int64) - cnt[w]
+    b = np.array([int(starts[x]) if x < len(starts) else len(out) for x in g], dtype=np.uint64)
+    return g, w, c, b
+
+split = D.candidate_split(dist, len(starts), len(out), b0, n, world, split_fn, "gloo")
+w0, w1, c0, ncand, bstart, nbytes = D.shard_of(split, rank)
+sout, sstarts, _ = stream(words[w0:w1])
+lo = int(sstarts[c0]) if c0 < len(sstarts) else len(sout)
+hi = int(sstarts[c0 + ncand]) if c0 + ncand < len(sstarts) else len(sout)
+piece = sout[lo:hi]
+rows = D.allgather_u64(dist, [bstart, len(piece), int.from_bytes(hashlib.sha256(piece).digest()[:7], "little")],
+                       "gloo")
+ok = len(piece) == nbytes
+if rank == 0:
+    full, _, _ = stream(words)
+    pos = 0
+    for r in range(world):
+        s, L, h = (int(x) for x in rows[r])
+        ok = ok and s == pos and int.from_bytes(hashlib.sha256(full[s:s + L]).digest()[:7], "little") == h
+        pos += L
+    ok = ok and pos == len(full)
+sizes = [int(x) for x in rows[:, 1]]
+print(json.dumps(dict(rank=rank, ok=bool(ok), sizes=sizes, split=split.tolist())), flush=True)
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_candidate_split_cuts_huge_words(tmp_path, world):
+    """SURVEY 8(e) e1 / VERDICT r3: words larger than a rank's share are split inside at the
+    candidate whose first byte reaches the rank's byte target, so shards stay balanced
+    (max/min bytes < 1.01) where a word-granular split cannot be; the ranks' pieces tile the
+    single-rank stream exactly (byte ranges and contents)."""
+    res = _run_ranks(tmp_path, HUGE_WORKER.format(root=ROOT), world)
+    assert all(r["ok"] for r in res), res
+    sizes = res[0]["sizes"]
+    assert max(sizes) / min(sizes) < 1.01, sizes
+    split = res[0]["split"]
+    assert any(c > 0 for c in split[2]), split  # at least one split falls inside a word
