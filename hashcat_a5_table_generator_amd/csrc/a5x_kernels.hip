@@ -1772,6 +1772,169 @@ struct FxDigest {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Fused digest with one candidate per 64-B message slot (windows whose candidates fit
+// one MD block, FXD_MAXL bytes with the '\n'): lane L's candidate is OR-placed at ring
+// byte 64 L and its '\n' turned into the 0x80 pad byte (one ds_xor), so the slot IS the
+// MD5 / MD4 message block -- four 16-B LDS reads, no per-word keep / pad masks, the bit
+// length in M[14].  NTLM windows carry big entries already converted to UTF-16LE
+// (fx_utf16_entry), so the slot holds the UTF-16LE message and MD4 runs on it directly;
+// the UTF-8 walk of ntlm_stream is left to windows that cannot take the slots.
+// ---------------------------------------------------------------------------
+#define FXD_MAXL 56u  // slot path: candidate + '\n' (NTLM: UTF-16LE bytes + "\n\0") <= 56 B
+
+typedef u32 fx6_v4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) fx6_v4 fx6_lds128;
+__device__ __forceinline__ uint4 fx6_ld16(u32 a) {
+  const fx6_v4 v = *(const fx6_lds128*)(uintptr_t)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void fx6_st16(u32 a, uint4 v) {
+  const fx6_v4 x = {v.x, v.y, v.z, v.w};
+  *(fx6_lds128*)(uintptr_t)a = x;
+}
+__device__ __forceinline__ void fx7_xor(u32 a, u32 v) {
+  __hip_atomic_fetch_xor((fx6_lds32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// One rune of Go's utf8.DecodeRune from the 4 bytes x (avail of them belong to the
+// string): r, its byte size sz (invalid: U+FFFD, 1 byte), cut = a valid lead byte whose
+// sequence runs past the available bytes (decoded here it differs from the decoding in
+// the longer string).
+__device__ __forceinline__ void utf8_rune(u32 x, u32 avail, u32& r, u32& sz, bool& cut) {
+  const u32 b0 = x & 255u, b1 = (x >> 8) & 255u, b2 = (x >> 16) & 255u, b3 = x >> 24;
+  r = b0; sz = 1; cut = false;
+  if (b0 < 0x80u) return;
+  r = 0xFFFDu;
+  u32 size = 0, lo = 0x80u, hi = 0xBFu;
+  if (b0 >= 0xC2u && b0 <= 0xDFu) size = 2;
+  else if (b0 >= 0xE0u && b0 <= 0xEFu) { size = 3; lo = b0 == 0xE0u ? 0xA0u : 0x80u; hi = b0 == 0xEDu ? 0x9Fu : 0xBFu; }
+  else if (b0 >= 0xF0u && b0 <= 0xF4u) { size = 4; lo = b0 == 0xF0u ? 0x90u : 0x80u; hi = b0 == 0xF4u ? 0x8Fu : 0xBFu; }
+  cut = size > avail;
+  const bool c2 = b2 >= 0x80u && b2 <= 0xBFu, c3 = b3 >= 0x80u && b3 <= 0xBFu;
+  if (size && size <= avail && b1 >= lo && b1 <= hi && (size < 3 || c2) && (size < 4 || c3)) {
+    sz = size;
+    r = size == 2 ? ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu)
+      : size == 3 ? ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu)
+                  : ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
+  }
+}
+
+// A big entry (<= 15 UTF-8 bytes) as UTF-16LE (Go []rune + utf16.Encode of the piece).
+// The candidate's UTF-16LE is the concatenation of its pieces' when no piece ends inside
+// a rune: ok = false for an entry cut inside a rune or longer than 15 bytes as UTF-16LE.
+__device__ __forceinline__ uint4 fx_utf16_entry(const uint4 e, bool& ok) {
+  typedef unsigned __int128 u128;
+  u128 in = (u128)((u64)e.x | ((u64)e.y << 32)) | ((u128)((u64)e.z | ((u64)(e.w & 0xFFFFFFu) << 32)) << 64);
+  const u32 n = e.w >> 24;
+  u128 out = 0;
+  u32 i = 0, o = 0;
+  bool good = true;
+  for (u32 it = 0; it < 15u && i < n; it++) {
+    u32 r, sz;
+    bool cut;
+    utf8_rune((u32)in, n - i, r, sz, cut);
+    good = good && !cut;
+    if (r >= 0x10000u) {
+      const u32 v = r - 0x10000u;
+      const u32 pair = (0xD800u + (v >> 10)) | ((0xDC00u + (v & 0x3FFu)) << 16);
+      if (o < 16u) out |= (u128)pair << (8u * o);
+      o += 4;
+    } else {
+      if (o < 16u) out |= (u128)r << (8u * o);
+      o += 2;
+    }
+    in >>= 8u * sz;
+    i += sz;
+  }
+  ok = good && o <= 15u;
+  const u64 lo = (u64)out, hi = (u64)(out >> 64);
+  return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, ((u32)(hi >> 32) & 0xFFFFFFu) | ((o <= 15u ? o : 0u) << 24));
+}
+
+// One round of the slot path: lane L < nr takes window candidate rr + L (one candidate
+// per run), places it at ring + 64 L, hashes the slot and probes the target set.
+template <int NB, bool MD5>
+__device__ __forceinline__ void fxd_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
+                                          u32 rr, u32 j, bool act, const ExpArgs& a, u64 wbase) {
+  const u32 lane = lane_id();
+  const uint4 q0 = wq[j][0], q1 = wq[j][1];
+  const u32 st = act ? rr + lane - q1.w + rb[j] : 0u;  // the candidate's rank in its word
+  const bool on = act && st < re[j];
+  u32 d[4];
+  fx6_digits<NB>(st + 1u, q0, q1.x, d);
+  uint4 ent[NB];
+  u32 len = 0;
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    ent[b] = be[on ? fx6_eb(q1, b) + d[b] : (u32)FX6_ZBE];
+    len += ent[b].w >> 24;
+  }
+  const u32 slot = ring + 64u * lane;
+  u32 P = slot, sink = 0;
+#pragma unroll
+  for (int b = 0; b < NB; b++) fx7_put(ent[b], P, sink);
+  constexpr u32 TL = MD5 ? 1u : 2u;  // the '\n' ("\n\0" in UTF-16LE) becomes the 0x80 pad
+  if (on) {
+    const u32 pb = slot + len - TL;
+    fx7_xor(pb & ~3u, 0x8Au << (8u * (pb & 3u)));
+  }
+  WAVE_SYNC();
+  u32 M[16];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 v = fx6_ld16(slot + 16u * q);
+    M[4 * q] = v.x; M[4 * q + 1] = v.y; M[4 * q + 2] = v.z; M[4 * q + 3] = v.w;
+  }
+  M[14] = on ? (len - TL) << 3 : 0u;
+  M[15] = 0u;
+#pragma unroll
+  for (int q = 0; q < 4; q++) fx6_st16(slot + 16u * q, make_uint4(0, 0, 0, 0));  // zero again for the next round
+  u32 h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+#if FX_DABL & 1
+  h[0] ^= M[0] + M[14]; h[1] ^= M[1]; h[2] ^= M[2]; h[3] ^= M[3];
+#else
+  if constexpr (MD5) md5_block(h, M);
+  else md4_block(h, M);
+#endif
+#if FX_DABL & 2
+  const bool hit = (h[0] ^ h[1] ^ h[2] ^ h[3]) == 0x7A5A5A5Au && h[0] == 0x13579BDFu;
+#else
+  const bool hit = md_probe(a.dg_bitmap, a.dg_bm_mask, a.dg_table, a.dg_tmask, a.dg_has_zero != 0, h);
+#endif
+  if (on && hit) {
+    const u32 k = atomicAdd(a.dg_nhits, 1u);
+    if (k < a.dg_hit_cap) {
+      A5xHitRaw r;
+      r.blk = wbase + j;
+      r.idx = st;
+      r.d[0] = h[0]; r.d[1] = h[1]; r.d[2] = h[2]; r.d[3] = h[3];
+      a.dg_hits[k] = r;
+    }
+  }
+  WAVE_SYNC();
+}
+
+// The window's candidates (T of them) in rounds of 64 on the slot path.
+template <bool MD5>
+__device__ __forceinline__ void fxd_rounds(FXWin& F, u32* ring, const ExpArgs& a, u64 wbase, u32 T, u32 k, u32 rw,
+                                           u64 m2, u64 m3, u64 m4) {
+  const u32 lane = lane_id();
+  const u32 ringa = fx6_addr(ring);
+  u32 jcur = 0;
+  for (u32 rr = 0; rr < T; rr += 64u) {
+    const u32 nr = min(64u, T - rr);
+    const u32 j = fx6_word(rw, k, rr, nr, jcur);
+    const bool act = lane < nr;
+    const u32 jl = readlane_u32(j, nr - 1u);
+    const u64 span = ((2ull << (jl - jcur)) - 1ull) << jcur;  // words jcur .. jl
+    if (span & m4) fxd_round<4, MD5>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
+    else if (span & m3) fxd_round<3, MD5>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
+    else if (span & m2) fxd_round<2, MD5>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
+    else fxd_round<1, MD5>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
+  }
+}
+
 // The window's rounds: T runs of K candidates, nl runs per round; each round takes
 // the largest big-piece count among the words it spans (m2 / m3 / m4: window words
 // with >= 2 / 3 / 4 big pieces).
@@ -1989,15 +2152,18 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     const u32 ebase = incE - E;
     // ---- per-word info: magics, R - 1, entry bases (pieces past the count: R 1, the
     // empty entry), the word's ranks inside [g, g1) and its runs ----
-    // candidates per run: a round always takes at least one run (K (longest) <= ring)
-    const u32 K = FX_K * winmax + 16u <= FX_RING - 32u ? FX_K : 1u;
+    // candidates per run: a round always takes at least one run (K (longest) <= ring);
+    // the fused digest's slot path (fxd_rounds): one candidate per run
+    bool dslot = false;
+    if constexpr (DIG != 0) dslot = (DIG == 1 ? winmax : 2u * winmax) <= FXD_MAXL;
+    u32 K = dslot ? 1u : (FX_K * winmax + 16u <= FX_RING - 32u ? FX_K : 1u);
     const u64 wc0 = uniform64(c0);
     const u32 rbw = lane == 0 ? (u32)(g - wc0) : 0u;
     const u32 rew = inw ? (u32)(min(c1, g1) - c0) : 0u;
-    const u32 nrun = inw && rs ? (rew - rbw + K - 1u) / K : 0u;
-    const u32 incr = wave_incl_scan_u32(nrun);
-    const u32 rw = inw ? incr - nrun : 0xffffffffu;
-    const u32 T = readlane_u32(incr, k - 1);
+    u32 nrun = inw && rs ? (rew - rbw + K - 1u) / K : 0u;
+    u32 incr = wave_incl_scan_u32(nrun);
+    u32 rw = inw ? incr - nrun : 0xffffffffu;
+    u32 T = readlane_u32(incr, k - 1);
     if (inw) {
       const u32 b1 = ebase + R0, b2 = b1 + R1, b3 = b2 + R2;
       const u32 e1 = nbw > 1 ? b1 : (u32)FX_ZBE, e2 = nbw > 2 ? b2 : (u32)FX_ZBE, e3 = nbw > 3 ? b3 : (u32)FX_ZBE;
@@ -2009,10 +2175,11 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     }
     WAVE_SYNC();
     STAMP(5);
-    // ---- build the big entries: lanes over the window's entries ----
+    // ---- build the big entries: lanes over the window's entries (conv: as UTF-16LE, the
+    // NTLM slot path; returns whether an entry could not be converted) ----
     u32 thr = 0;  // bit 5 b + ceil(len / 4): the entry lengths of big piece b (fx8_slots)
-    if (!(FX_ABL & 16))
-    {
+    auto build_entries = [&](bool conv) -> bool {
+      bool bad = false;
       const u32 etot = readlane_u32(incE, k - 1);
       const u32 est = lane < k ? ebase : 0xffffffffu;
       u32 jb = 0;  // word of the pass's first entry (uniform)
@@ -2044,10 +2211,29 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
         const u32 np = frh_np(h), nbh = frh_nbig(h);
         const u32 sp0 = frh_bstart(h, b), sp1 = b + 1 < nbh ? frh_bstart(h, b + 1) : np;
         const u32 span = on ? sp1 - sp0 : 0u;
-        const uint4 e = fx_entry(rec, wrb + 1u + sp0, wrb + 1u + np, span, wave_max_u32(span), u - cb);
+        uint4 e = fx_entry(rec, wrb + 1u + sp0, wrb + 1u + np, span, wave_max_u32(span), u - cb);
+        if (DIG == 2 && conv) {
+          bool ok = true;
+          e = fx_utf16_entry(e, ok);
+          bad = bad || (on && !ok);
+        }
         if (on) F.be[t] = e;
         thr |= on ? (1u << ((((e.w >> 24) + 3u) >> 2) + 5u * b)) : 0u;
       }
+      return wave_or_u32(bad ? 1u : 0u) != 0u;
+    };
+    if (!(FX_ABL & 16) && build_entries(DIG == 2 && dslot)) {
+      // an entry cut inside a rune (or too long as UTF-16LE): UTF-8 entries, K-candidate runs
+      WAVE_SYNC();
+      dslot = false;
+      thr = 0;
+      (void)build_entries(false);
+      K = FX_K * winmax + 16u <= FX_RING - 32u ? FX_K : 1u;
+      nrun = inw && rs ? (rew - rbw + K - 1u) / K : 0u;
+      incr = wave_incl_scan_u32(nrun);
+      rw = inw ? incr - nrun : 0xffffffffu;
+      T = readlane_u32(incr, k - 1);
+      if (inw) F.wq[lane][1].w = rw;
     }
     // slot counts of the window's big pieces (wave-uniform)
     const u32 thm = uniform(wave_or_u32(thr));
@@ -2087,7 +2273,8 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     // ---- rounds ----
     if (!(FX_ABL & 8))
     {
-      if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4, nsm);
+      if (DIG != 0 && dslot) fxd_rounds<DIG == 1>(F, ring, a, w, T, k, rw, m2, m3, m4);
+      else if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4, nsm);
       else fx_rounds<1>(F, ring, R, fl, T, k, rw, m2, m3, m4, nsm);
     }
     STAMP(3);

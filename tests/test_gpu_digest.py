@@ -198,3 +198,37 @@ def test_format_hits_word_past_4gib_of_output(gpu_ctx):
         assert sorted(lines) == sorted(dg.md5(p).hex().encode() + b":" + p for p in plains)
     finally:
         gpu_ctx.clear_table()
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_fused_slot_path_every_candidate_mixed_utf8(gpu_ctx, algo):
+    """The fused kernels' slot path (one candidate per 64-B message block, '\\n' turned into
+    the 0x80 pad; NTLM on big entries pre-converted to UTF-16LE) beside their general path
+    (windows with candidates past one block, or with a piece boundary inside a rune: the
+    UTF-8 walk): every candidate of every word is a target, so each (word, candidate) must
+    come back once with its MD5 / NTLM bit-exact vs the oracle (hashlib, RFC 1320 over Go's
+    UTF-16LE).  Words mix ASCII, 2/3/4-byte runes (surrogate pairs), literal runs of 3-byte
+    runes (the 7-byte literal pieces cut them) and invalid bytes (U+FFFD)."""
+    from hashcat_a5_table_generator_amd import pack_words
+    from oracle import digest_oracle as dg
+    sub = {b"a": ["€".encode(), b"A"], b"e": ["é".encode(), "😀".encode()], b"o": [b"0", "ö".encode()]}
+    gpu_ctx.set_table(sub)
+    rng = np.random.default_rng(41 + algo)
+    parts = [b"a", b"e", b"o", b"x", b"y", "日".encode(), "😀".encode(), b"\xff", b"\xc3", "é".encode(), "本語".encode()]
+    words = [b"".join(parts[int(i)] for i in rng.integers(0, len(parts), size=int(rng.integers(1, 9))))
+             for _ in range(1500)]
+    words += [("日本語" * 3 + "ae").encode(), b"q" * 40 + b"ao", ("β" * 20 + "eo").encode()]  # long: general path
+    per_word = gpu_ctx.expand_words(words, 0, 0, 15)
+    f = dg.ALGOS[algo]
+    want = {}
+    for w, cs in enumerate(per_word):
+        for i, c in enumerate(cs):
+            want.setdefault(f(c), set()).add((w, i))
+    gpu_ctx.set_targets(algo, b"".join(want))
+    hits, st = gpu_ctx.expand_digest(*pack_words(words), 0, 0, 15, hit_cap=1 << 18)
+    got = {}
+    for w, c, d in hits:
+        assert f(per_word[w][c]) == d, (algo, w, c, per_word[w][c])
+        got.setdefault(d, set()).add((w, c))
+    assert sum(len(v) for v in got.values()) == len(hits)  # each (word, candidate) once
+    assert got == want
