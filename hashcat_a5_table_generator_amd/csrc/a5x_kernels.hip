@@ -1783,19 +1783,6 @@ struct FxDigest {
 // ---------------------------------------------------------------------------
 #define FXD_MAXL 56u  // slot path: candidate + '\n' (NTLM: UTF-16LE bytes + "\n\0") <= 56 B
 
-typedef u32 fx6_v4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) fx6_v4 fx6_lds128;
-__device__ __forceinline__ uint4 fx6_ld16(u32 a) {
-  const fx6_v4 v = *(const fx6_lds128*)(uintptr_t)a;
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void fx6_st16(u32 a, uint4 v) {
-  const fx6_v4 x = {v.x, v.y, v.z, v.w};
-  *(fx6_lds128*)(uintptr_t)a = x;
-}
-__device__ __forceinline__ void fx7_xor(u32 a, u32 v) {
-  __hip_atomic_fetch_xor((fx6_lds32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
 
 // One rune of Go's utf8.DecodeRune from the 4 bytes x (avail of them belong to the
 // string): r, its byte size sz (invalid: U+FFFD, 1 byte), cut = a valid lead byte whose

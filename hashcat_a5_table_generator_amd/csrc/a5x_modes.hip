@@ -1225,6 +1225,79 @@ __device__ __forceinline__ u64 m_fast_step(u64 sel, bool rev, u64 biasm) {
 __device__ __forceinline__ void m_digest_probe(const A5xModeLaunch& a, const uint8_t* base, u32 off, u32 len, bool on,
                                                u64 w, u64 t);
 
+// Fused MD5, one leaf per 64-lane slot of SLOT bytes (SLOT - 1 >= the leaf, <= 55): the leaf
+// is OR-placed at ring + SLOT lane with a 0x80 pad byte after it (the slot is zero beyond),
+// so its MD5 message block is the slot itself plus the bit length -- no prefix scan, no
+// per-word masks (k_expand_fast's fxd_round does the same for FAST words).  Reads the
+// lane's slot back, zeroes it for the next round and probes the target set.
+template <u32 SLOT>
+__device__ __forceinline__ void m_slot_md5_probe(const A5xModeLaunch& a, u32 slot, u32 len, bool on, u64 w, u64 t) {
+  static_assert(SLOT % 16 == 0 && SLOT <= 64, "one MD5 block per slot");
+  if (on) fx7_or((slot + len) & ~3u, 0x80u << (8u * ((slot + len) & 3u)));
+  M_WAVE_SYNC();
+  u32 M[16];
+#pragma unroll
+  for (u32 q = 0; q < 4; q++) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (16u * q < SLOT) {
+      v = fx6_ld16(slot + 16u * q);
+      fx6_st16(slot + 16u * q, make_uint4(0, 0, 0, 0));
+    }
+    M[4 * q] = v.x; M[4 * q + 1] = v.y; M[4 * q + 2] = v.z; M[4 * q + 3] = v.w;
+  }
+  M[14] = on ? len << 3 : 0u;
+  M[15] = 0u;
+  u32 d[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  md5_block(d, M);
+  if (on && md_probe(a.dg_bitmap, a.dg_bm_mask, a.dg_table, a.dg_tmask, a.dg_has_zero != 0, d)) {
+    const u32 h = atomicAdd(a.dg_nhits, 1u);
+    if (h < a.dg_hit_cap) {
+      A5xHitRaw r;
+      r.blk = w;
+      r.idx = t;
+      r.d[0] = d[0]; r.d[1] = d[1]; r.d[2] = d[2]; r.d[3] = d[3];
+      a.dg_hits[h] = r;
+    }
+  }
+  M_WAVE_SYNC();
+}
+
+// The piece engine's fused MD5 on the slot layout: rounds of 64 leaves of [tb, te), one
+// per lane at ring + 48 lane, while every leaf of the round fits a 48-byte slot.  Returns
+// the first leaf it did not hash (a round with a longer leaf: m_fast_expand's run layout
+// takes the rest).  The ring is zero before and after.
+template <class SL>
+__device__ u64 m_fast_digest_slots(SL& S, const MInfo& I, const A5xModeLaunch& a, u64 tb, u64 te, u32 np, u64 w) {
+  constexpr u32 SLOT = 48;
+  static_assert(sizeof(S.buf) >= 64 * SLOT + 32, "ring: 64 slots");
+  const u32 lane = m_lane();
+  uint4* r4 = (uint4*)&S.buf[0];
+  constexpr u32 RB = sizeof(S.buf) / 16;
+  const u32 ringa = fx6_addr(r4);
+  for (u32 i = lane; i < RB; i += 64) r4[i] = make_uint4(0, 0, 0, 0);
+  M_WAVE_SYNC();
+  const bool rev = a.mode == A5X_MODE_REVERSE;
+  const u32 Lc = I.L + 1;
+  for (u64 t0 = tb; t0 < te; t0 += 64) {
+    const u64 t = t0 + lane;
+    const bool on = t < te;
+    const u64 sel = on ? m_fast_sel(S, I, rev, t) : 0ull;
+    u32 len = on && rev ? Lc - 1u : 0u;
+    if (!rev) {
+      for (u32 p = 0; p < np; p++) len += S.elen[on ? m_piece_ix(S.pdesc[p], sel) : SL::ZE];
+    }
+    if (__builtin_amdgcn_ballot_w64(on && len > SLOT - 1u)) return t0;  // (uniform)
+    u32 P1 = ringa + SLOT * lane - 1u;
+    for (u32 p = 0; p < np; p++) {
+      const uint4 pd = S.pdesc[p];
+      const u32 nsl = (u32)__builtin_amdgcn_readfirstlane((int)(pd.w >> 8));
+      fx8_put(S.ent[on ? m_piece_ix(pd, sel) : SL::ZE], P1, nsl);
+    }
+    m_slot_md5_probe<SLOT>(a, ringa + SLOT * lane, len, on, w, t);
+  }
+  return te;
+}
+
 // Expand leaves [tb, te) of the radix word set up in S (pieces from m_piece_setup);
 // the first one's bytes start at a.out + pos0.  A round: 64 runs of MF_K leaves,
 // lengths -> wave scan -> the runs that fit the ring OR-place their pieces (piece-major:
@@ -1235,6 +1308,12 @@ __device__ __forceinline__ void m_digest_probe(const A5xModeLaunch& a, const uin
 template <class SL, bool DIG = false>
 __device__ void m_fast_expand(SL& S, const MInfo& I, const A5xModeLaunch& a, u64 tb, u64 te, u64 pos0, u32 np,
                               u64 biasm, u32& err, u64 w = 0) {
+  if constexpr (DIG) {
+    if (a.dg_algo == A5X_ALGO_MD5) {
+      tb = m_fast_digest_slots(S, I, a, tb, te, np, w);
+      if (tb >= te) return;
+    }
+  }
   const u32 lane = m_lane();
   uint4* r4 = (uint4*)&S.buf[0];
   constexpr u32 RB = sizeof(S.buf) / 16;
@@ -1372,6 +1451,19 @@ __device__ void m_pos_digest(SL& S, const MT& T, const MInfo& I, const A5xModeLa
     if (t < te) {
       len = m_pos_sel(S, T, I, a.mode, t, sel);
       if (len + 1 > A5X_M_CBUF) { err |= M_ERR_CLEN; len = 0; }
+    }
+    if (a.dg_algo == A5X_ALGO_MD5 && !__builtin_amdgcn_ballot_w64(t < te && len > 55u)) {
+      // every leaf fits one MD5 block: one 64-byte slot per lane (m_slot_md5_probe)
+      u32 P = ringa + 64u * lane, sink = 0;
+      if (t < te && len) {
+        for (u32 k = 0; k < ntok; k++) {
+          const u32 d = S.tok[k], pi = d >> 16;
+          const u32 ix = (d & 0xFFFFu) + (pi ? (rev ? (u32)(sel >> (pi - 1)) & 1u : (u32)(sel >> (4 * (pi - 1))) & 15u) : 0u);
+          fx7_put(S.ent[ix], P, sink);
+        }
+      }
+      m_slot_md5_probe<64>(a, ringa + 64u * lane, len, t < te, w, t);
+      continue;
     }
     const u32 incl = m_incl_scan(len);
     const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);

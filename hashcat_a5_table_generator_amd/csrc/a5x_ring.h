@@ -20,6 +20,21 @@ __device__ __forceinline__ uint32_t fx6_addr(const void* p) {
 }
 __device__ __forceinline__ void fx6_st(uint32_t a, uint32_t v) { *(fx6_lds32*)(uintptr_t)a = v; }
 
+// 16-byte LDS accesses at a byte address (16-B aligned) and an XOR into a ring dword
+typedef uint32_t fx6_v4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) fx6_v4 fx6_lds128;
+__device__ __forceinline__ uint4 fx6_ld16(uint32_t a) {
+  const fx6_v4 v = *(const fx6_lds128*)(uintptr_t)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void fx6_st16(uint32_t a, uint4 v) {
+  const fx6_v4 x = {v.x, v.y, v.z, v.w};
+  *(fx6_lds128*)(uintptr_t)a = x;
+}
+__device__ __forceinline__ void fx7_xor(uint32_t a, uint32_t v) {
+  __hip_atomic_fetch_xor((fx6_lds32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 // byte shift of a piece: w_k = bytes [4k - n, 4k - n + 4) of the piece (v_perm selector;
 // n replicated into every byte by a perm with selector 0)
 __device__ __forceinline__ uint32_t fx6_sel(uint32_t n) { return 0x07060504u - __builtin_amdgcn_perm(0u, n, 0u); }
