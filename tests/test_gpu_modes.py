@@ -232,3 +232,38 @@ def test_mode_hits_regenerate_their_plains(wl, tabs, mode, mn):
         assert hashlib.md5(plain).hexdigest().encode() == hx, line
         seen.add(bytes.fromhex(hx.decode()))
     assert set(planted) <= seen
+
+
+@pytest.mark.parametrize("mode,mn", [(1, 0), (2, 0), (3, 1), (2, 1)])
+def test_mode_fused_md5_every_candidate(mode, mn):
+    """-r / -s / -s -r fused MD5 with EVERY candidate of the batch a target: the mode
+    engines' slot layout (one leaf per 48-B or 64-B slot, the 0x80 pad placed after it, the
+    block read straight from the ring) and its fallbacks (leaves past a slot: the run
+    layout / the contiguous positional ring) must each report every (word, candidate) once
+    with the hashlib MD5 of the candidate that index names.  Greek words (C5 shape) with
+    2-8 letters, and digit runs with a few letters (leaves of 30-70 bytes) so rounds of both
+    kinds occur."""
+    from hashcat_a5_table_generator_amd import Context, pack_words
+    rng = np.random.default_rng(70 + mode)
+    letters = "αβγδεζηθικλμνξοπρστυφχψω"
+
+    def greek(n):
+        return "".join(letters[int(x)] for x in rng.integers(0, 24, size=int(n)))
+
+    words = [greek(rng.integers(2, 9)).encode() for _ in range(1200)]
+    words += [("7" * int(n) + greek(3)).encode() for n in range(24, 64, 3)]
+    with Context(0) as ctx:
+        ctx.load_tables([table_path("greek-hebrew")])
+        per_word = ctx.expand_words(words, mode, mn, 15)
+        want = {}
+        for w, cs in enumerate(per_word):
+            for i, c in enumerate(cs):
+                want.setdefault(hashlib.md5(c).digest(), set()).add((w, i))
+        ctx.set_targets(0, b"".join(want))
+        hits, _ = ctx.expand_digest(*pack_words(words), mode, mn, 15, hit_cap=1 << 20)
+    got = {}
+    for w, c, d in hits:
+        assert hashlib.md5(per_word[w][c]).digest() == d, (mode, w, c)
+        got.setdefault(d, set()).add((w, c))
+    assert sum(len(v) for v in got.values()) == len(hits)
+    assert got == want
