@@ -30,6 +30,7 @@ EXPORTS = (
     "a5x_memcpy_d2h", "a5x_synchronize", "a5x_debug_stamps", "a5x_debug_plan_word",
     "a5x_set_targets", "a5x_expand_digest", "a5x_expand_digest_device", "a5x_digest_lines_device",
     "a5x_format_plain", "a5x_format_hits", "a5x_locate_device", "a5x_split_device",
+    "a5x_stream_reserve",
 )
 
 
@@ -111,6 +112,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     L.a5x_format_plain.argtypes = [ctypes.c_char_p, sz, vp, sz, ctypes.POINTER(sz)]
     L.a5x_format_hits.argtypes = [vp, vp, vp, u64, i, i, i, vp, u64, SINK, vp]
     L.a5x_locate_device.argtypes = [vp, vp, vp, u64, i, i, i, vp, u64, vp, vp]
+    L.a5x_stream_reserve.argtypes = [vp, u64, u64]
     L.a5x_split_device.argtypes = [vp, vp, vp, u64, i, i, i, vp, u32, vp, vp, vp, vp]
     _lib = L
     return L

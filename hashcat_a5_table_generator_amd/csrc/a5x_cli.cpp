@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -272,46 +273,54 @@ int main(int argc, char** argv) {
 
   g_tl = getenv("A5X_CLI_TIMELINE") != nullptr;
   TL("main");
-  a5x_ctx* ctx = nullptr;
-  int rc = a5x_create(device, &ctx);
-  TL("context 1 created");
-  if (rc) { fprintf(stderr, "a5_generator: no usable GPU (a5x_create=%d)\n", rc); return 1; }
-  for (auto& t : tables) {
-    rc = a5x_load_table_file(ctx, t.c_str());
-    if (rc) { fprintf(stderr, "%s\n", a5x_last_error(ctx)); a5x_destroy(ctx); return 1; }  // log.Fatal
-  }
-  FILE* f = fopen(dict.c_str(), "rb");
-  if (!f) { perror(dict.c_str()); a5x_destroy(ctx); return 1; }
-  static char obuf[1 << 22];
-  setvbuf(stdout, obuf, _IOFBF, sizeof obuf);
   const int mode = (suball ? A5X_MODE_SUBALL : A5X_MODE_DEFAULT) + (rev ? 1 : 0);
-  if (!hashes.empty() && (rc = load_targets(ctx, hashes.c_str(), algo))) {
-    fprintf(stderr, "a5_generator: %s\n", rc == A5X_E_IO ? "cannot read --hashes file" : a5x_last_error(ctx));
-    a5x_destroy(ctx);
-    fclose(f);
-    return 1;
-  }
   uint64_t B = 1u << 22;           // words per batch
   size_t BB = (size_t)64 << 20;    // word bytes per batch
   size_t chunk = (size_t)64 << 20; // dictionary bytes read at a time
   // (test hooks: small batches / chunks exercise the pipeline and the chunk edges)
   if (const char* e = getenv("A5X_CLI_BATCH")) B = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   if (const char* e = getenv("A5X_CLI_CHUNK")) chunk = std::max<size_t>(1, strtoull(e, nullptr, 10));
-  DictStream ds(f, chunk);
+  static char obuf[1 << 22];
+  setvbuf(stdout, obuf, _IOFBF, sizeof obuf);
   if (hashes.empty()) {
-    // two contexts, two threads, alternate batches, ordered output
-    a5x_ctx* ctx2 = nullptr;
-    rc = a5x_create(device, &ctx2);
-    for (size_t t = 0; rc == 0 && t < tables.size(); t++) rc = a5x_load_table_file(ctx2, tables[t].c_str());
-    if (rc) {
-      fprintf(stderr, "a5_generator: %s\n", ctx2 ? a5x_last_error(ctx2) : "second context");
-      a5x_destroy(ctx2);
-      a5x_destroy(ctx);
-      fclose(f);
+    // The stdout pipeline.  The GPU contexts are created (and their stream buffers made)
+    // on a second thread while this one reads the first batch, which is small so output
+    // starts early; two contexts on two threads then take alternate batches and write
+    // them in batch order.
+    a5x_ctx* cx[2] = {nullptr, nullptr};
+    int irc = 0;
+    std::string ierr;
+    std::thread init([&] {
+      for (int i = 0; i < 2 && irc == 0; i++) {
+        irc = a5x_create(device, &cx[i]);
+        if (irc) {
+          char m[96];
+          snprintf(m, sizeof m, "a5_generator: no usable GPU (a5x_create=%d)", irc);
+          ierr = m;
+          break;
+        }
+        for (size_t t = 0; irc == 0 && t < tables.size(); t++) {
+          irc = a5x_load_table_file(cx[i], tables[t].c_str());
+          if (irc) ierr = a5x_last_error(cx[i]);  // log.Fatal (main.go:43-45)
+        }
+        if (irc == 0) (void)a5x_stream_reserve(cx[i], B, BB);  // (optional warm-up)
+        TL("context %d ready", i + 1);
+      }
+    });
+    FILE* f = fopen(dict.c_str(), "rb");
+    DictStream ds(f, chunk);
+    std::vector<uint8_t> w0;
+    std::vector<uint64_t> o0;
+    const bool have0 = f && ds.next(w0, o0, std::max<uint64_t>(1, B / 16), BB / 16);
+    TL("batch 0 read (%zu words)", o0.size() - 1);
+    init.join();
+    if (irc) {  // the tables are read before the dictionary is opened (main.go:40-56)
+      fprintf(stderr, "%s\n", ierr.c_str());
+      if (f) fclose(f);
       return 1;
     }
-    TL("context 2 ready");
-    a5x_ctx* cx[2] = {ctx, ctx2};
+    if (!f) { perror(dict.c_str()); return 1; }
+    int rc = 0;
     Turn turn;
     std::mutex qmu;
     std::condition_variable qcv;
@@ -349,8 +358,16 @@ int main(int argc, char** argv) {
     for (uint64_t k = 0;; k++) {
       std::vector<uint8_t> words;
       std::vector<uint64_t> off;
-      if (!ds.next(words, off, B, BB)) break;
-      TL("batch %llu read (%zu words)", (unsigned long long)k, off.size() - 1);
+      if (k == 0) {
+        if (!have0) break;
+        words.swap(w0);
+        off.swap(o0);
+      } else {
+        words.reserve(BB + 16 + (1 << 16));
+        off.reserve(std::min<uint64_t>(B, 1u << 24) + 1);
+        if (!ds.next(words, off, B, BB)) break;
+        TL("batch %llu read (%zu words)", (unsigned long long)k, off.size() - 1);
+      }
       std::unique_lock<std::mutex> l(qmu);
       qcv.wait(l, [&] { return q[k & 1].empty() || failed.load(); });  // one batch ahead per context
       if (failed.load()) break;
@@ -369,11 +386,28 @@ int main(int argc, char** argv) {
     fflush(stdout);
     TL("all batches written");
     if (rc) fprintf(stderr, "a5_generator: %s\n", emsg.c_str());
-    a5x_destroy(ctx2);
-    a5x_destroy(ctx);
-    TL("contexts destroyed");
-    return rc ? 2 : 0;
+    fflush(stderr);
+    // (every device call has completed; the process's GPU state goes with it -- tearing
+    // the two contexts down first only costs time)
+    _exit(rc ? 2 : 0);
   }
+  a5x_ctx* ctx = nullptr;
+  int rc = a5x_create(device, &ctx);
+  TL("context 1 created");
+  if (rc) { fprintf(stderr, "a5_generator: no usable GPU (a5x_create=%d)\n", rc); return 1; }
+  for (auto& t : tables) {
+    rc = a5x_load_table_file(ctx, t.c_str());
+    if (rc) { fprintf(stderr, "%s\n", a5x_last_error(ctx)); a5x_destroy(ctx); return 1; }  // log.Fatal
+  }
+  FILE* f = fopen(dict.c_str(), "rb");
+  if (!f) { perror(dict.c_str()); a5x_destroy(ctx); return 1; }
+  if ((rc = load_targets(ctx, hashes.c_str(), algo))) {
+    fprintf(stderr, "a5_generator: %s\n", rc == A5X_E_IO ? "cannot read --hashes file" : a5x_last_error(ctx));
+    a5x_destroy(ctx);
+    fclose(f);
+    return 1;
+  }
+  DictStream ds(f, chunk);
   std::vector<uint8_t> words;
   std::vector<uint64_t> sub;
   std::vector<a5x_hit> hits(1 << 16);

@@ -1767,6 +1767,56 @@ int a5x_keyspace(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_
   return A5X_OK;
 }
 
+// The stdout path's buffers: two HBM range buffers and two pinned host buffers of cap
+// bytes, the copy stream and its events (a5x_expand; a5x_stream_reserve makes them ahead).
+size_t stream_cap() {
+  size_t cap = (size_t)1 << 27;
+  if (const char* e = getenv("A5X_HOST_CHUNK_BYTES")) cap = std::max<size_t>(4096, strtoull(e, nullptr, 10));
+  return cap;
+}
+
+int stream_buffers(a5x_ctx* c, size_t cap) {
+  int rc;
+  if ((rc = grow(c, c->s_out[0], cap)) || (rc = grow(c, c->s_out[1], cap))) return rc;
+  if (c->h_out_cap < cap) {
+    for (auto& h : c->h_out)
+      if (h) (void)hipHostFree(h), h = nullptr;
+    c->h_out_cap = 0;
+    HIPCHK(c, hipHostMalloc((void**)&c->h_out[0], cap, 0));
+    HIPCHK(c, hipHostMalloc((void**)&c->h_out[1], cap, 0));
+    c->h_out_cap = cap;
+  }
+  if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  for (int i = 0; i < 2; i++) {
+    if (!c->ev_exp[i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_exp[i], hipEventDisableTiming));
+    if (!c->ev_cpy[i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_cpy[i], hipEventDisableTiming));
+  }
+  return A5X_OK;
+}
+
+int a5x_stream_reserve(a5x_ctx* c, uint64_t words, uint64_t word_bytes) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c) return A5X_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = stream_buffers(c, stream_cap()))) return rc;
+  // the per-batch keyspace state of a batch of this size, and the staged words
+  if ((rc = grow(c, c->s_words, word_bytes + 16)) || (rc = grow(c, c->s_woff, words + 1)) ||
+      (rc = grow(c, c->count, words + 1)) || (rc = grow(c, c->bytes, words + 1)) ||
+      (rc = grow(c, c->flags, words + 1)) || (rc = grow(c, c->defer, words + 1)) ||
+      (rc = grow(c, c->roff, words + 1)) || (rc = grow(c, c->cplx, words + 1)) ||
+      (rc = grow(c, c->slow_list, words + 1)) || (rc = grow(c, c->big_list, words + 1)) ||
+      (rc = grow(c, c->glob, words + 1)) || (rc = grow(c, c->cand_off, words + 1)) ||
+      (rc = grow(c, c->byte_off, words + 1)) ||
+      (rc = grow(c, c->scan_tmp, a5x_scan_tmp_elems(words + 1) + 16)) ||
+      (rc = grow(c, c->rec, ((words + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC +
+                                (uint64_t)ks_cplx_cap(words) * FW_RMAX + 2)))
+    return rc;
+  if ((rc = upload_table(c))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return A5X_OK;
+}
+
 // The stdout path (main.go:58-68): ranges of <= cap bytes expanded into two HBM buffers
 // in turn; each range's D2H runs on a copy stream into a pinned buffer while the next
 // range expands, and the sink consumes range k while range k + 1 is being copied.
@@ -1784,26 +1834,10 @@ int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t 
   Job J;
   job_open(c, J, c->s_words.p, c->s_woff.p, nw, mode, mn, mx, c->stream);
   if ((rc = job_prepare(c, J, nullptr, nullptr, true))) return rc;
-  size_t cap = (size_t)1 << 27;
-  if (const char* e = getenv("A5X_HOST_CHUNK_BYTES")) cap = std::max<size_t>(4096, strtoull(e, nullptr, 10));
+  const size_t cap = stream_cap();
   std::vector<Range> ranges;
   if ((rc = plan_ranges(c, J, cap, ranges))) return rc;
-  if (!ranges.empty()) {
-    if ((rc = grow(c, c->s_out[0], cap)) || (rc = grow(c, c->s_out[1], cap))) return rc;
-    if (c->h_out_cap < cap) {
-      for (auto& h : c->h_out)
-        if (h) (void)hipHostFree(h), h = nullptr;
-      c->h_out_cap = 0;
-      HIPCHK(c, hipHostMalloc((void**)&c->h_out[0], cap, 0));
-      HIPCHK(c, hipHostMalloc((void**)&c->h_out[1], cap, 0));
-      c->h_out_cap = cap;
-    }
-    if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-    for (int i = 0; i < 2; i++) {
-      if (!c->ev_exp[i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_exp[i], hipEventDisableTiming));
-      if (!c->ev_cpy[i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_cpy[i], hipEventDisableTiming));
-    }
-  }
+  if (!ranges.empty() && (rc = stream_buffers(c, cap))) return rc;
   // error word of each range, copied behind its launch (valid once its copy event fired)
   uint32_t* herr = c->h_scalars + 32;
   auto drain = [&](size_t k) -> int {  // range k has been copied: check it, hand it to the sink

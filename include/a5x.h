@@ -135,6 +135,12 @@ A5X_API int a5x_keyspace(a5x_ctx* ctx, const uint8_t* words, const uint64_t* wor
 A5X_API int a5x_expand(a5x_ctx* ctx, const uint8_t* words, const uint64_t* word_off, uint64_t n_words, int mode,
                        int min, int max, a5x_sink_fn sink, void* user, a5x_stats* stats);
 
+/* Make a5x_expand's buffers ahead of the first call (pinned double buffer, HBM range
+ * buffers, copy stream, the keyspace state of a batch of `words` words / `word_bytes`
+ * bytes, the table upload), so a pipeline's first batch does not pay for them; a host may
+ * call it on a second thread while it reads its first batch.  Optional. */
+A5X_API int a5x_stream_reserve(a5x_ctx* ctx, uint64_t words, uint64_t word_bytes);
+
 /* ---- device-resident API (words already in HBM; used by bench and multi-GPU) -- */
 /* Expands global candidates [cand_begin, cand_end) of the batch (cand_end =
  * UINT64_MAX: to the end) into d_out (d_out[0] = first byte of cand_begin).
