@@ -153,6 +153,22 @@ step_dabl() {  # fused-digest op breakdown: VALU instructions per candidate with
   python3 tools/digest_prof_summary.py breakdown "${ALGOS:-md5 ntlm}"
 }
 
+step_ksab() {  # keyspace-only A/B of liba5x variants under rocprofv3 kernel stats [KSVARIANTS, WL, WORDS]
+  for v in ${KSVARIANTS:-cur}; do
+    local lib=""
+    [ $v != cur ] && lib=$R/hashcat_a5_table_generator_amd/_build_$v/liba5x.so
+    ( cd /tmp && export TMPDIR=/tmp && A5X_LIB_PATH=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats \
+        -d $R/gpurun_out/ksab_${T}_$v -o run --output-format csv -- python3 $R/tools/ks_time.py ${WL:-c3} ${WORDS:-10000000} \
+        > $R/gpurun_out/ksab_${T}_$v.log 2>&1 ) || { echo "ksab $v failed"; tail -3 gpurun_out/ksab_${T}_$v.log; return 19; }
+    echo "-- $v: $(tail -1 gpurun_out/ksab_${T}_$v.log)"
+    python3 - <<PY
+import csv
+for r in list(csv.DictReader(open("$R/gpurun_out/ksab_${T}_$v/run_kernel_stats.csv")))[:6]:
+    print("   %-26s calls %3s avg %9.1f us" % (r["Name"][:26], r["Calls"], float(r["AverageNs"]) / 1e3))
+PY
+  done
+}
+
 step_stamps() {
   timeout -k 10 120 python tools/stamps.py ${WL:-c3} ${SW:-2000000} > gpurun_out/stamps_$T.txt 2>&1 \
     || { tail -5 gpurun_out/stamps_$T.txt; return 17; }
