@@ -32,7 +32,9 @@ struct A5xTableHdr {
   uint32_t max_vlen;
   uint32_t has_empty_key; // the map has "" (matters for -s only, main.go:315)
   uint32_t max_bucket;    // most keys sharing a first byte
-  uint32_t pad[3];
+  uint32_t off_kmatch;    // u64 kmatch[max(nkeys, 1)]: key k's first min(klen, 4) bytes | klen << 32
+  uint32_t off_bucket2;   // u32 bucket2[256]: bucket[b] | bucket[b + 1] << 16 (one read per byte)
+  uint32_t pad;
 };
 
 struct A5xKey {

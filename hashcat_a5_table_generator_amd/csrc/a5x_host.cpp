@@ -337,7 +337,9 @@ int compile_table(a5x_ctx* c) {
   h.off_bucket = sizeof(A5xTableHdr);
   h.off_keys = (uint32_t)al16(h.off_bucket + 257 * sizeof(uint16_t));
   h.off_choices = (uint32_t)al16(h.off_keys + keys.size() * sizeof(A5xKey));
-  h.off_blob = (uint32_t)al16(h.off_choices + ch.size() * sizeof(A5xChoice));
+  h.off_kmatch = (uint32_t)al16(h.off_choices + ch.size() * sizeof(A5xChoice));
+  h.off_bucket2 = (uint32_t)al16(h.off_kmatch + std::max<size_t>(keys.size(), 1) * 8);
+  h.off_blob = (uint32_t)al16(h.off_bucket2 + 256 * 4);
   h.blob_bytes = (uint32_t)blob.size();
   h.total_bytes = (uint32_t)al16(h.off_blob + blob.size() + 8);  // 8 B tail for 4-byte reads
   h.max_klen = max_klen;
@@ -353,6 +355,15 @@ int compile_table(a5x_ctx* c) {
   if (!keys.empty()) memcpy(c->blob.data() + h.off_keys, keys.data(), keys.size() * sizeof(A5xKey));
   if (!ch.empty()) memcpy(c->blob.data() + h.off_choices, ch.data(), ch.size() * sizeof(A5xChoice));
   if (!blob.empty()) memcpy(c->blob.data() + h.off_blob, blob.data(), blob.size());
+  // the walk's compact views (k_keyspace_thread psk_walk): one read per byte, one per key
+  for (size_t k = 0; k < keys.size(); k++) {
+    const uint64_t km = (uint64_t)ch[keys[k].choice_base].first4 | ((uint64_t)keys[k].klen << 32);
+    memcpy(c->blob.data() + h.off_kmatch + 8 * k, &km, 8);
+  }
+  for (int b = 0; b < 256; b++) {
+    const uint32_t v = (uint32_t)bucket[b] | ((uint32_t)bucket[b + 1] << 16);
+    memcpy(c->blob.data() + h.off_bucket2 + 4 * b, &v, 4);
+  }
   c->table_bytes = h.total_bytes;
   return A5X_OK;
 }

@@ -331,6 +331,9 @@ __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const
 #ifndef KS_ULOG
 #define KS_ULOG 16
 #endif
+#ifndef PSK_KB
+#define PSK_KB 2  // bucket keys read together per position (more: a loop)
+#endif
 template <bool COUNT, class PL>
 __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 Lmax, u32 bmax, const Tab& T,
                                          PL& pl, CountAcc& A, bool& cplx, int rmode, uint16_t* ulog = nullptr,
@@ -340,25 +343,30 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
   for (u32 q = 0; q < Lmax; q++) {
     const bool act = act0 && q < L && !cplx;
     if (act) {
-      const u32 b = lw.at(q);
-      const u32 ks = T.bucket[b], ke = T.bucket[b + 1];
+      // three dependent LDS trips per position: the word's 4 bytes, the byte's bucket, the
+      // bucket's keys (compact first-4-bytes | length records, read together)
       const u32 w4 = lds_ld4(lw.base, lw.off + q);
+      const u32 bk = T.bucket2[w4 & 255u];
+      const u32 ks = bk & 0xFFFFu, ke = bk >> 16;
+      const u32 nk1 = T.hdr->nkeys ? T.hdr->nkeys - 1u : 0u;
       u32 nm = 0, kk = 0;
-      for (u32 i = 0; i < bmax; i++) {
-        const u32 k2 = ks + i;
-        if (k2 < ke) {
-          const A5xKey key = T.keys[k2];
-          const u32 kl = key.klen;
-          if (q + kl <= L) {
-            if (kl > 4) {
-              cplx = true;
-            } else {
-              const u32 m = kl >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kl)) - 1u);
-              if ((w4 & m) == T.ch[key.choice_base].first4) { nm++; kk = k2; }
-            }
+      u64 kmv[PSK_KB];
+#pragma unroll
+      for (u32 i = 0; i < PSK_KB; i++) kmv[i] = T.kmatch[min(ks + i, nk1)];
+      auto test = [&](u32 k2, u64 km) {
+        const u32 kl = (u32)(km >> 32) & 0xFFFFu;
+        if (k2 < ke && q + kl <= L) {
+          if (kl > 4) {
+            cplx = true;
+          } else {
+            const u32 m = kl >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kl)) - 1u);
+            if ((w4 & m) == (u32)km) { nm++; kk = k2; }
           }
         }
-      }
+      };
+#pragma unroll
+      for (u32 i = 0; i < PSK_KB; i++) test(ks + i, kmv[i]);
+      for (u32 i = PSK_KB; i < bmax; i++) test(ks + i, T.kmatch[min(ks + i, nk1)]);
       if (nm > 1 || (nm == 1 && q < cur_end)) {
         cplx = true;
       } else if (nm == 1 && !cplx) {

@@ -32,6 +32,8 @@ struct Tab {
   const A5xKey* keys;
   const A5xChoice* ch;
   const uint8_t* blob;
+  const u64* kmatch;   // first min(klen, 4) key bytes | klen << 32
+  const u32* bucket2;  // bucket[b] | bucket[b + 1] << 16
 };
 
 A5X_HD Tab tab_view(const uint8_t* base) {
@@ -41,6 +43,8 @@ A5X_HD Tab tab_view(const uint8_t* base) {
   t.keys = (const A5xKey*)(base + t.hdr->off_keys);
   t.ch = (const A5xChoice*)(base + t.hdr->off_choices);
   t.blob = base + t.hdr->off_blob;
+  t.kmatch = (const u64*)(base + t.hdr->off_kmatch);
+  t.bucket2 = (const u32*)(base + t.hdr->off_bucket2);
   return t;
 }
 
