@@ -539,12 +539,21 @@ def run_stdout(args, D):
         with open(dpath, "wb") as f:
             f.write(text)
         cmd = [CLI, dpath] + sum((["-t", t] for t in tpaths), []) + ["-m", str(args.min), "-x", str(args.max)]
+        tl = {}
         for name, shell in (("cli_devnull", None), ("cli_pipe_wc", " | wc -c")):
             best = None
             for _ in range(2):
                 t0 = time.perf_counter()
                 if shell is None:
-                    r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+                    r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                       env=dict(os.environ, A5X_CLI_TIMELINE="1"))
+                    # the CLI's own clock (ms since main): first byte streamed, last batch written
+                    ev = [ln.split("]", 1) for ln in r.stderr.decode(errors="replace").splitlines()
+                          if ln.startswith("[tl")]
+                    ts = [float(a[3:]) for a, b in ev if "streaming" in b]
+                    te = [float(a[3:]) for a, b in ev if "all batches written" in b]
+                    if ts and te and (not tl or te[0] - ts[0] < tl["stream_ms"]):
+                        tl = {"first_byte_ms": ts[0], "stream_ms": te[0] - ts[0], "main_to_end_ms": te[0]}
                 else:
                     r = subprocess.run(["bash", "-o", "pipefail", "-c", " ".join(cmd) + shell], stdout=subprocess.PIPE,
                                        stderr=subprocess.PIPE)
@@ -581,6 +590,11 @@ def run_stdout(args, D):
             "config": {"workload": f"{args.workload}: {desc}", "words": n, "candidates": tc, "bytes": tb,
                        "dict_bytes": len(text), "pcie_peak_GBps": PCIE_GBS},
             "cli_devnull": rec(runs["cli_devnull"]), "cli_pipe_wc": rec(runs["cli_pipe_wc"]),
+            "cli_devnull_timeline": dict(tl, stream_GB_per_s=tb / (tl["stream_ms"] * 1e-3) / 1e9,
+                                         main_to_end_GB_per_s=tb / (tl["main_to_end_ms"] * 1e-3) / 1e9,
+                                         note="the CLI's own clock (A5X_CLI_TIMELINE): from main() / from its first "
+                                              "streamed byte to the last batch written; the wall rate above adds "
+                                              "process start and exit") if tl else None,
             "a5x_expand_host_sink": rec(lib_t),
             "note": "a5x_generator <dict> -t ... > /dev/null (and | wc -c): file read, batches of 4M words through "
                     "two contexts, pinned double-buffered D2H, fwrite; a5x_expand: the same D2H into a no-op C sink"}

@@ -288,37 +288,42 @@ int main(int argc, char** argv) {
     // starts early; two contexts on two threads then take alternate batches and write
     // them in batch order.
     a5x_ctx* cx[2] = {nullptr, nullptr};
-    int irc = 0;
-    std::string ierr;
-    std::thread init([&] {
-      for (int i = 0; i < 2 && irc == 0; i++) {
-        irc = a5x_create(device, &cx[i]);
-        if (irc) {
-          char m[96];
-          snprintf(m, sizeof m, "a5_generator: no usable GPU (a5x_create=%d)", irc);
-          ierr = m;
-          break;
-        }
-        for (size_t t = 0; irc == 0 && t < tables.size(); t++) {
-          irc = a5x_load_table_file(cx[i], tables[t].c_str());
-          if (irc) ierr = a5x_last_error(cx[i]);  // log.Fatal (main.go:43-45)
-        }
-        if (irc == 0) (void)a5x_stream_reserve(cx[i], B, BB);  // (optional warm-up)
-        TL("context %d ready", i + 1);
+    int irc[2] = {0, 0};
+    std::string ierr[2];
+    auto make_ctx = [&](int i) {
+      irc[i] = a5x_create(device, &cx[i]);
+      if (irc[i]) {
+        char m[96];
+        snprintf(m, sizeof m, "a5_generator: no usable GPU (a5x_create=%d)", irc[i]);
+        ierr[i] = m;
+        return;
       }
-    });
+      for (size_t t = 0; irc[i] == 0 && t < tables.size(); t++) {
+        irc[i] = a5x_load_table_file(cx[i], tables[t].c_str());
+        if (irc[i]) ierr[i] = a5x_last_error(cx[i]);  // log.Fatal (main.go:43-45)
+      }
+      if (irc[i] == 0) (void)a5x_stream_reserve(cx[i], B, BB);  // (optional warm-up)
+      TL("context %d ready", i + 1);
+    };
+    std::thread init0(make_ctx, 0), init1(make_ctx, 1);
+    // the first two batches (the first one small, so output starts early) are read while
+    // the runtime and the contexts come up
     FILE* f = fopen(dict.c_str(), "rb");
     DictStream ds(f, chunk);
-    std::vector<uint8_t> w0;
-    std::vector<uint64_t> o0;
-    const bool have0 = f && ds.next(w0, o0, std::max<uint64_t>(1, B / 16), BB / 16);
-    TL("batch 0 read (%zu words)", o0.size() - 1);
-    init.join();
-    if (irc) {  // the tables are read before the dictionary is opened (main.go:40-56)
-      fprintf(stderr, "%s\n", ierr.c_str());
-      if (f) fclose(f);
-      return 1;
-    }
+    std::vector<uint8_t> pw[2];
+    std::vector<uint64_t> po[2];
+    int npre = 0;
+    if (f && ds.next(pw[0], po[0], std::max<uint64_t>(1, B / 16), BB / 16)) npre = 1;
+    if (npre == 1 && ds.next(pw[1], po[1], B, BB)) npre = 2;
+    TL("first batches read (%d)", npre);
+    init0.join();
+    init1.join();
+    for (int i = 0; i < 2; i++)
+      if (irc[i]) {  // the tables are read before the dictionary is opened (main.go:40-56)
+        fprintf(stderr, "%s\n", ierr[i].c_str());
+        if (f) fclose(f);
+        return 1;
+      }
     if (!f) { perror(dict.c_str()); return 1; }
     int rc = 0;
     Turn turn;
@@ -358,10 +363,10 @@ int main(int argc, char** argv) {
     for (uint64_t k = 0;; k++) {
       std::vector<uint8_t> words;
       std::vector<uint64_t> off;
-      if (k == 0) {
-        if (!have0) break;
-        words.swap(w0);
-        off.swap(o0);
+      if (k < 2) {
+        if ((int)k >= npre) break;
+        words.swap(pw[k]);
+        off.swap(po[k]);
       } else {
         words.reserve(BB + 16 + (1 << 16));
         off.reserve(std::min<uint64_t>(B, 1u << 24) + 1);

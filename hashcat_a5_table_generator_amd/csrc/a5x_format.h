@@ -34,7 +34,7 @@ struct A5xTableHdr {
   uint32_t max_bucket;    // most keys sharing a first byte
   uint32_t off_kmatch;    // u64 kmatch[max(nkeys, 1)]: key k's first min(klen, 4) bytes | klen << 32
   uint32_t off_bucket2;   // u32 bucket2[256]: bucket[b] | bucket[b + 1] << 16 (one read per byte)
-  uint32_t pad;
+  uint32_t off_cval;      // u64 cval[nchoices]: choice's first min(len, 7) bytes | min(len, 255) << 56
 };
 
 struct A5xKey {

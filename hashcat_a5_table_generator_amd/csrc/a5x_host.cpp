@@ -339,7 +339,8 @@ int compile_table(a5x_ctx* c) {
   h.off_choices = (uint32_t)al16(h.off_keys + keys.size() * sizeof(A5xKey));
   h.off_kmatch = (uint32_t)al16(h.off_choices + ch.size() * sizeof(A5xChoice));
   h.off_bucket2 = (uint32_t)al16(h.off_kmatch + std::max<size_t>(keys.size(), 1) * 8);
-  h.off_blob = (uint32_t)al16(h.off_bucket2 + 256 * 4);
+  h.off_cval = (uint32_t)al16(h.off_bucket2 + 256 * 4);
+  h.off_blob = (uint32_t)al16(h.off_cval + std::max<size_t>(ch.size(), 1) * 8);
   h.blob_bytes = (uint32_t)blob.size();
   h.total_bytes = (uint32_t)al16(h.off_blob + blob.size() + 8);  // 8 B tail for 4-byte reads
   h.max_klen = max_klen;
@@ -363,6 +364,12 @@ int compile_table(a5x_ctx* c) {
   for (int b = 0; b < 256; b++) {
     const uint32_t v = (uint32_t)bucket[b] | ((uint32_t)bucket[b + 1] << 16);
     memcpy(c->blob.data() + h.off_bucket2 + 4 * b, &v, 4);
+  }
+  for (size_t i = 0; i < ch.size(); i++) {  // the planner's choice bytes, one read each
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < ch[i].len && k < 7; k++) v |= (uint64_t)blob[ch[i].blob_off + k] << (8 * k);
+    v |= (uint64_t)std::min<uint32_t>(ch[i].len, 255) << 56;
+    memcpy(c->blob.data() + h.off_cval + 8 * i, &v, 8);
   }
   c->table_bytes = h.total_bytes;
   return A5X_OK;

@@ -34,6 +34,7 @@ struct Tab {
   const uint8_t* blob;
   const u64* kmatch;   // first min(klen, 4) key bytes | klen << 32
   const u32* bucket2;  // bucket[b] | bucket[b + 1] << 16
+  const u64* cval;     // choice bytes (<= 7) | len << 56
 };
 
 A5X_HD Tab tab_view(const uint8_t* base) {
@@ -45,6 +46,7 @@ A5X_HD Tab tab_view(const uint8_t* base) {
   t.blob = base + t.hdr->off_blob;
   t.kmatch = (const u64*)(base + t.hdr->off_kmatch);
   t.bucket2 = (const u32*)(base + t.hdr->off_bucket2);
+  t.cval = (const u64*)(base + t.hdr->off_cval);
   return t;
 }
 
@@ -193,6 +195,7 @@ struct Unit {
   int maxd;        // longest choice - span
   u32 nm;          // key matches in the unit (bounds the substitutions of a choice)
   u32 key;         // lone match: its key index
+  u32 cb;          // lone match: the key's choice_base (choices cb + a, a < R)
   u32 k;           // cluster: number of matches (0 for a lone match)
   u64 m0, m1;      // cluster matches 0-3 / 4-7, 16 bits each: (pos - s) << 10 | key index
   bool ok;         // cluster fits FW_UMAXM matches, FW_UMAXR choices of <= FW_PLEN bytes
@@ -299,7 +302,7 @@ A5X_HD bool next_unit(const W& wd, u32 L, u32& p, const Tab& T, Unit& U) {
     U.s = p; U.e = e; U.nm = nmatch;
     if (nmatch == 1) {
       const A5xKey key = T.keys[k0];
-      U.key = k0; U.k = 0;
+      U.key = k0; U.k = 0; U.cb = key.choice_base;
       U.R = key.nvals + 1u; U.ml = key.maxclen; U.mnl = key.minclen;
       U.spos = key.sum_dpos; U.sneg = key.sum_dneg; U.maxd = key.maxdelta;
       U.ok = true;
@@ -316,10 +319,10 @@ A5X_HD bool next_unit(const W& wd, u32 L, u32& p, const Tab& T, Unit& U) {
 // bytes and length of choice a of a unit
 template <class W>
 A5X_HD u64 unit_choice(const W& wd, const Unit& U, const Tab& T, u32 a, u32& len) {
-  if (U.k == 0) {
-    const u32 ci = T.keys[U.key].choice_base + a;
-    len = T.ch[ci].len;
-    return choice7(T, ci);
+  if (U.k == 0) {  // (entries hold <= FW_PLEN = 7 bytes: longer choices never get here)
+    const u64 e = T.cval[U.cb + a];
+    len = (u32)(e >> 56);
+    return e & FW_M56;
   }
   Unit V = U;
   u64 v = 0;
@@ -567,7 +570,7 @@ A5X_HD u32 fb_balanced_cap(u64 P, u32 slack8 = FB_BAL_SLACK8) {
 A5X_HD void lone_unit(const Tab& T, u32 s, u32 k, Unit& U) {
   const A5xKey key = T.keys[k];
   U.s = s; U.e = s + key.klen; U.nm = 1;
-  U.key = k; U.k = 0; U.m0 = 0; U.m1 = 0;
+  U.key = k; U.k = 0; U.m0 = 0; U.m1 = 0; U.cb = key.choice_base;
   U.R = key.nvals + 1u; U.ml = key.maxclen; U.mnl = key.minclen;
   U.spos = key.sum_dpos; U.sneg = key.sum_dneg; U.maxd = key.maxdelta;
   U.ok = true;
