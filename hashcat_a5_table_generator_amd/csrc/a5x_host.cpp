@@ -1934,7 +1934,7 @@ int a5x_debug_plan_word(a5x_ctx* c, const uint8_t* word, size_t len, int mn, int
   // build, FB_BAL_SLACK8, for the window simulation in tools/window_sim.py)
   u32 slack = FB_BAL_SLACK8;
   if (const char* e = getenv("A5X_BAL_SLACK8")) slack = (u32)atoi(e);
-  const Plan P = plan_word_rule<true>(gw, (u32)len, T, sk, C.maxR, fb_balanced_cap(C.count + 1, slack));
+  const Plan P = plan_word<true>(gw, (u32)len, T, sk, fb_balanced_cap(C.count + 1, slack));
   wrec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
   wrec[FX_ZSLOT] = 0;
   if (!P.ok || P.ng != ff_ng(C.flags) || P.ne != ff_ne(C.flags) || P.np != ff_np(C.flags))

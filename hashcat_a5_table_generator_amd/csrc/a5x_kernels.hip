@@ -266,7 +266,6 @@ __device__ __forceinline__ u32 wave_append(bool pred, u32* ctr) {
 // k_keyspace_thread's open group holds KS_GCAP entries (a unit with more choices
 // makes the word complex: k_keyspace_cplx plans it with FW_UMAXR)
 #define KS_GCAP 8
-static_assert(KS_GCAP == PLAN_GCAP, "k_keyspace_thread plans with classify_word's group-cap rule");
 
 // The open group of plan_word lives in LDS (<= FW_UMAXR u64 per lane, lane-strided);
 // entries and group descriptors go straight to the word's record in HBM.
@@ -311,10 +310,10 @@ __device__ __forceinline__ u32 ks_classify(const W& wd, u64 L64, const Tab& T, c
 
 template <class W>
 __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const KsArgs& a, u32 f, u64 count, u64* rec,
-                                         u64* g, u32 maxR) {
+                                         u64* g) {
   DevRecSink sk;
   sk.g = g; sk.c = g + 256 * FW_UMAXR; sk.rec = rec; sk.np = ff_np(f);
-  const Plan P = plan_word_rule<true>(wd, L, T, sk, maxR, fb_balanced_cap(count + 1));
+  const Plan P = plan_word<true>(wd, L, T, sk, fb_balanced_cap(count + 1));
   rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
   if (!P.ok || P.ng != ff_ng(f) || P.ne != ff_ne(f) || P.np != ff_np(f)) atomicOr(a.err, A5X_DERR_STATE);
 }
@@ -342,7 +341,7 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
   u32 cur_end = 0;
   u64 seen = 0;
   for (u32 q = 0; q < Lmax; q++) {
-    const bool act = act0 && q < L && !cplx && q >= cur_end;
+    const bool act = act0 && q < L && !cplx;
     if (act) {
       // three dependent LDS trips per position: the word's 4 bytes, the byte's bucket, the
       // bucket's keys (compact first-4-bytes | length records, read together)
@@ -350,8 +349,7 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
       const u32 bk = T.bucket2[w4 & 255u];
       const u32 ks = bk & 0xFFFFu, ke = bk >> 16;
       const u32 nk1 = T.hdr->nkeys ? T.hdr->nkeys - 1u : 0u;
-      u32 nm = 0, kk = 0, kl1 = 0;
-      bool lk = false;  // a key longer than 4 bytes fits at q (not compared here)
+      u32 nm = 0, kk = 0;
       u64 kmv[PSK_KB];
 #pragma unroll
       for (u32 i = 0; i < PSK_KB; i++) kmv[i] = T.kmatch[min(ks + i, nk1)];
@@ -359,36 +357,17 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
         const u32 kl = (u32)(km >> 32) & 0xFFFFu;
         if (k2 < ke && q + kl <= L) {
           if (kl > 4) {
-            lk = true;
+            cplx = true;
           } else {
             const u32 m = kl >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kl)) - 1u);
-            if ((w4 & m) == (u32)km) { nm++; kk = k2; kl1 = kl; }
+            if ((w4 & m) == (u32)km) { nm++; kk = k2; }
           }
         }
       };
 #pragma unroll
       for (u32 i = 0; i < PSK_KB; i++) test(ks + i, kmv[i]);
       for (u32 i = PSK_KB; i < bmax; i++) test(ks + i, T.kmatch[min(ks + i, nk1)]);
-      if (!rmode && (lk || nm > 1 || (nm == 1 && kl1 > 1))) {
-        // not a lone one-byte match: the general unit at or after q -- several keys here,
-        // a multi-byte key (matches inside its span join it: a cluster), a long key --
-        // exactly as k_keyspace_cplx's walk finds it (next_unit); units past the group
-        // cap go to that kernel.  Cluster units make the build pass walk again (ulog).
-        Unit U;
-        u32 p = q;
-        if (next_unit(lw, L, p, T, U)) {
-          if (U.R > KS_GCAP) {
-            cplx = true;
-          } else {
-            if (COUNT) count_unit(A, U);
-            if (!(KS_ABL & 2)) pl.unit(U);
-            cur_end = U.e;
-            if (COUNT && ulog) *nlog = (u32)KS_ULOG + 1u;
-          }
-        } else {
-          cur_end = L;  // no unit at or after q
-        }
-      } else if (lk || nm > 1 || (nm == 1 && q < cur_end)) {
+      if (nm > 1 || (nm == 1 && q < cur_end)) {
         cplx = true;
       } else if (nm == 1 && !cplx) {
         Unit U;
@@ -509,7 +488,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     {
       u64* rec = a.rec + tile * FW_TILE_REC + ro;
       DevRecSink sk;
-      sk.g = gbuf + tid; sk.c = nullptr; sk.rec = rec; sk.np = ff_np(f);  // (clusters: per-choice enumeration)
+      sk.g = gbuf + tid; sk.c = sk.g; sk.rec = rec; sk.np = ff_np(f);  // no clusters here
       Planner<true, LWord, DevRecSink, KS_GCAP> pb(lw, T, sk, build ? fb_balanced_cap(C.count + 1) : 0u);
       CountAcc A2;
       bool c2 = false;
@@ -636,7 +615,7 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
     u64* rec = a.rec + a.cplx_base + (u64)i * FW_RMAX;
     {
       DevRecSink sk;
-      sk.g = gbuf + tid; sk.c = nullptr; sk.rec = rec; sk.np = ff_np(f);
+      sk.g = gbuf + tid; sk.c = sk.g; sk.rec = rec; sk.np = ff_np(f);
       Planner<true, LWord, DevRecSink, KS_GCAP> pb(lw, T, sk, rf ? fb_balanced_cap(C.count + 1) : 0u);
       CountAcc A2;
       bool c2 = false;
@@ -699,12 +678,12 @@ __global__ void __launch_bounds__(256) k_keyspace_cplx(KsArgs a) {
       LWord lw;
       lw.base = wst; lw.off = threadIdx.x * KC_SLOT;
       f = ks_classify(lw, L64, T, a, C);
-      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(lw, (u32)L64, T, a, f, C.count, rec, gbuf + threadIdx.x, C.maxR);
+      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(lw, (u32)L64, T, a, f, C.count, rec, gbuf + threadIdx.x);
     } else {
       GWord gw;
       gw.p = a.words + s;
       f = ks_classify(gw, L64, T, a, C);
-      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(gw, (u32)L64, T, a, f, C.count, rec, gbuf + threadIdx.x, C.maxR);
+      if ((f & A5X_WF_FAST) && C.count > 0 && fits) ks_build(gw, (u32)L64, T, a, f, C.count, rec, gbuf + threadIdx.x);
     }
     if ((f & A5X_WF_FAST) && C.count > 0) {
       if (fits) a.roff[w] = (u32)(a.cplx_base + (u64)i * FW_RMAX);

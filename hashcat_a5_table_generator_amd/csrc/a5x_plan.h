@@ -334,7 +334,7 @@ A5X_HD u64 unit_choice(const W& wd, const Unit& U, const Tab& T, u32 a, u32& len
 // unit_choice with a cluster's choices already enumerated into cb (stride cs)
 template <class W>
 A5X_HD u64 unit_choice_b(const W& wd, const Unit& U, const Tab& T, u32 a, u32& len, const u64* cb, u32 cs) {
-  if (U.k == 0 || !cb) return unit_choice(wd, U, T, a, len);  // (no buffer: enumerate per choice)
+  if (U.k == 0) return unit_choice(wd, U, T, a, len);
   const u64 e = cb[a * cs];
   len = (u32)(e >> 56);
   return e & FW_M56;
@@ -458,7 +458,7 @@ struct Planner {
     u64* cb = nullptr;
     u32 cs = 1;
     if constexpr (BUILD) {
-      if (U.k && sk.cbuf()) {  // cluster: all choices once (unit_choice would re-enumerate per entry)
+      if (U.k) {  // cluster: all choices once (unit_choice would re-enumerate per entry)
         cb = sk.cbuf(); cs = sk.cstride();
         Unit V = U;
         cluster_choices(wd, V, T, -2, cb, nullptr, cs);
@@ -533,9 +533,9 @@ struct Planner {
   }
 };
 
-template <bool BUILD, class W, class S, u32 CAP = FW_UMAXR>
+template <bool BUILD, class W, class S>
 A5X_HD Plan plan_word(const W& wd, u32 L, const Tab& T, S& sk, u32 balanced_cap = 0) {
-  Planner<BUILD, W, S, CAP> pl(wd, T, sk, balanced_cap);
+  Planner<BUILD, W, S> pl(wd, T, sk, balanced_cap);
   u32 p = 0;
   Unit U;
   while (pl.P.ok && next_unit(wd, L, p, T, U)) pl.unit(U);
@@ -582,7 +582,6 @@ A5X_HD void lone_unit(const Tab& T, u32 s, u32 k, Unit& U) {
 struct WordClass {
   u64 count, bytes;
   u32 flags;       // A5X_WF_* (+ FAST fields) or A5X_WF_DEFER
-  u32 maxR;        // most choices of one unit
   bool ovf;        // count/bytes overflow u64
   bool clusters;   // the word has overlapping-key units (the slow path needs the DP)
 };
@@ -593,17 +592,15 @@ struct WordClass {
 struct CountAcc {
   u64 P, Dp, Dn;
   u32 nmatch, nunits, maxl;
-  u32 maxR;        // most choices of one unit (which group cap plans the word: PLAN_GCAP)
   bool bin, clusters, ok, ovf;
 };
 A5X_HD void count_init(CountAcc& A, u32 L) {
-  A.P = 1; A.Dp = 0; A.Dn = 0; A.nmatch = 0; A.nunits = 0; A.maxl = L + 1; A.maxR = 0;
+  A.P = 1; A.Dp = 0; A.Dn = 0; A.nmatch = 0; A.nunits = 0; A.maxl = L + 1;
   A.bin = true; A.clusters = false; A.ok = true; A.ovf = false;
 }
 A5X_HD void count_unit(CountAcc& A, const Unit& U) {
   A.nunits++;
   A.nmatch += U.nm;
-  A.maxR = umax32(A.maxR, U.R);
   if (U.k) {
     A.clusters = true;
     if (!U.ok) A.ok = false;
@@ -621,7 +618,7 @@ A5X_HD void count_unit(CountAcc& A, const Unit& U) {
 // slow kernel's per-wave ring (a radix word's longest candidate must fit).
 A5X_HD WordClass classify_finish(const CountAcc& A, const Plan& PL, u32 L, int mn, int mx, u32 ringmax) {
   WordClass C;
-  C.count = 0; C.bytes = 0; C.flags = 0; C.ovf = false; C.clusters = A.clusters; C.maxR = A.maxR;
+  C.count = 0; C.bytes = 0; C.flags = 0; C.ovf = false; C.clusters = A.clusters;
   if (A.ok && A.nunits == 0) {
     C.flags = A5X_WF_RADIX | A5X_WF_FAST;
     return C;
@@ -657,25 +654,19 @@ A5X_HD WordClass classify_finish(const CountAcc& A, const Plan& PL, u32 L, int m
   return C;
 }
 
-// The group cap a word is planned with: PLAN_GCAP (= k_keyspace_thread's register-light open
-// group) unless a unit has more choices, then FW_UMAXR.  Every kernel that plans a word
-// (k_keyspace_thread, k_keyspace_cplx) and the host replay use this rule, so a word gets the
-// same plan -- and FAST or not, i.e. the same candidate numbering -- wherever it is planned.
-#define PLAN_GCAP 8u
-
 // One walk over the units: counts and the piece plan (count mode) together.
-template <u32 CAP = FW_UMAXR, class W>
-A5X_HD WordClass classify_word_cap(const W& wd, u32 L, const Tab& T, int mn, int mx, u32 ringmax) {
+template <class W>
+A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx, u32 ringmax) {
   if (mx < 1 || L == 0) {  // processWord emits nothing
     WordClass C;
-    C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false; C.maxR = 0;
+    C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
     C.flags = A5X_WF_RADIX | A5X_WF_FAST;
     return C;
   }
   CountAcc A;
   count_init(A, L);
   NullSink ns;
-  Planner<false, W, NullSink, CAP> pl(wd, T, ns);
+  Planner<false, W, NullSink> pl(wd, T, ns);
   u32 p = 0;
   Unit U;
   while (next_unit(wd, L, p, T, U)) {
@@ -685,19 +676,6 @@ A5X_HD WordClass classify_word_cap(const W& wd, u32 L, const Tab& T, int mn, int
   }
   pl.finish(L);
   return classify_finish(A, pl.P, L, mn, mx, ringmax);
-}
-
-template <class W>
-A5X_HD WordClass classify_word(const W& wd, u32 L, const Tab& T, int mn, int mx, u32 ringmax) {
-  const WordClass C = classify_word_cap<PLAN_GCAP>(wd, L, T, mn, mx, ringmax);
-  return C.maxR > PLAN_GCAP ? classify_word_cap<FW_UMAXR>(wd, L, T, mn, mx, ringmax) : C;
-}
-
-// plan_word with the group cap of classify_word's rule (maxR from the classification)
-template <bool BUILD, class W, class S>
-A5X_HD Plan plan_word_rule(const W& wd, u32 L, const Tab& T, S& sk, u32 maxR, u32 balanced_cap = 0) {
-  return maxR > PLAN_GCAP ? plan_word<BUILD, W, S, FW_UMAXR>(wd, L, T, sk, balanced_cap)
-                          : plan_word<BUILD, W, S, PLAN_GCAP>(wd, L, T, sk, balanced_cap);
 }
 
 // ---------------------------------------------------------------------------
