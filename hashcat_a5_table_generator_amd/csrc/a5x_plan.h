@@ -376,6 +376,9 @@ struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
 #ifndef PL_FIXED_TRIP
 #define PL_FIXED_TRIP 0  // 1: CAP-iteration entry loops for every group (A/B)
 #endif
+#ifndef PL_SPLIT_CAP
+#define PL_SPLIT_CAP 8   // groups of <= this many entries merge read-all-then-write-all (registers)
+#endif
 
 // Cut a unit-radix word into pieces (see the record format above), one unit at a
 // time (unit() in word order, then finish()).  BUILD: also write the entries and
@@ -468,7 +471,29 @@ struct Planner {
       // merge: entry a1 + cR * a2 = old[a1] ++ run ++ choice a2 (descending: in place;
       // fixed trip count so lanes of a wave stay together)
       const u32 nR = cR * Ru;
-      if constexpr (BUILD) {
+      if constexpr (BUILD && CAP <= PL_SPLIT_CAP) {
+        // small groups: every old entry and choice read first (one round trip, nothing
+        // written yet), then every new entry written -- no read waits behind a write
+        const u64 rb = run ? wd.ld(prev, run) : 0ull;
+        const u32 inv = (256u + cR - 1u) / cR;  // t / cR = (t * inv) >> 8 for t < 16
+        u64 ov[CAP], cv[CAP];
+        u32 cl[CAP];
+#pragma unroll
+        for (u32 t = 0; t < CAP; t++) {
+          const u32 a2 = (t * inv) >> 8, a1 = t - a2 * cR;
+          cl[t] = 0;
+          ov[t] = t < nR ? sk.gld(a1) : 0ull;
+          cv[t] = t < nR ? unit_choice_b(wd, U, T, a2, cl[t], cb, cs) : 0ull;
+        }
+#pragma unroll
+        for (u32 t = 0; t < CAP; t++) {
+          if (t < nR) {
+            const u32 ol = fw_len(ov[t]);
+            const u64 v = (ov[t] & FW_M56) | (rb << (8 * ol)) | (cv[t] << (8 * (ol + run)));
+            sk.gst(t, (v & FW_M56) | fw_meta(ol + run + cl[t], nR));
+          }
+        }
+      } else if constexpr (BUILD) {
         const u64 rb = run ? wd.ld(prev, run) : 0ull;
         const u32 inv = (256u + cR - 1u) / cR;  // t / cR = (t * inv) >> 8 for t < 16
         for (int t = (PL_FIXED_TRIP ? CAP : nR) - 1; t >= 0; t--) {
@@ -493,7 +518,19 @@ struct Planner {
       }
       open = true; cR = Ru; cmax = rem + ml; cmin = rem + U.mnl; cpi = P.np;
       P.np++;
-      if constexpr (BUILD) {
+      if constexpr (BUILD && CAP <= PL_SPLIT_CAP) {  // (read every choice, then write)
+        const u64 rb = rem ? wd.ld(off, rem) : 0ull;
+        u64 cv[CAP];
+        u32 cl[CAP];
+#pragma unroll
+        for (u32 a = 0; a < CAP; a++) {
+          cl[a] = 0;
+          cv[a] = a < Ru ? unit_choice_b(wd, U, T, a, cl[a], cb, cs) : 0ull;
+        }
+#pragma unroll
+        for (u32 a = 0; a < CAP; a++)
+          if (a < Ru) sk.gst(a, ((rb | (cv[a] << (8 * rem))) & FW_M56) | fw_meta(rem + cl[a], Ru));
+      } else if constexpr (BUILD) {
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
         for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : Ru); a++) {
           if (a >= Ru) continue;
