@@ -70,6 +70,7 @@ enum : uint32_t {
   A5X_WF_DEFER = 1u << 4,   // keyspace needs the wave-level DP kernel
   A5X_WF_FAST = 1u << 5,    // radix, <= 64 B, piece plan fits (plan_word): k_expand_fast
   A5X_WF_GLOB = 1u << 6,    // (with BIG) beyond the pass-B LDS budget: pass G, global scratch
+  A5X_WF_VIRT = 1u << 7,    // (with FAST) -s / -s -r word split into FAST sub-words (k_keyspace_vsub)
   A5X_WF_ERR_OVF = 1u << 8, // count/bytes overflow u64
   A5X_WF_ERR_BIG = 1u << 9, // exceeds pass-B limits
 };

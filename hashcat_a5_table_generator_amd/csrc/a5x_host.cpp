@@ -99,6 +99,14 @@ struct a5x_ctx {
   uint64_t mseg = 4096;  // candidates per mode-engine item (C5 -r: most words one item, sized by k_mode_count)
   uint64_t rov_need = 0;  // -r/-s FAST probe: overflow slots a previous batch needed (k_keyspace_rprobe)
   uint64_t cplx_need = 0;  // default mode: complex-word record slots a previous batch needed
+  // -s / -s -r virtual words (k_keyspace_vsub, k_vwords_fill): the words left to the mode
+  // engine, per-word sub-word counts / record sizes and their scans, the sub-word records,
+  // and the virtual word list k_expand_fast runs on
+  DevBuf<uint32_t> m_vl;
+  DevBuf<uint64_t> vn, vrsz, vpre, vrpre, vrec, vrec2, vcand_off, vbyte_off;
+  DevBuf<uint16_t> vocc;  // per word 16 u16: occurrence rows (k_keyspace_thread -> k_keyspace_vsub)
+  DevBuf<uint32_t> vflags, vroff, vmap, vobase;
+  uint64_t vrec_need = 0;  // sub-word record u64 a previous batch needed
   // fused digest + lookup (a5x_digest.hip)
   int t_algo = -1;
   uint64_t n_targets = 0;
@@ -440,6 +448,8 @@ struct Batch {  // device-side per-batch state after keyspace
   uint32_t nglob = 0;  // pass G words (on the BIG list, expanded by k_expand_g)
   bool rfast = false;  // -r / -s / -s -r: FAST words probed by k_keyspace_thread (k_expand_fast)
   uint64_t nmode = 0;  // -r / -s / -s -r: words left to the mode engine (0: no mode-item launch)
+  bool virt = false;   // -s / -s -r: virtual words present; k_expand_fast runs on the virtual list
+  uint64_t nv = 0;     // its entries
   const uint64_t* cand_off = nullptr;
   const uint64_t* byte_off = nullptr;
 };
@@ -654,11 +664,15 @@ int upload_mtable(a5x_ctx* c) {
 }
 
 A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode,
-                          int mn, int mx, bool rfast = false) {
+                          int mn, int mx, bool rfast = false, bool virt = false) {
   A5xModeLaunch M;
   memset(&M, 0, sizeof M);
   M.rfast = rfast ? 1 : 0;
   if (rfast) { M.rec = c->rec.p; M.roff = c->roff.p; }
+  if (virt) {
+    M.vpre = c->vpre.p; M.vcand_off = c->vcand_off.p; M.vbyte_off = c->vbyte_off.p;
+    M.vroff = c->vroff.p; M.vrec = c->vrec2.p;
+  }
   M.mtab = c->d_mtab; M.mtab_bytes = c->mtab_bytes; M.words = d_words; M.woff = d_woff; M.nw = nw;
   M.mode = mode; M.mn = mn; M.mx = mx; M.SEG = c->mseg;
   M.count = c->count.p; M.nseg = c->m_nseg.p; M.flags = c->flags.p;
@@ -670,6 +684,55 @@ A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_
   M.glob_list = c->glob.p; M.glob_n = c->d_scalars + 7;
   if (c->m_nglob) { M.gscr = c->mgscr; M.gslots = A5X_G_SLOTS; }
   return M;
+}
+
+// The virtual word list of a -s / -s -r batch with virtual words (k_keyspace_vsub): every
+// word one entry, a virtual word one per sub-word, records copied in list order; the
+// chunk -> first entry map of k_expand_fast over it.  byte_off null: no output layout
+// (fused digest).  Synchronises once.
+int build_virtual(a5x_ctx* c, uint64_t nw, const uint64_t* d_cand_off, const uint64_t* d_byte_off, hipStream_t st,
+                  Batch* B) {
+  int rc;
+  if ((rc = grow(c, c->vpre, nw + 1)) || (rc = grow(c, c->vrpre, nw + 1))) return rc;
+  HIPCHK(c, a5x_launch_vwords_sizes(c->flags.p, d_cand_off, nw, c->vn.p, c->vrsz.p, st));
+  HIPCHK(c, a5x_launch_scan(c->vn.p, c->vrsz.p, nw, c->vpre.p, c->vrpre.p, c->scan_tmp.p, c->d_scalars + 2, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_totals + 4, c->vpre.p + nw, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_totals + 5, c->vrpre.p + nw, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  const uint64_t nv = nw + c->h_totals[4], nrec = c->h_totals[5];
+  if (nv > 0xffffffffull || nrec + 4 > 0xffffffffull)
+    return fail(c, A5X_E_ARG, "batch of %llu words is too large for one -s call (virtual word list)",
+                (unsigned long long)nw);
+  if ((rc = grow(c, c->vcand_off, nv + 1)) || (rc = grow(c, c->vbyte_off, nv + 1)) ||
+      (rc = grow(c, c->vflags, nv + 1)) || (rc = grow(c, c->vroff, nv + 1)) || (rc = grow(c, c->vmap, nv + 1)) ||
+      (rc = grow(c, c->vobase, nv + 1)) || (rc = grow(c, c->vrec2, nrec + 4)))
+    return rc;
+  A5xVwLaunch V;
+  V.flags = c->flags.p; V.cand_off = d_cand_off; V.byte_off = d_byte_off; V.roff = c->roff.p; V.rec = c->rec.p;
+  V.vrec = c->vrec.p; V.vpre = c->vpre.p; V.vrpre = c->vrpre.p; V.nw = nw;
+  V.vcand_off = c->vcand_off.p; V.vbyte_off = c->vbyte_off.p; V.vflags = c->vflags.p; V.vroff = c->vroff.p;
+  V.vmap = c->vmap.p; V.vobase = c->vobase.p; V.vrec2 = c->vrec2.p;
+  HIPCHK(c, a5x_launch_vwords_fill(V, st));
+  if (B->total_cands) {
+    const uint64_t nchunks = (B->total_cands + c->chunk - 1) / c->chunk;
+    if ((rc = grow(c, c->chunk_w0, nchunks + 1))) return rc;
+    HIPCHK(c, a5x_launch_plan(c->vcand_off.p, nv, c->chunk, c->chunk_w0.p, st));
+  }
+  B->virt = true;
+  B->nv = nv;
+  return A5X_OK;
+}
+
+// k_expand_fast over a -r / -s / -s -r batch's FAST words (the virtual word list when the
+// batch has virtual words)
+A5xExpLaunch exp_launch_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mn, int mx,
+                             const Batch& B) {
+  A5xExpLaunch E = exp_launch(c, d_words, d_woff, nw, mn, mx, B);
+  if (B.virt) {
+    E.nw = B.nv; E.cand_off = c->vcand_off.p; E.byte_off = c->vbyte_off.p; E.flags = c->vflags.p;
+    E.roff = c->vroff.p; E.rec = c->vrec2.p; E.rec_n = c->vrec2.cap; E.vmap = c->vmap.p; E.vobase = c->vobase.p;
+  }
+  return E;
 }
 
 // Keyspace of the -r / -s / -s -r engines: per-word counts (DP), items of mseg
@@ -709,6 +772,8 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   B->byte_off = d_byte_off;
   B->nbig = B->nslow = 0;
   B->rfast = false;
+  B->virt = false;
+  B->nv = 0;
   if (nw == 0) {
     HIPCHK(c, hipMemsetAsync(d_cand_off, 0, 8, st));
     HIPCHK(c, hipMemsetAsync(d_byte_off, 0, 8, st));
@@ -737,6 +802,13 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   const bool mct = (mode == A5X_MODE_SUBALL || mode == A5X_MODE_SUBALL_REVERSE) && mx >= 0 && !has_empty &&
                    !getenv("A5X_NO_MCT");
   if ((rfast || mct) && ((rc = grow(c, c->m_cl, nw + 1)) || (rc = grow(c, c->m_cl2, nw + 1)))) return rc;
+  // -s / -s -r words the probe refused for repeated patterns: split into FAST sub-words
+  // (k_keyspace_vsub) before the mode engine counts the rest
+  const bool vsub = rfast && mct && mode != A5X_MODE_REVERSE && !getenv("A5X_NO_VSUB");
+  const uint64_t vcap = std::min<uint64_t>(0xfffffff0ull, std::max<uint64_t>(nw * 64 + 4096, c->vrec_need));
+  if (vsub && ((rc = grow(c, c->m_vl, nw + 1)) || (rc = grow(c, c->vn, nw + 1)) || (rc = grow(c, c->vrsz, nw + 1)) ||
+               (rc = grow(c, c->vrec, vcap + 2)) || (rc = grow(c, c->vocc, 16 * (nw + 1)))))
+    return rc;
   // (the probe's overflow slots: words a keyspace tile could not decide, k_keyspace_rprobe)
   const uint64_t rtiles = ((nw + FW_TILE - 1) / FW_TILE) * (uint64_t)FW_TILE_REC;
   const uint64_t rcap = std::min<uint64_t>(nw, std::max<uint64_t>(ks_cplx_cap(nw), c->rov_need));
@@ -756,12 +828,19 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     K.defer_list = c->m_cl.p; K.defer_n = c->d_scalars + 12;
     K.cplx_list = c->cplx.p; K.cplx_n = c->d_scalars + 14; K.cplx_cap = (uint32_t)rcap; K.cplx_base = rtiles;
     K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nw + 255) / 256, (uint64_t)c->cus * 2));
+    K.vocc = vsub ? c->vocc.p : nullptr;
     HIPCHK(c, a5x_launch_keyspace(K, st));
+    if (vsub) {
+      K.vout_list = c->m_vl.p; K.vout_n = c->d_scalars + 15;
+      K.vn = c->vn.p; K.vrsz = c->vrsz.p; K.vrec = c->vrec.p;
+      K.vrec_n = (uint64_t*)(c->d_scalars + 10); K.vrec_cap = vcap;
+      HIPCHK(c, a5x_launch_vsub(K, st));
+    }
   }
   A5xModeLaunch M = mode_launch(c, d_words, d_woff, nw, mode, mn, mx, rfast);
   if (mct) {
-    M.in_list = rfast ? c->m_cl.p : nullptr;
-    M.in_n = rfast ? c->d_scalars + 12 : nullptr;
+    M.in_list = vsub ? c->m_vl.p : rfast ? c->m_cl.p : nullptr;
+    M.in_n = vsub ? c->d_scalars + 15 : rfast ? c->d_scalars + 12 : nullptr;
     M.cl_list = rfast ? c->m_cl2.p : c->m_cl.p;
     M.cl_n = c->d_scalars + (rfast ? 13 : 12);
     HIPCHK(c, a5x_launch_mode_count_thread(M, st));
@@ -782,7 +861,32 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     c->rov_need = c->h_scalars[14];
     return run_keyspace_mode(c, d_words, d_woff, nw, mode, mn, mx, d_cand_off, d_byte_off, st, B, timed, lengths);
   }
-  B->nmode = rfast ? c->h_scalars[12] : nw;
+  uint64_t vused = 0;
+  if (vsub) memcpy(&vused, c->h_scalars + 10, 8);
+  if (vsub && vused > vcap) {
+    // more sub-word records than room: grow to fit them all and run again (words past
+    // the room were left undecided)
+    if (vused > 0xfffffff0ull)
+      return fail(c, A5X_E_ARG, "batch of %llu words is too large for one -s call (sub-word records)",
+                  (unsigned long long)nw);
+    c->vrec_need = vused;
+    return run_keyspace_mode(c, d_words, d_woff, nw, mode, mn, mx, d_cand_off, d_byte_off, st, B, timed, lengths);
+  }
+  B->nmode = vsub ? c->h_scalars[15] : rfast ? c->h_scalars[12] : nw;
+  if (vsub && getenv("A5X_VSUB_DEBUG")) {  // (diagnostics: what the split leaves to the mode engine)
+    fprintf(stderr, "[vsub] words %llu probe-left %u split-left %u vrec %llu\n", (unsigned long long)nw,
+            c->h_scalars[12], c->h_scalars[15], (unsigned long long)vused);
+    const uint32_t k = std::min<uint32_t>(c->h_scalars[15], 24);
+    std::vector<uint32_t> li(k);
+    std::vector<uint64_t> wo(nw + 1);
+    if (k && hipMemcpy(li.data(), c->m_vl.p, 4 * k, hipMemcpyDeviceToHost) == hipSuccess &&
+        hipMemcpy(wo.data(), d_woff, 8 * (nw + 1), hipMemcpyDeviceToHost) == hipSuccess)
+      for (uint32_t x : li) {
+        std::string s((size_t)(wo[x + 1] - wo[x]), '\0');
+        (void)hipMemcpy(&s[0], d_words + wo[x], s.size(), hipMemcpyDeviceToHost);
+        fprintf(stderr, "[vsub]   left: %s\n", s.c_str());
+      }
+  }
   if (c->h_scalars[2] == 0 && c->h_scalars[7] > 0) {
     // mode pass G: words longer than the LDS engines take are counted in HBM scratch
     // slots (their counts were 0 in the first scan), then the scan runs again
@@ -842,7 +946,7 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     HIPCHK(c, hipStreamSynchronize(st));
     if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
     B->total_bytes = 0;
-    return A5X_OK;
+    return vused ? build_virtual(c, nw, d_cand_off, nullptr, st, B) : A5X_OK;
   }
   if (items) HIPCHK(c, a5x_launch_mode_items(M, 0, st));
   if (items)
@@ -856,7 +960,7 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   HIPCHK(c, hipStreamSynchronize(st));
   if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
   B->total_bytes = c->h_totals[1];
-  return A5X_OK;
+  return vused ? build_virtual(c, nw, d_cand_off, d_byte_off, st, B) : A5X_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -908,7 +1012,7 @@ int job_locate(a5x_ctx* c, const Job& J, const std::vector<uint64_t>& q, std::ve
   if ((rc = grow(c, c->loc_q, n)) || (rc = grow(c, c->loc_r, 3 * (size_t)n))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->loc_q.p, q.data(), 8 * (size_t)n, hipMemcpyHostToDevice, J.st));
   if (J.mode != A5X_MODE_DEFAULT) {
-    A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, J.B.rfast);
+    A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, J.B.rfast, J.B.virt);
     M.cand_off = J.B.cand_off;
     HIPCHK(c, a5x_launch_mode_locate(M, c->loc_q.p, n, c->loc_r.p, J.st));
     std::vector<uint64_t> t(3 * (size_t)n);
@@ -1023,7 +1127,7 @@ int job_launch(a5x_ctx* c, const Job& J, const Range& R, uint8_t* d_out, uint64_
     HIPCHK(c, hipEventRecord(c->ev_fork, J.st));
     HIPCHK(c, hipStreamWaitEvent(c->sstream, c->ev_fork, 0));
     if (J.B.nmode) HIPCHK(c, a5x_launch_mode_items(M, 1, c->sstream));  // (every word FAST: none)
-    A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
+    A5xExpLaunch E = exp_launch_mode(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
     E.cand_begin = R.cb;
     E.cand_end = R.ce;
     E.out = d_out;
@@ -1172,7 +1276,7 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
       HIPCHK(c, hipEventRecord(c->ev[1], J.st));
       if (J.B.nmode) HIPCHK(c, a5x_launch_mode_items(M, 2, J.st));
       if (J.B.rfast && tc) {  // -r FAST words: hashed in k_expand_fast_md5 / _ntlm's ring
-        A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
+        A5xExpLaunch E = exp_launch_mode(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
         E.cand_begin = 0;
         E.cand_end = tc;
         E.dg_bitmap = D.bitmap; E.dg_bm_mask = D.bm_mask; E.dg_has_zero = D.has_zero_target;
@@ -1471,6 +1575,9 @@ void a5x_destroy(a5x_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   release(c->glob);
+  release(c->m_vl); release(c->vn); release(c->vrsz); release(c->vpre); release(c->vrpre); release(c->vrec);
+  release(c->vrec2); release(c->vcand_off); release(c->vbyte_off); release(c->vflags); release(c->vroff);
+  release(c->vmap); release(c->vobase); release(c->vocc);
   if (c->mgscr) (void)hipFree(c->mgscr);
   if (c->gscr) (void)hipFree(c->gscr);
   if (c->sstream) (void)hipStreamSynchronize(c->sstream);

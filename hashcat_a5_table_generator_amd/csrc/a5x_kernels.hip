@@ -109,6 +109,9 @@ __device__ __forceinline__ u32 wave_incl_scan_u32(u32 x) {
 }
 __device__ __forceinline__ u32 lane63(u32 x) { return (u32)__builtin_amdgcn_readlane((int)x, 63); }
 __device__ __forceinline__ u32 readlane_u32(u32 x, u32 l) { return (u32)__builtin_amdgcn_readlane((int)x, (int)l); }
+__device__ __forceinline__ u64 readlane_u64(u64 x, u32 l) {
+  return ((u64)readlane_u32((u32)(x >> 32), l) << 32) | (u64)readlane_u32((u32)x, l);
+}
 // Whole-wave reductions on DPP (row_shr 1/2/4/8, row_bcast 15/31, as the scan above):
 // no cross-lane address registers (ds_bpermute index VGPRs that the compiler would
 // keep live through the whole kernel).  The result is uniform (lane 63).
@@ -208,6 +211,16 @@ struct KsArgs {
   u32 rcmin;       // -r: max(min, 0) (0 or 1 for a FAST word)
   u64* rnseg;      // -r: mode-engine items per FAST word (ceil(count / rseg))
   u64 rseg;
+  // -s / -s -r virtual words (k_keyspace_vsub over the probe's leftover list defer_list)
+  u32* vout_list;  // the words left to the mode engine
+  u32* vout_n;
+  u64* vn;         // per word: sub-words - 1 (virtual words; 0 elsewhere)
+  u64* vrsz;       // per word: record u64 of its FAST entries (virtual words; k_vwords_sizes the rest)
+  u64* vrec;       // per virtual word: its sub-word records, then one meta u64 per sub-word
+  unsigned long long* vrec_n;  // bump counter of vrec (u64 units)
+  u64 vrec_cap;
+  uint16_t* vocc;  // per word 16 u16: the occurrence row of k_keyspace_thread's -s / -s -r words
+                   // with a repeated pattern (null: none logged)
 };
 
 // -r / -s / -s -r on the FAST path (the mode-engine probe of k_keyspace_thread, rmode =
@@ -276,8 +289,8 @@ struct DevRecSink {
   u32 np;
   __device__ u64* cbuf() const { return c; }
   __device__ u32 cstride() const { return 256u; }
-  __device__ u64 gld(u32 a) const { return g[a * 256u]; }
-  __device__ void gst(u32 a, u64 v) { g[a * 256u] = v; }
+  __device__ u64 gld(u32, u32 a) const { return g[a * 256u]; }
+  __device__ void gst(u32, u32 a, u64 v) { g[a * 256u] = v; }
   __device__ void ent(u32 i, u64 v) { if (!(KS_ABL & 4)) rec[1 + np + i] = v; }
   __device__ void desc(u32 i, u64 v) { if (!(KS_ABL & 4)) rec[1 + i] = v; }
 };
@@ -331,13 +344,14 @@ __device__ __forceinline__ void ks_build(const W& wd, u32 L, const Tab& T, const
 #ifndef KS_ULOG
 #define KS_ULOG 16
 #endif
+__device__ bool psk_norep;  // (psk_walk's rep when the caller does not track repeats: never written)
 #ifndef PSK_KB
 #define PSK_KB 2  // bucket keys read together per position (more: a loop)
 #endif
 template <bool COUNT, class PL>
 __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 Lmax, u32 bmax, const Tab& T,
                                          PL& pl, CountAcc& A, bool& cplx, int rmode, uint16_t* ulog = nullptr,
-                                         u32* nlog = nullptr) {
+                                         u32* nlog = nullptr, bool logrep = false, bool& rep = psk_norep) {
   u32 cur_end = 0;
   u64 seen = 0;
   for (u32 q = 0; q < Lmax; q++) {
@@ -372,7 +386,16 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
       } else if (nm == 1 && !cplx) {
         Unit U;
         lone_unit(T, q, kk, U);
-        if (rmode && !mode_unit(T, U, rmode, seen, true)) {
+        // -s / -s -r with rep: a positional pattern met again is a tied occurrence -- no
+        // unit (the word is not FAST); the walk goes on logging the occurrences for
+        // k_keyspace_vsub (seen holds key index mod 64: a collision is taken for a repeat)
+        const bool again = logrep && rmode >= 2 && ((seen >> (kk & 63u)) & 1u) &&
+                           (T.keys[kk].pad0 & (rmode == 2 ? 1u : 2u)) && T.keys[kk].nvals >= 1;
+        bool logit = again;
+        if (again) {
+          rep = true;
+          cur_end = U.e;
+        } else if (rmode && !mode_unit(T, U, rmode, seen, true)) {
           cplx = true;
         } else if (U.R > KS_GCAP) {
           cplx = true;
@@ -380,11 +403,12 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
           if (COUNT) count_unit(A, U);
           if (!(KS_ABL & 2)) pl.unit(U);
           cur_end = U.e;
-          if (COUNT && ulog) {
-            const bool fits = *nlog < KS_ULOG && kk < 1024u && q < 64u;
-            if (fits) ulog[*nlog * 256u] = (uint16_t)((q << 10) | kk);
-            *nlog = fits ? *nlog + 1u : (u32)KS_ULOG + 1u;
-          }
+          logit = true;
+        }
+        if (COUNT && ulog && logit) {
+          const bool fits = *nlog < KS_ULOG && kk < 1024u && q < 64u;
+          if (fits) ulog[*nlog * 256u] = (uint16_t)((q << 10) | kk);
+          *nlog = fits ? *nlog + 1u : (u32)KS_ULOG + 1u;
         }
       }
     }
@@ -450,7 +474,8 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
     u32 nlog = 0;
     const bool rm = a.rmode != 0;
-    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, a.rmode, ulog, &nlog);
+    bool rep = false;  // (-s / -s -r with vocc: a repeated pattern; the occurrences logged)
+    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, a.rmode, ulog, &nlog, a.vocc != nullptr, rep);
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
     u32 f = 0;
@@ -468,8 +493,8 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       // added when min = 0; -s / -s -r words only as one mode-engine item (the length pass
       // takes their bytes whole); every other word (flags 0) is left to the mode engine
       const u64 cnt = A.P - a.rcmin;
-      const bool rf = psk && !cplx && (f & A5X_WF_FAST) && !(f & A5X_WF_DEFER) && A.nunits > 0 && C.count > 0 &&
-                      (a.rmode == 1 || cnt <= a.rseg);
+      const bool rf = psk && !cplx && !rep && (f & A5X_WF_FAST) && !(f & A5X_WF_DEFER) && A.nunits > 0 &&
+                      C.count > 0 && (a.rmode == 1 || cnt <= a.rseg);
       f = rf ? f : 0u;
       C.bytes = rf ? C.bytes + (a.rcmin ? 0ull : (u64)(L + 1)) : 0ull;
       C.count = rf ? cnt : 0ull;
@@ -537,6 +562,21 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
       if (rov) a.cplx_list[ri] = (u32)w;
       const u32 mi = wave_append(valid && !kept && !rov, a.defer_n);  // the mode engine's words
       if (valid && !kept && !rov) a.defer_list[mi] = (u32)w;
+      if (a.vocc && valid && !kept) {
+        // the occurrence row of a word with a repeated pattern (k_keyspace_vsub): <= 15
+        // entries q << 10 | key, row[15] = their number; 0xFFFF: not logged (vsub walks)
+        const bool logged = rep && !cplx && psk && nlog <= 15u;
+        u32 r[8];
+#pragma unroll
+        for (u32 k = 0; k < 8; k++) {
+          const u32 e0 = 2 * k < nlog ? ulog[(2 * k) * 256u] : 0u, e1 = 2 * k + 1 < nlog ? ulog[(2 * k + 1) * 256u] : 0u;
+          r[k] = e0 | (e1 << 16);
+        }
+        r[7] = (r[7] & 0xFFFFu) | ((logged ? nlog : 0xFFFFu) << 16);
+        uint4* row = (uint4*)(a.vocc + w * 16);
+        row[0] = make_uint4(r[0], r[1], r[2], r[3]);
+        row[1] = make_uint4(r[4], r[5], r[6], r[7]);
+      }
       __syncthreads();
       continue;
     }
@@ -637,6 +677,537 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
     }
     const u32 mi = wave_append(valid && !rf, a.defer_n);  // the mode engine's words
     if (valid && !rf) a.defer_list[mi] = (u32)w;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// -s / -s -r virtual words (processWordSubstituteAll / ...Reverse, main.go:308-440)
+// ---------------------------------------------------------------------------
+// The probe (mode_unit) refuses a positional word whose patterns repeat: ReplaceAll gives
+// every occurrence of a pattern the same value, so those occurrences are one tied digit,
+// which the FAST plan (one digit per unit) cannot express.  Fixing the choices of the
+// tied patterns splits the word into S = prod R_tied sub-words: sub-word s writes tied
+// pattern t's choice d_t (digits of s, first tied pattern least significant; choice 0 =
+// the pattern kept, then its values, -s -r: subs[0] only) into the word and keeps the
+// once-occurring patterns as units, so it is a plain FAST word.  The word's candidates
+// are its sub-words' in order: sub-word 0 (every tied pattern kept) has P - min(min, 1)
+// candidates (min 0: FAST index P wraps to the all-keep word), every other sub-word P
+// (its all-keep combination of the units still substitutes a tied pattern).  The window
+// cuts nothing: min <= 1 (the probe's condition) and #patterns <= max.
+// vrec per virtual word: its sub-words' records back to back, then one meta u64 per
+// sub-word (count | record u64 << 24 | bytes << 32); roff[w] = their base.
+#define VS_SLOT 92   // sub-word bytes per lane (sub-words <= VS_SLOT - 8 bytes; 23 dwords: lane
+                     // slots on distinct LDS banks)
+#define VS_WSLOT 76  // word bytes per lane (words <= A5X_LMAX_A + over-read; 19 dwords)
+#define VS_OCC 16    // pattern occurrences per word
+#define VS_SMAX 16   // sub-words per word
+#define VS_TMAX 4    // tied patterns per word
+#ifndef VS_ABL
+#define VS_ABL 0     // k_keyspace_vsub timing ablations (variant builds only, wrong output): 1 no build
+                     // pass, 2 no count pass, 4 no tasks (walk + pattern analysis only)
+#endif
+#define VS_RST 65    // record u64 per sub-word (built in the wave's LDS stage, copied out by the wave; odd:
+                     // the lanes' records start on distinct LDS banks)
+#define VS_BLOCK 64  // k_keyspace_vsub workgroup (LDS per lane ~340 B: 7 one-wave workgroups per CU)
+
+struct VsWord {
+  u32 L, nocc, nt, S;
+  u64 tk;  // tied pattern t's key: bits [10 t, 10 t + 10)
+  u32 tr;  // its radix: bits [5 t, 5 t + 5)
+};
+
+// Appends bytes to a lane's LDS sub-word slot a dword at a time (pending bytes in acc).
+struct SubW {
+  u32* d;
+  u32 n, na;  // dwords stored, pending bytes
+  u64 acc;
+  __device__ __forceinline__ u32 len() const { return 4 * n + na; }
+  __device__ __forceinline__ void put(u32 v, u32 k) {  // k <= 4 bytes of v
+    acc |= (u64)keep_bytes(v, k) << (8 * na);
+    na += k;
+    if (na >= 4) {
+      d[n++] = (u32)acc;
+      acc >>= 32;
+      na -= 4;
+    }
+  }
+  __device__ __forceinline__ void run(const uint8_t* src, u32 i0, u32 i1) {  // src[i0, i1)
+    for (u32 i = i0; i < i1; i += 4) put(lds_ld4(src, i), min(4u, i1 - i));
+  }
+  __device__ __forceinline__ void sync() { d[n] = (u32)acc; }  // the partial dword readable
+};
+
+// Sub-word s of the word at orig (LDS) written to the lane's slot sub; every untied
+// occurrence goes to pl (and A) as a unit at its sub-word position.  occ: the word's
+// occurrences (q << 10 | key, strided by 256).  Returns the length, 0 when it does not
+// fit the slot.
+template <class PL>
+__device__ u32 vs_build(const Tab& T, const VsWord& V, const uint8_t* orig, uint8_t* sub, const uint16_t* occ, u32 s,
+                        int rmode, PL& pl, CountAcc& A) {
+  u32 ch[VS_TMAX];
+  u32 x = s;
+#pragma unroll
+  for (u32 t = 0; t < VS_TMAX; t++) {
+    const u32 R = (V.tr >> (5 * t)) & 31u;
+    const u32 key = (u32)(V.tk >> (10 * t)) & 1023u;
+    const bool on = t < V.nt;
+    const u32 d = on ? x % R : 0u;
+    x = on ? x / R : x;
+    ch[t] = on ? T.keys[key].choice_base + d : 0u;
+  }
+  SubW W;
+  W.d = (u32*)sub; W.n = 0; W.na = 0; W.acc = 0;
+  u32 prev = 0;
+  for (u32 j = 0; j < V.nocc; j++) {
+    const u32 e = occ[j * VS_BLOCK];
+    const u32 q = e >> 10, key = e & 1023u;
+    if (W.len() + (q - prev) + 16u > VS_SLOT - 8u) return 0;  // (values <= 15 bytes)
+    W.run(orig, prev, q);
+    u32 ci = ~0u;
+#pragma unroll
+    for (u32 t = 0; t < VS_TMAX; t++)
+      if (t < V.nt && ((u32)(V.tk >> (10 * t)) & 1023u) == key) ci = ch[t];
+    u32 kl;
+    if (ci == ~0u) {  // a once-occurring pattern: a unit of the sub-word
+      Unit U;
+      lone_unit(T, W.len(), key, U);
+      kl = U.e - U.s;
+      u64 seen = 0;
+      (void)mode_unit(T, U, rmode, seen, false);
+      count_unit(A, U);
+      W.sync();
+      pl.unit(U);
+      W.put(lds_ld4(orig, q), kl);  // (keys <= 4 bytes)
+    } else {
+      kl = T.keys[key].klen;
+      const u64 cv = T.cval[ci];
+      const u32 cl = (u32)(cv >> 56);
+      if (cl <= 7) {
+        W.put((u32)cv, min(4u, cl));
+        if (cl > 4) W.put((u32)(cv >> 32), cl - 4);
+      } else {
+        const A5xChoice c = T.ch[ci];
+        W.put(c.first4, 4);
+        for (u32 i = 4; i < c.len; i++) W.put(T.blob[c.blob_off + i], 1);
+      }
+    }
+    prev = q + kl;
+  }
+  if (W.len() + (V.L - prev) > VS_SLOT - 8u) return 0;
+  W.run(orig, prev, V.L);
+  W.sync();
+  return W.len();
+}
+
+// classify_finish's FAST conditions for a sub-word; its count (cmin: the all-keep word
+// cut, sub-word 0 with min >= 1), bytes and record size (0 without candidates)
+__device__ __forceinline__ bool vs_fast(const CountAcc& A, const Plan& PL, u32 Ls, u32 cmin, u32& rs, u64& cnt,
+                                        u64& byt) {
+  if (!A.ok || A.ovf || !PL.ok) return false;
+  if (!(PL.np <= FW_PMAX && PL.ne <= 255 && 1 + PL.np + PL.ne <= FW_RMAX && PL.maxl <= FW_MAXL && PL.minl >= 3 &&
+        A.P <= FW_PMAX_CNT && PL.nbig <= FB_NMAX && PL.bent <= FB_EMAX))
+    return false;
+  cnt = A.P - cmin;
+  byt = A.P * (u64)(Ls + 1) + A.Dp - A.Dn - (cmin ? (u64)(Ls + 1) : 0ull);
+  rs = cnt ? 1u + PL.np + PL.ne : 0u;
+  return true;
+}
+
+// The word (lane l of the wave) that owns task t of the wave: the largest l with
+// tbase[l] <= t (tbase: exclusive scan of the sub-word counts, 64 entries)
+__device__ __forceinline__ u32 vs_owner(const uint16_t* tbase, u32 t) {
+  u32 l = 0;
+#pragma unroll
+  for (u32 st = 32; st; st >>= 1)
+    if (tbase[l + st] <= t) l += st;
+  return l;
+}
+
+// Lane per word of the probe's list (defer_list): the word's occurrences and tied
+// patterns; then its sub-words as tasks spread over the wave's lanes (a word's S
+// sub-words do not serialise its lane): count pass (per-word sums by LDS atomics), one
+// bump allocation per wave, build pass writing the records and metas.  The words it
+// cannot split go to vout_list (the mode engine).  A vrec too small leaves the words past
+// it undecided (the host reruns the keyspace with room for all).
+struct VsWave {  // per-wave LDS state
+  uint16_t tbase[65];                 // first task of each lane's word (+ total)
+  uint16_t tcbase[65];                // the same for the count pass (uniform words: sub-word 0 only)
+  u32 u0[64];                         // uniform word: sub-word 0's pieces | record u64 << 8 | length << 16
+  u32 uP[64];                         // ... and its combinations P
+  uint16_t tinfo[64 * VS_SMAX];       // per task: pieces | record u64 << 4 (0: none)
+  u32 ctot[64], btot[64], rtot[64], bad[64];
+  uint4 info[64];                     // word: L | nocc << 8 | nt << 16 | S << 24, tr, tk
+  unsigned long long base[64];
+  u64 stage[64 * VS_RST];             // build pass: the round's records (<= VS_RST u64), copied out
+};
+
+// Record sink of the build pass: the record in the lane's part of the wave's LDS stage,
+// the open group built in place where close_group leaves it (entries 1 + np + ne ...: its
+// copy-out is then a no-op).
+struct VsRecSink {
+  u64* rec;
+  u32 np;
+  __device__ u64* cbuf() const { return nullptr; }  // (no clusters: lone units only)
+  __device__ u32 cstride() const { return 1; }
+  __device__ u64 gld(u32 ne, u32 a) const { return rec[1 + np + ne + a]; }
+  __device__ void gst(u32 ne, u32 a, u64 v) { rec[1 + np + ne + a] = v; }
+  __device__ void ent(u32 i, u64 v) { rec[1 + np + i] = v; }
+  __device__ void desc(u32 i, u64 v) { rec[1 + i] = v; }
+};
+
+__global__ void __launch_bounds__(VS_BLOCK) k_keyspace_vsub(KsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const u32 tb = (a.table_bytes + 15u) & ~15u;
+  uint8_t* wsl = smem + tb;                                      // VS_BLOCK x VS_WSLOT word bytes
+  uint8_t* ssl = wsl + VS_BLOCK * VS_WSLOT;                      // VS_BLOCK x VS_SLOT sub-word bytes
+  uint16_t* occ0 = (uint16_t*)(ssl + VS_BLOCK * VS_SLOT);        // VS_OCC x VS_BLOCK occurrences
+  VsWave* wvs = (VsWave*)(occ0 + VS_BLOCK * VS_OCC);             // one per wave
+  load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  const u32 tid = threadIdx.x, lane = lane_id(), wv = tid / 64;
+  VsWave& Q = wvs[wv];
+  const u32 n = *a.defer_n;
+  const u32 pbit = a.rmode == 2 ? 1u : 2u;
+  uint8_t* orig = wsl + tid * VS_WSLOT;
+  uint16_t* occ = occ0 + tid;
+  uint8_t* sub = ssl + tid * VS_SLOT;
+  LWord lw;
+  lw.base = ssl; lw.off = tid * VS_SLOT;
+  for (u32 b0 = blockIdx.x * VS_BLOCK; b0 < n; b0 += gridDim.x * VS_BLOCK) {
+    // ---- word lane: occurrences, tied patterns ----
+    const u32 i = b0 + tid;
+    const bool valid = i < n;
+    const u64 w = valid ? a.defer_list[i] : 0ull;
+    const u64 s0 = valid ? a.woff[w] : 0ull;
+    const u64 L64 = valid ? a.woff[w + 1] - s0 : 0ull;
+    bool ok = valid && L64 >= 1 && L64 <= A5X_LMAX_A;
+    VsWord V;
+    V.L = ok ? (u32)L64 : 0u; V.nocc = 0; V.nt = 0; V.S = 1; V.tk = 0; V.tr = 0;
+    {
+      // aligned dwords of the word (the batch's words buffer has 16 readable bytes past
+      // the last word), shifted into place; zero past the word
+      u32* sl = (u32*)orig;
+      const u32* src = (const u32*)(a.words + (s0 & ~3ull));
+      const u32 sh = (u32)(s0 & 3u), nd = (V.L + 3u) / 4u;
+      u32 lo = V.L ? src[0] : 0u;
+      for (u32 q = 0; q < VS_WSLOT / 4; q++) {
+        const u32 hi = q < nd ? src[q + 1] : 0u;
+        const u32 v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        sl[q] = 4 * q + 4 <= V.L ? v : (4 * q < V.L ? keep_bytes(v, V.L - 4 * q) : 0u);
+        lo = hi;
+      }
+    }
+    // occurrences: the probe's row (k_keyspace_thread logged the word's lone matches),
+    // else the walk -- lone matches of positional patterns (as psk_walk: two keys at one
+    // position, a match inside another, a key longer than 4 bytes -> not split)
+    u32 rcnt = 0xFFFFu;
+    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+    if (ok && a.vocc) {
+      const uint4* row = (const uint4*)(a.vocc + w * 16);
+      r0 = row[0];
+      r1 = row[1];
+      rcnt = r1.w >> 16;
+    }
+    if (ok && rcnt != 0xFFFFu) {
+      const u32 rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+      for (u32 j = 0; j < 15; j++)
+        if (j < rcnt) occ[j * VS_BLOCK] = (uint16_t)(rw[j / 2] >> (16 * (j & 1)));
+      V.nocc = rcnt;
+    }
+    u32 cur_end = 0;
+    bool walk = ok && rcnt == 0xFFFFu;
+    for (u32 q = 0; walk && q < V.L; q++) {
+      const u32 w4 = lds_ld4(orig, q);
+      const u32 bk = T.bucket2[w4 & 255u];
+      const u32 ks = bk & 0xFFFFu, ke = bk >> 16;
+      u32 nm = 0, kk = 0;
+      for (u32 k2 = ks; k2 < ke; k2++) {
+        const u64 km = T.kmatch[k2];
+        const u32 kl = (u32)(km >> 32) & 0xFFFFu;
+        if (q + kl > V.L) continue;
+        if (kl > 4) { ok = false; break; }
+        const u32 m = kl >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kl)) - 1u);
+        if ((w4 & m) == (u32)km) { nm++; kk = k2; }
+      }
+      if (!ok) break;
+      if (nm > 1 || (nm == 1 && q < cur_end)) { ok = false; break; }
+      if (nm == 1) {
+        const A5xKey key = T.keys[kk];
+        if (!(key.pad0 & pbit) || key.nvals < 1 || V.nocc >= VS_OCC || kk >= 1024u || q >= 64u) { ok = false; break; }
+        occ[V.nocc * VS_BLOCK] = (uint16_t)((q << 10) | kk);
+        V.nocc++;
+        cur_end = q + key.klen;
+      }
+    }
+    // patterns (distinct keys); the tied ones (>= 2 occurrences) in first-occurrence order
+    u32 npat = 0;
+    for (u32 j = 0; ok && j < V.nocc; j++) {
+      const u32 kj = occ[j * VS_BLOCK] & 1023u;
+      bool first = true;
+      u32 mult = 0;
+      for (u32 j2 = 0; j2 < V.nocc; j2++) {
+        const u32 k2 = occ[j2 * VS_BLOCK] & 1023u;
+        if (k2 == kj) { mult++; first = first && j2 >= j; }
+      }
+      if (!first) continue;
+      npat++;
+      if (mult >= 2) {
+        const u32 R = a.rmode == 2 ? (u32)T.keys[kj].nvals + 1u : 2u;
+        if (V.nt >= VS_TMAX || V.S * R > VS_SMAX) { ok = false; break; }
+        V.tk |= (u64)kj << (10 * V.nt);
+        V.tr |= R << (5 * V.nt);
+        V.nt++;
+        V.S *= R;
+      }
+    }
+    ok = ok && npat >= 1 && (i64)npat <= (i64)a.mx && !(VS_ABL & 4);
+    // uniform: every choice of every tied pattern as long as the pattern, so all sub-words
+    // share one layout -- the count pass plans sub-word 0 only
+    bool uni = true;
+#pragma unroll
+    for (u32 t = 0; t < VS_TMAX; t++) {
+      if (t < V.nt) {
+        const A5xKey key = T.keys[(u32)(V.tk >> (10 * t)) & 1023u];
+        uni = uni && (a.rmode == 2 ? key.minclen == key.maxclen : T.ch[key.choice_base + 1].len == key.klen);
+      }
+    }
+    // ---- the wave's task lists: word lane l owns tasks [tbase[l], tbase[l] + S) ----
+    const u32 Sl = ok ? V.S : 0u, Sc = ok ? (uni ? 1u : V.S) : 0u;
+    const u32 tinc = wave_incl_scan_u32(Sl), tcinc = wave_incl_scan_u32(Sc);
+    const u32 ntask = readlane_u32(tinc, 63), nctask = readlane_u32(tcinc, 63);
+    Q.tbase[lane] = (uint16_t)(tinc - Sl);
+    Q.tcbase[lane] = (uint16_t)(tcinc - Sc);
+    if (lane == 63) { Q.tbase[64] = (uint16_t)ntask; Q.tcbase[64] = (uint16_t)nctask; }
+    Q.ctot[lane] = 0; Q.btot[lane] = 0; Q.rtot[lane] = 0; Q.bad[lane] = 0;
+    Q.info[lane] = make_uint4(V.L | (V.nocc << 8) | (V.nt << 16) | (V.S << 24), V.tr, (u32)V.tk, (u32)(V.tk >> 32));
+    WAVE_SYNC();
+    auto task_word = [&](const uint16_t* base, u32 t, VsWord& W, u32& l, u32& s) {
+      l = vs_owner(base, t);
+      s = t - base[l];
+      const uint4 in = Q.info[l];
+      W.L = in.x & 255u; W.nocc = (in.x >> 8) & 255u; W.nt = (in.x >> 16) & 255u; W.S = in.x >> 24;
+      W.tr = in.y; W.tk = (u64)in.z | ((u64)in.w << 32);
+    };
+    const u32 cmin = a.rcmin;
+    // ---- count pass: every sub-word FAST; sizes summed per word ----
+    for (u32 t0 = 0; t0 < nctask; t0 += 64) {
+      const u32 t = t0 + lane;
+      if (t < nctask && (VS_ABL & 2)) {
+        u32 l, s;
+        VsWord W;
+        task_word(Q.tcbase, t, W, l, s);
+        Q.tinfo[Q.tbase[l] + s] = 0;
+        atomicAdd(&Q.ctot[l], 1u);
+      } else if (t < nctask) {
+        VsWord W;
+        u32 l, s;
+        task_word(Q.tcbase, t, W, l, s);
+        const u32 wl = wv * 64 + l;
+        CountAcc A;
+        count_init(A, 0);
+        NullSink ns;
+        Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
+        const u32 Ls = vs_build(T, W, wsl + wl * VS_WSLOT, sub, occ0 + wl, s, a.rmode, pl, A);
+        u32 rs = 0;
+        u64 cnt = 0, byt = 0;
+        bool f = Ls != 0;
+        if (f) {
+          pl.finish(Ls);
+          f = vs_fast(A, pl.P, Ls, s == 0 ? cmin : 0u, rs, cnt, byt);
+        }
+        f = f && rs <= VS_RST;
+        Q.tinfo[Q.tbase[l] + s] = (uint16_t)(f && rs ? pl.P.np | (rs << 4) : 0u);
+        if (s == 0) {
+          const u32 rfull = 1u + pl.P.np + pl.P.ne;  // (the record of a sub-word with candidates)
+          Q.u0[l] = pl.P.np | (min(rfull, 255u) << 8) | (Ls << 16);
+          Q.uP[l] = (u32)min(A.P, (u64)0xFFFFFFFFu);
+          f = f && (W.S == 1 || rfull <= VS_RST);
+        }
+        if (!f) atomicOr(&Q.bad[l], 1u);
+        else {
+          atomicAdd(&Q.ctot[l], (u32)min(cnt, (u64)0xFFFFFFFFu));
+          atomicAdd(&Q.btot[l], (u32)min(byt, (u64)0xFFFFFFFFu));
+          atomicAdd(&Q.rtot[l], rs);
+        }
+      }
+    }
+    WAVE_SYNC();
+    // ---- word lane: the decision, one bump allocation per wave ----
+    u32 ctot = Q.ctot[lane], btot = Q.btot[lane], rtot = Q.rtot[lane];
+    if (ok && uni && V.S > 1 && !Q.bad[lane]) {
+      // sub-words 1 .. S-1 of a uniform word: sub-word 0's layout with every combination
+      const u32 u0 = Q.u0[lane], P = Q.uP[lane], np = u0 & 255u, rfull = (u0 >> 8) & 255u, Ls = u0 >> 16;
+      const u32 b0 = btot + (cmin ? Ls + 1u : 0u);  // sub-word 0's bytes + its cut all-keep word
+      ctot += (V.S - 1u) * P;
+      btot += (V.S - 1u) * b0;
+      rtot += (V.S - 1u) * rfull;
+      for (u32 s = 1; s < V.S; s++) Q.tinfo[Q.tbase[lane] + s] = (uint16_t)(np | (rfull << 4));
+    }
+    ok = ok && !Q.bad[lane] && ctot >= 1 && ctot <= a.rseg;  // (one mode-engine item, as the probe's -s words)
+    const u32 mtot = ok ? rtot + V.S : 0u;
+    const u32 minc = wave_incl_scan_u32(mtot);
+    unsigned long long wbase = 0;
+    if (lane == 63 && minc) wbase = atomicAdd(a.vrec_n, (unsigned long long)minc);
+    const unsigned long long base = readlane_u64((u64)wbase, 63) + (minc - mtot);
+    const bool room = ok && base + mtot <= a.vrec_cap;
+    Q.base[lane] = room ? base : ~0ull;
+    Q.rtot[lane] = rtot;
+    WAVE_SYNC();
+    // ---- build pass: records and metas at the word's base; records of <= VS_RST u64 built
+    // in the wave's LDS stage and copied out by the whole wave (coalesced) ----
+    for (u32 t0 = 0; t0 < ntask; t0 += 64) {
+      const u32 t = t0 + lane;
+      u32 rso = 0;       // record u64 staged by this lane
+      u64 dst = 0;       // its place in vrec
+      if (t < ntask) {
+        VsWord W;
+        u32 l, s;
+        task_word(Q.tbase, t, W, l, s);
+        const unsigned long long wb = Q.base[l];
+        if (wb != ~0ull && !(VS_ABL & 1)) {
+          const u32 wl = wv * 64 + l;
+          u32 ro = 0;
+          for (u32 t2 = Q.tbase[l]; t2 < t; t2++) ro += Q.tinfo[t2] >> 4;
+          const u32 ti = Q.tinfo[t], np = ti & 15u, rs0 = ti >> 4;
+          u64* rb = a.vrec + wb;
+          u32 rs = 0;
+          u64 cnt = 0, byt = 0;
+          if (np) {
+            VsRecSink sk;
+            sk.rec = &Q.stage[lane * VS_RST]; sk.np = np;
+            Planner<true, LWord, VsRecSink, KS_GCAP> pb(lw, T, sk, 0u);
+            CountAcc A;
+            count_init(A, 0);
+            const u32 Ls = vs_build(T, W, wsl + wl * VS_WSLOT, sub, occ0 + wl, s, a.rmode, pb, A);
+            pb.finish(Ls);
+            const Plan& P = pb.P;
+            if (!Ls || !vs_fast(A, P, Ls, s == 0 ? cmin : 0u, rs, cnt, byt) || P.np != np || rs != rs0)
+              atomicOr(a.err, A5X_DERR_STATE);
+            sk.rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
+            rso = rs0;
+            dst = (u64)wb + ro;
+          }
+          rb[Q.rtot[l] + s] = cnt | ((u64)rs << 24) | (byt << 32);
+        }
+      }
+      WAVE_SYNC();
+      for (u32 l = 0; l < 64; l++) {
+        const u32 n2 = readlane_u32(rso, l);
+        if (!n2) continue;
+        const u64 d2 = readlane_u64(dst, l);
+        if (lane < n2) a.vrec[d2 + lane] = Q.stage[l * VS_RST + lane];
+      }
+      WAVE_SYNC();
+    }
+    // ---- word lane: results ----
+    if (room) {
+      a.count[w] = ctot;
+      a.bytes[w] = btot;
+      a.flags[w] = A5X_WF_FAST | A5X_WF_VIRT;
+      a.rnseg[w] = 1;
+      a.roff[w] = (u32)base;
+      a.vn[w] = V.S - 1u;
+      a.vrsz[w] = rtot;
+    }
+    const bool left = valid && !ok;  // (ok without room: undecided, the host reruns)
+    const u32 mi = wave_append(left, a.vout_n);
+    if (left) a.vout_list[mi] = (u32)w;
+    WAVE_SYNC();  // (Q is rewritten by the next words)
+  }
+}
+
+// k_expand_fast over a batch with virtual words runs on the virtual word list: every word
+// one entry (mode-engine words as holes, flags 0), a virtual word one entry per sub-word;
+// records copied into one area in list order (each window one contiguous copy).
+struct VwArgs {
+  const u32* flags;
+  const u64* cand_off;
+  const u64* byte_off;  // (null: the fused digest, no layout)
+  const u32* roff;
+  const u64* rec;
+  const u64* vrec;
+  const u64* vpre;   // exclusive scan of vn: entry of word w = w + vpre[w]
+  const u64* vrpre;  // exclusive scan of vrsz: record u64 of word w in vrec2
+  u64 nw;
+  u64* vcand_off;
+  u64* vbyte_off;
+  u32* vflags;
+  u32* vroff;
+  u32* vmap;    // entry -> word
+  u32* vobase;  // entry -> its first candidate's index in the word
+  u64* vrec2;
+};
+
+// record u64 of the words that are not virtual (virtual words: k_keyspace_vsub)
+__global__ void __launch_bounds__(256) k_vwords_sizes(const u32* flags, const u64* cand_off, u64 nw, u64* vn,
+                                                      u64* vrsz) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+    const u32 f = flags[w];
+    if (f & A5X_WF_VIRT) continue;
+    vn[w] = 0;
+    vrsz[w] = (f & A5X_WF_FAST) && cand_off[w + 1] > cand_off[w] ? ff_rsize(f) : 0ull;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_vwords_fill(VwArgs a) {
+  const u32 lane = lane_id();
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 wb = (u64)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); wb < a.nw; wb += stride) {
+    const u64 w = wb + lane;
+    const bool valid = w < a.nw;
+    const u32 f = valid ? a.flags[w] : 0u;
+    const u64 v0 = valid ? w + a.vpre[w] : 0ull, r0 = valid ? a.vrpre[w] : 0ull;
+    const u64 c0 = valid ? a.cand_off[w] : 0ull, b0 = valid && a.byte_off ? a.byte_off[w] : 0ull;
+    const u32 nrec = valid ? (u32)(a.vrpre[w + 1] - r0) : 0u;
+    u64 src = 0;  // (address of the word's records)
+    if (valid && !(f & A5X_WF_VIRT)) {
+      a.vcand_off[v0] = c0; a.vbyte_off[v0] = b0; a.vflags[v0] = nrec ? f : 0u; a.vroff[v0] = (u32)r0;
+      a.vmap[v0] = (u32)w; a.vobase[v0] = 0;
+      if (nrec) src = (u64)(a.rec + a.roff[w]);
+    } else if (valid) {
+      const u64* vr = a.vrec + a.roff[w];
+      src = (u64)vr;
+      const u32 S = (u32)(a.vpre[w + 1] - a.vpre[w]) + 1u;
+      u64 co = 0, bo = 0;
+      u32 ro = 0;
+      for (u32 s = 0; s < S; s++) {
+        const u64 m = vr[nrec + s];
+        const u32 cnt = (u32)m & 0xFFFFFFu, rs = (u32)(m >> 24) & 255u;
+        u32 vf = 0;
+        if (rs) {
+          const u64 h = vr[ro];
+          vf = A5X_WF_FAST | A5X_WF_RADIX | (frh_ng(h) << 10) | (frh_ne(h) << 16) | (frh_np(h) << 24);
+        }
+        const u64 v = v0 + s;
+        a.vcand_off[v] = c0 + co; a.vbyte_off[v] = b0 + bo; a.vflags[v] = vf; a.vroff[v] = (u32)(r0 + ro);
+        a.vmap[v] = (u32)w; a.vobase[v] = (u32)co;
+        co += cnt; bo += m >> 32; ro += rs;
+      }
+    }
+    if (valid && w + 1 == a.nw) {
+      const u64 ve = a.nw + a.vpre[a.nw];
+      a.vcand_off[ve] = a.cand_off[a.nw];
+      a.vbyte_off[ve] = a.byte_off ? a.byte_off[a.nw] : 0ull;
+    }
+    // the records: the wave copies its lanes' ranges in lane order (contiguous ones merged)
+    u64 cs = 0, cd = 0;
+    u32 cn = 0;
+    auto copy = [&]() {
+      const u64* sp = (const u64*)cs;
+      for (u32 k = lane; k < cn; k += 64) a.vrec2[cd + k] = sp[k];
+    };
+    for (u32 l = 0; l < 64; l++) {
+      const u32 ln = readlane_u32(nrec, l);
+      if (!ln) continue;
+      const u64 ls = readlane_u64(src, l), ld = readlane_u64(r0, l);
+      if (cn && ls == cs + 8ull * cn && ld == cd + cn) { cn += ln; continue; }
+      copy();
+      cs = ls; cd = ld; cn = ln;
+    }
+    copy();
   }
 }
 
@@ -1171,7 +1742,15 @@ struct ExpArgs {
   u32* dg_nhits;
   uint8_t* gscr;         // pass G scratch slots (k_expand_g, k_locate)
   u32 gslots;
+  const u32* vmap;       // virtual word list (k_vwords_fill; null: words): entry -> word,
+  const u32* vobase;     // and its first candidate's index in the word (hit records)
 };
+
+// a fused-digest hit of candidate c of list entry e as (word, candidate in word)
+__device__ __forceinline__ void hit_word(const ExpArgs& a, u64 e, u64 c, A5xHitRaw& r) {
+  r.blk = a.vmap ? (u64)a.vmap[e] : e;
+  r.idx = a.vmap ? c + a.vobase[e] : c;
+}
 
 // Record the first tripped guard (code + context) and flag the call as failed.
 // Takes the two pointers (not the argument struct) so the kernel arguments are
@@ -1769,8 +2348,7 @@ struct FxDigest {
         const u32 h = atomicAdd(a->dg_nhits, 1u);
         if (h < a->dg_hit_cap) {
           A5xHitRaw r;
-          r.blk = wbase + lr.j;
-          r.idx = lr.st + c;
+          hit_word(*a, wbase + lr.j, lr.st + c, r);
           r.d[0] = d[0]; r.d[1] = d[1]; r.d[2] = d[2]; r.d[3] = d[3];
           a->dg_hits[h] = r;
         }
@@ -1901,8 +2479,7 @@ __device__ __forceinline__ void fxd_round(const uint4* be, const uint4 (*wq)[2],
     const u32 k = atomicAdd(a.dg_nhits, 1u);
     if (k < a.dg_hit_cap) {
       A5xHitRaw r;
-      r.blk = wbase + j;
-      r.idx = st;
+      hit_word(a, wbase + j, st, r);
       r.d[0] = h[0]; r.d[1] = h[1]; r.d[2] = h[2]; r.d[3] = h[3];
       a.dg_hits[k] = r;
     }
@@ -2484,7 +3061,7 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   a.rec = L.rec; a.roff = L.roff;
   a.cplx_list = L.cplx_list; a.cplx_n = L.cplx_n; a.cplx_cap = L.cplx_cap; a.cplx_base = L.cplx_base;
   a.glob_list = L.glob_list; a.glob_n = L.glob_n; a.gscr = L.gscr;
-  a.rmode = L.rmode; a.rcmin = L.rcmin; a.rnseg = L.rnseg; a.rseg = L.rseg;
+  a.rmode = L.rmode; a.rcmin = L.rcmin; a.rnseg = L.rnseg; a.rseg = L.rseg; a.vocc = L.vocc;
   hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -2521,6 +3098,41 @@ size_t a5x_keyspace_thread_lds(u32 table_bytes) {
 
 size_t a5x_keyspace_rprobe_lds(u32 table_bytes) {
   return ((table_bytes + 15u) & ~15u) + 256 * KS_GCAP * 8 + 256 * RP_SLOT;
+}
+
+size_t a5x_keyspace_vsub_lds(u32 table_bytes) {
+  return ((table_bytes + 15u) & ~15u) + VS_BLOCK * (VS_WSLOT + VS_SLOT + VS_OCC * 2) +
+         (VS_BLOCK / 64) * sizeof(VsWave);
+}
+
+hipError_t a5x_launch_vsub(const A5xKsLaunch& L, hipStream_t st) {
+  KsArgs a;
+  memset(&a, 0, sizeof a);
+  a.table = L.table; a.table_bytes = L.table_bytes; a.words = L.words; a.woff = L.woff; a.nw = L.nw;
+  a.mn = L.mn; a.mx = L.mx; a.count = L.count; a.bytes = L.bytes; a.flags = L.flags; a.err = L.err;
+  a.defer_list = L.defer_list; a.defer_n = L.defer_n; a.roff = L.roff;
+  a.rmode = L.rmode; a.rcmin = L.rcmin; a.rnseg = L.rnseg; a.rseg = L.rseg;
+  a.vout_list = L.vout_list; a.vout_n = L.vout_n; a.vn = L.vn; a.vrsz = L.vrsz;
+  a.vrec = L.vrec; a.vrec_n = (unsigned long long*)L.vrec_n; a.vrec_cap = L.vrec_cap; a.vocc = L.vocc;
+  hipLaunchKernelGGL(k_keyspace_vsub, dim3(L.defer_blocks * (256 / VS_BLOCK)), dim3(VS_BLOCK),
+                     a5x_keyspace_vsub_lds(L.table_bytes), st, a);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_vwords_sizes(const uint32_t* flags, const uint64_t* cand_off, uint64_t nw, uint64_t* vn,
+                                   uint64_t* vrsz, hipStream_t st) {
+  hipLaunchKernelGGL(k_vwords_sizes, dim3(blocks_for(nw, 256, 8192)), dim3(256), 0, st, flags, cand_off, nw, vn, vrsz);
+  return hipGetLastError();
+}
+
+hipError_t a5x_launch_vwords_fill(const A5xVwLaunch& L, hipStream_t st) {
+  VwArgs a;
+  a.flags = L.flags; a.cand_off = L.cand_off; a.byte_off = L.byte_off; a.roff = L.roff; a.rec = L.rec;
+  a.vrec = L.vrec; a.vpre = L.vpre; a.vrpre = L.vrpre; a.nw = L.nw;
+  a.vcand_off = L.vcand_off; a.vbyte_off = L.vbyte_off; a.vflags = L.vflags; a.vroff = L.vroff;
+  a.vmap = L.vmap; a.vobase = L.vobase; a.vrec2 = L.vrec2;
+  hipLaunchKernelGGL(k_vwords_fill, dim3(blocks_for(L.nw, 256, 8192)), dim3(256), 0, st, a);
+  return hipGetLastError();
 }
 
 size_t a5x_keyspace_wave_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + sizeof(LdsB); }
@@ -2575,6 +3187,7 @@ static ExpArgs exp_args(const A5xExpLaunch& L) {
   a.dg_bitmap = L.dg_bitmap; a.dg_bm_mask = L.dg_bm_mask; a.dg_has_zero = L.dg_has_zero; a.dg_hit_cap = L.dg_hit_cap;
   a.dg_table = L.dg_table; a.dg_tmask = L.dg_tmask; a.dg_hits = L.dg_hits; a.dg_nhits = L.dg_nhits;
   a.gscr = L.gscr; a.gslots = L.gslots;
+  a.vmap = L.vmap; a.vobase = L.vobase;
   return a;
 }
 
@@ -2670,6 +3283,8 @@ hipError_t a5x_set_kernel_attrs() {
   e = hipFuncSetAttribute((const void*)k_keyspace_cplx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_keyspace_rprobe, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_keyspace_vsub, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_locate, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;

@@ -38,7 +38,42 @@ struct A5xKsLaunch {
   uint32_t rcmin;       // -r: max(min, 0)
   uint64_t* rnseg;      // -r: per FAST word, ceil(count / rseg) mode-engine items
   uint64_t rseg;
+  // -s / -s -r virtual words (k_keyspace_vsub over defer_list): the words it leaves to the
+  // mode engine, per word sub-words - 1 and record u64, the sub-word records (bump area)
+  uint32_t* vout_list;
+  uint32_t* vout_n;
+  uint64_t* vn;
+  uint64_t* vrsz;
+  uint64_t* vrec;
+  uint64_t* vrec_n;
+  uint64_t vrec_cap;
+  uint16_t* vocc;  // per word 16 u16: k_keyspace_thread's occurrence rows for k_keyspace_vsub (null: none)
 };
+
+// the virtual word list of a batch with virtual words (k_vwords_fill)
+struct A5xVwLaunch {
+  const uint32_t* flags;
+  const uint64_t* cand_off;
+  const uint64_t* byte_off;  // null: no layout (fused digest)
+  const uint32_t* roff;
+  const uint64_t* rec;
+  const uint64_t* vrec;
+  const uint64_t* vpre;
+  const uint64_t* vrpre;
+  uint64_t nw;
+  uint64_t* vcand_off;
+  uint64_t* vbyte_off;
+  uint32_t* vflags;
+  uint32_t* vroff;
+  uint32_t* vmap;
+  uint32_t* vobase;
+  uint64_t* vrec2;
+};
+size_t a5x_keyspace_vsub_lds(uint32_t table_bytes);
+hipError_t a5x_launch_vsub(const A5xKsLaunch& L, hipStream_t st);
+hipError_t a5x_launch_vwords_sizes(const uint32_t* flags, const uint64_t* cand_off, uint64_t nw, uint64_t* vn,
+                                   uint64_t* vrsz, hipStream_t st);
+hipError_t a5x_launch_vwords_fill(const A5xVwLaunch& L, hipStream_t st);
 
 struct A5xHitRaw;
 struct A5xExpLaunch {
@@ -78,6 +113,10 @@ struct A5xExpLaunch {
   // pass G (words beyond the pass-B LDS budget): HBM scratch slots, one per wave
   uint8_t* gscr;
   uint32_t gslots;
+  // the virtual word list (-s / -s -r batches with virtual words): entry -> word and its
+  // first candidate in the word, for the fused digest's hit records (null: words)
+  const uint32_t* vmap;
+  const uint32_t* vobase;
 };
 
 hipError_t a5x_set_kernel_attrs();
@@ -149,6 +188,12 @@ struct A5xModeLaunch {
   const uint32_t* in_n;
   const uint64_t* rec;      // FAST plan records / offsets (k_mode_locate inside -s FAST words)
   const uint32_t* roff;
+  // virtual words (flags & A5X_WF_VIRT; k_mode_locate): the virtual word list
+  const uint64_t* vpre;
+  const uint64_t* vcand_off;
+  const uint64_t* vbyte_off;
+  const uint32_t* vroff;
+  const uint64_t* vrec;
   // fused digest (op 2): every candidate hashed where it is built and probed against the
   // target set; hits as (word, candidate in word) -- see A5xDigLaunch
   int dg_algo;

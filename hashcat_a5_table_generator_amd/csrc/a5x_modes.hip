@@ -1920,9 +1920,18 @@ __device__ void m_locate(SL& S, const MT& T, const A5xModeLaunch& a, const u64* 
       pre = (u64)r * (a.woff[w + 1] - a.woff[w] + 1);
     } else {
       const u64* rec = a.rec + a.roff[w];
-      const u32 np = (u32)rec[0] & 15u;
+      u32 rr = r;
       u64 sum = 0;
-      for (u32 cnd = m_lane(); cnd < r; cnd += 64) {
+      if (a.flags[w] & A5X_WF_VIRT) {
+        // a virtual word: the sub-word holding g, its bytes before g from its record
+        u64 v = w + a.vpre[w];
+        while (a.vcand_off[v + 1] <= g) v++;
+        rec = a.vrec + a.vroff[v];
+        rr = (u32)(g - a.vcand_off[v]);
+        if (m_lane() == 0) sum = a.vbyte_off[v] - a.vbyte_off[w + a.vpre[w]];
+      }
+      const u32 np = (u32)rec[0] & 15u;
+      for (u32 cnd = m_lane(); cnd < rr; cnd += 64) {
         u32 n = cnd + 1, len = 0;
         for (u32 p = 0; p < np; p++) {
           const u64 G = rec[1 + p];

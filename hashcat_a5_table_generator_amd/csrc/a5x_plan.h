@@ -350,14 +350,14 @@ struct Plan {
   bool ok;
 };
 
-// Record sinks.  gld/gst: the R <= FW_UMAXR entries of the open group (built in
-// place while units merge into it); ent(i, v): final entry i; desc(i, v): piece i.
+// Record sinks.  gld/gst(ne, a): entry a of the open group (R <= FW_UMAXR entries, built in
+// place while units merge into it; ne = the entries closed so far); ent(i, v): final entry i; desc(i, v): piece i.
 // cbuf / cstride: where a cluster unit's choices are enumerated once (BUILD only).
 struct NullSink {
   A5X_HD u64* cbuf() const { return nullptr; }
   A5X_HD u32 cstride() const { return 1; }
-  A5X_HD u64 gld(u32) const { return 0; }
-  A5X_HD void gst(u32, u64) {}
+  A5X_HD u64 gld(u32, u32) const { return 0; }
+  A5X_HD void gst(u32, u32, u64) {}
   A5X_HD void ent(u32, u64) {}
   A5X_HD void desc(u32, u64) {}
 };
@@ -367,8 +367,8 @@ struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
   u64 g[FW_UMAXR], c[FW_UMAXR];
   A5X_HD u64* cbuf() { return c; }
   A5X_HD u32 cstride() const { return 1; }
-  A5X_HD u64 gld(u32 a) const { return g[a]; }
-  A5X_HD void gst(u32 a, u64 v) { g[a] = v; }
+  A5X_HD u64 gld(u32, u32 a) const { return g[a]; }
+  A5X_HD void gst(u32, u32 a, u64 v) { g[a] = v; }
   A5X_HD void ent(u32 i, u64 v) { rec[1 + np + i] = v; }
   A5X_HD void desc(u32 i, u64 v) { rec[1 + i] = v; }
 };
@@ -436,7 +436,7 @@ struct Planner {
   A5X_HD void close_group() {
     if constexpr (BUILD) {
       for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : cR); a++)
-        if (a < cR) sk.ent(P.ne + a, sk.gld(a));
+        if (a < cR) sk.ent(P.ne + a, sk.gld(P.ne, a));
       sk.desc(cpi, fr_desc(cR, P.ne));
     }
     big_add(cR, cmax, cpi);
@@ -482,7 +482,7 @@ struct Planner {
         for (u32 t = 0; t < CAP; t++) {
           const u32 a2 = (t * inv) >> 8, a1 = t - a2 * cR;
           cl[t] = 0;
-          ov[t] = t < nR ? sk.gld(a1) : 0ull;
+          ov[t] = t < nR ? sk.gld(P.ne, a1) : 0ull;
           cv[t] = t < nR ? unit_choice_b(wd, U, T, a2, cl[t], cb, cs) : 0ull;
         }
 #pragma unroll
@@ -490,7 +490,7 @@ struct Planner {
           if (t < nR) {
             const u32 ol = fw_len(ov[t]);
             const u64 v = (ov[t] & FW_M56) | (rb << (8 * ol)) | (cv[t] << (8 * (ol + run)));
-            sk.gst(t, (v & FW_M56) | fw_meta(ol + run + cl[t], nR));
+            sk.gst(P.ne, t, (v & FW_M56) | fw_meta(ol + run + cl[t], nR));
           }
         }
       } else if constexpr (BUILD) {
@@ -501,10 +501,10 @@ struct Planner {
           const u32 a2 = ((u32)t * inv) >> 8, a1 = (u32)t - a2 * cR;
           u32 cl = 0;
           const u64 cv = unit_choice_b(wd, U, T, a2, cl, cb, cs);
-          const u64 old = sk.gld(a1);
+          const u64 old = sk.gld(P.ne, a1);
           const u32 ol = fw_len(old);
           const u64 v = (old & FW_M56) | (rb << (8 * ol)) | (cv << (8 * (ol + run)));
-          sk.gst((u32)t, (v & FW_M56) | fw_meta(ol + run + cl, nR));
+          sk.gst(P.ne, (u32)t, (v & FW_M56) | fw_meta(ol + run + cl, nR));
         }
       }
       cR = nR; cmax += run + ml; cmin += run + U.mnl;
@@ -529,7 +529,7 @@ struct Planner {
         }
 #pragma unroll
         for (u32 a = 0; a < CAP; a++)
-          if (a < Ru) sk.gst(a, ((rb | (cv[a] << (8 * rem))) & FW_M56) | fw_meta(rem + cl[a], Ru));
+          if (a < Ru) sk.gst(P.ne, a, ((rb | (cv[a] << (8 * rem))) & FW_M56) | fw_meta(rem + cl[a], Ru));
       } else if constexpr (BUILD) {
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
         for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : Ru); a++) {
@@ -537,7 +537,7 @@ struct Planner {
           u32 cl = 0;
           const u64 cv = unit_choice_b(wd, U, T, a, cl, cb, cs);
           const u64 v = rb | (cv << (8 * rem));
-          sk.gst(a, (v & FW_M56) | fw_meta(rem + cl, Ru));
+          sk.gst(P.ne, a, (v & FW_M56) | fw_meta(rem + cl, Ru));
         }
       }
     }
@@ -551,9 +551,9 @@ struct Planner {
         const u64 tb = (run ? wd.ld(prev, run) : 0ull) | (10ull << (8 * run));
         for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : cR); a++) {
           if (a >= cR) continue;
-          const u64 old = sk.gld(a);
+          const u64 old = sk.gld(P.ne, a);
           const u32 ol = fw_len(old);
-          sk.gst(a, ((old | (tb << (8 * ol))) & FW_M56) | fw_meta(ol + tl, cR));
+          sk.gst(P.ne, a, ((old | (tb << (8 * ol))) & FW_M56) | fw_meta(ol + tl, cR));
         }
       }
       cmax += tl; cmin += tl;

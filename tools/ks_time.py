@@ -1,6 +1,6 @@
 """Time the keyspace pass (device) for a table set over a synthetic word batch (GPU box).
 
-    python tools/ks_time.py [workload] [words] [table ...]
+    [KSMODE=m] python tools/ks_time.py [workload] [words] [table ...]
 """
 import os
 import sys
@@ -18,10 +18,11 @@ if len(sys.argv) > 3:
 ctx = Context(0)
 ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
 dw, do = DeviceBuffer.from_array(ctx, data), DeviceBuffer.from_array(ctx, offs)
-ctx.keyspace_device(dw.ptr, do.ptr, n)
+mode = int(os.environ.get("KSMODE", "0"))
+ctx.keyspace_device(dw.ptr, do.ptr, n, mode=mode)
 best = 1e9
 for _ in range(5):
     t0 = time.perf_counter()
-    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n)
+    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, mode=mode)
     best = min(best, time.perf_counter() - t0)
 print(f"{wl} {tables}: {n} words -> {tc} candidates; keyspace_device {best * 1e3:.2f} ms (host wall, incl. sync)")
