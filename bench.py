@@ -180,10 +180,10 @@ def kernel_src_sha() -> str:
 digest_src_sha = kernel_src_sha
 
 
-def digest_profile(algo: str, words: int, kernel: str):
+def digest_profile(algo: str, words: int, kernel: str, mode: int = 0, mn: int = 0):
     """VALU evidence of the digest kernel (tools/gpu.sh digestprof): the profile of THESE
-    sources when committed, else the newest one for the same kernel and size, flagged
-    (its int ops per candidate are those of the profiled sources)."""
+    sources when committed, else the newest one for the same kernel, size and mode,
+    flagged (its int ops per candidate are those of the profiled sources)."""
     sha = digest_src_sha()
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_digest_*.json")), key=os.path.getmtime, reverse=True):
@@ -192,7 +192,8 @@ def digest_profile(algo: str, words: int, kernel: str):
                 d = json.load(fh)
         except Exception:
             continue
-        if d.get("algo") == algo and d.get("words") == words and d.get("kernel") == kernel:
+        if (d.get("algo") == algo and d.get("words") == words and d.get("kernel") == kernel
+                and d.get("mode", 0) == mode and d.get("min", 0) == (mn if mode else d.get("min", 0))):
             d["_file"] = os.path.relpath(f, ROOT)
             d["_sha_match"] = d.get("kernel_src_sha") == sha
             if d["_sha_match"]:
@@ -201,9 +202,10 @@ def digest_profile(algo: str, words: int, kernel: str):
     return best
 
 
-def latest_profile_traffic(workload: str, words: int):
-    """HBM bytes per expansion launch from a committed rocprofv3 --pmc pass
-    (tools/gpu_pmc_traffic.sh) of THESE kernel sources on this workload and size, else None."""
+def latest_profile_traffic(workload: str, words: int, mode: int = 0):
+    """HBM bytes per expansion launch (-r / -s / -s -r: per expansion, k_expand_fast and the
+    mode-engine item kernels beside it summed) from a committed rocprofv3 --pmc pass
+    (tools/gpu.sh traffic) of THESE kernel sources on this workload, size and mode, else None."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     sha = kernel_src_sha()
     for f in reversed(files):
@@ -213,7 +215,7 @@ def latest_profile_traffic(workload: str, words: int):
         except Exception:
             continue
         if (d.get("workload") == workload and d.get("words") == words and d.get("kernel_src_sha") == sha
-                and d.get("bytes_per_launch")):
+                and d.get("mode", 0) == mode and d.get("bytes_per_launch")):
             return d
     return None
 
@@ -299,9 +301,12 @@ def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
     expand, hash and probe in one kernel, so the stage time is the expansion time.  The
     step's time is accounted as keyspace + stage (+ two-pass digest) + the rest (host)."""
     fused = ms_dig < 1e-3
-    kernel = (f"k_expand_fast_{args.digest}" if args.mode == 0 else "k_mode_digest_*") if fused else "k_digest_stream"
+    # (-r / -s / -s -r: the FAST-probe and virtual words hash in k_expand_fast_<algo>, the
+    # rest in the mode engine's k_mode_digest_* beside it -- ops summed over both)
+    kernel = ((f"k_expand_fast_{args.digest}" if args.mode == 0 else f"k_expand_fast_{args.digest}+k_mode_digest_*")
+              if fused else "k_digest_stream")
     ms_stage = ms_exp if fused else ms_dig
-    prof = digest_profile(args.digest, args.words, kernel)
+    prof = digest_profile(args.digest, args.words, kernel, args.mode, args.min)
     peak = 256 * 4 * 32 * 2.4e9 / 1e12  # Tops/s
     r = {"bound": "valu", "kernel": kernel + ("" if fused else f"<{args.digest}>"), "fused": fused,
          "unit": "Tops/s (int32 lane ops)", "peak": peak, "ms_digest_per_step": ms_stage if not fused else 0.0,
@@ -677,7 +682,7 @@ def main():
 
     if D.rank == 0:
         achieved = tb / (ms_exp * 1e-3) / 1e9  # GB/s, algorithmic bytes per launch / launch time
-        prof = latest_profile_traffic(args.workload, n) if args.mode == 0 and D.world == 1 else None
+        prof = latest_profile_traffic(args.workload, n, args.mode) if D.world == 1 else None
         traffic = None
         if prof:
             traffic = prof["bytes_per_launch"]

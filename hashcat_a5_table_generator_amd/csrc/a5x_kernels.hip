@@ -706,8 +706,6 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
 #define VS_ABL 0     // k_keyspace_vsub timing ablations (variant builds only, wrong output): 1 no build
                      // pass, 2 no count pass, 4 no tasks (walk + pattern analysis only)
 #endif
-#define VS_RST 65    // record u64 per sub-word (built in the wave's LDS stage, copied out by the wave; odd:
-                     // the lanes' records start on distinct LDS banks)
 #define VS_BLOCK 64  // k_keyspace_vsub workgroup (LDS per lane ~340 B: 7 one-wave workgroups per CU)
 
 struct VsWord {
@@ -838,27 +836,30 @@ struct VsWave {  // per-wave LDS state
   u32 ctot[64], btot[64], rtot[64], bad[64];
   uint4 info[64];                     // word: L | nocc << 8 | nt << 16 | S << 24, tr, tk
   unsigned long long base[64];
-  u64 stage[64 * VS_RST];             // build pass: the round's records (<= VS_RST u64), copied out
 };
 
-// Record sink of the build pass: the record in the lane's part of the wave's LDS stage,
-// the open group built in place where close_group leaves it (entries 1 + np + ne ...: its
-// copy-out is then a no-op).
+// Record sink of the build pass: the open group in LDS (lane-strided by VS_BLOCK),
+// descriptors and entries straight to the record in HBM (DevRecSink's layout).
 struct VsRecSink {
+  u64* g;
   u64* rec;
   u32 np;
   __device__ u64* cbuf() const { return nullptr; }  // (no clusters: lone units only)
   __device__ u32 cstride() const { return 1; }
-  __device__ u64 gld(u32 ne, u32 a) const { return rec[1 + np + ne + a]; }
-  __device__ void gst(u32 ne, u32 a, u64 v) { rec[1 + np + ne + a] = v; }
+  __device__ u64 gld(u32, u32 a) const { return g[a * VS_BLOCK]; }
+  __device__ void gst(u32, u32 a, u64 v) { g[a * VS_BLOCK] = v; }
   __device__ void ent(u32 i, u64 v) { rec[1 + np + i] = v; }
   __device__ void desc(u32 i, u64 v) { rec[1 + i] = v; }
 };
 
-__global__ void __launch_bounds__(VS_BLOCK) k_keyspace_vsub(KsArgs a) {
+#ifndef VS_WPE
+#define VS_WPE 3  // waves per SIMD the register budget is cut for (LDS admits ~7 one-wave workgroups per CU)
+#endif
+__global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(VS_WPE))) k_keyspace_vsub(KsArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 tb = (a.table_bytes + 15u) & ~15u;
-  uint8_t* wsl = smem + tb;                                      // VS_BLOCK x VS_WSLOT word bytes
+  u64* gbuf = (u64*)(smem + tb);                                 // VS_BLOCK x KS_GCAP open-group entries
+  uint8_t* wsl = smem + tb + VS_BLOCK * KS_GCAP * 8;             // VS_BLOCK x VS_WSLOT word bytes
   uint8_t* ssl = wsl + VS_BLOCK * VS_WSLOT;                      // VS_BLOCK x VS_SLOT sub-word bytes
   uint16_t* occ0 = (uint16_t*)(ssl + VS_BLOCK * VS_SLOT);        // VS_OCC x VS_BLOCK occurrences
   VsWave* wvs = (VsWave*)(occ0 + VS_BLOCK * VS_OCC);             // one per wave
@@ -1017,13 +1018,11 @@ __global__ void __launch_bounds__(VS_BLOCK) k_keyspace_vsub(KsArgs a) {
           pl.finish(Ls);
           f = vs_fast(A, pl.P, Ls, s == 0 ? cmin : 0u, rs, cnt, byt);
         }
-        f = f && rs <= VS_RST;
         Q.tinfo[Q.tbase[l] + s] = (uint16_t)(f && rs ? pl.P.np | (rs << 4) : 0u);
         if (s == 0) {
           const u32 rfull = 1u + pl.P.np + pl.P.ne;  // (the record of a sub-word with candidates)
           Q.u0[l] = pl.P.np | (min(rfull, 255u) << 8) | (Ls << 16);
           Q.uP[l] = (u32)min(A.P, (u64)0xFFFFFFFFu);
-          f = f && (W.S == 1 || rfull <= VS_RST);
         }
         if (!f) atomicOr(&Q.bad[l], 1u);
         else {
@@ -1055,12 +1054,9 @@ __global__ void __launch_bounds__(VS_BLOCK) k_keyspace_vsub(KsArgs a) {
     Q.base[lane] = room ? base : ~0ull;
     Q.rtot[lane] = rtot;
     WAVE_SYNC();
-    // ---- build pass: records and metas at the word's base; records of <= VS_RST u64 built
-    // in the wave's LDS stage and copied out by the whole wave (coalesced) ----
+    // ---- build pass: records and metas at the word's base ----
     for (u32 t0 = 0; t0 < ntask; t0 += 64) {
       const u32 t = t0 + lane;
-      u32 rso = 0;       // record u64 staged by this lane
-      u64 dst = 0;       // its place in vrec
       if (t < ntask) {
         VsWord W;
         u32 l, s;
@@ -1076,7 +1072,7 @@ __global__ void __launch_bounds__(VS_BLOCK) k_keyspace_vsub(KsArgs a) {
           u64 cnt = 0, byt = 0;
           if (np) {
             VsRecSink sk;
-            sk.rec = &Q.stage[lane * VS_RST]; sk.np = np;
+            sk.g = gbuf + tid; sk.rec = rb + ro; sk.np = np;
             Planner<true, LWord, VsRecSink, KS_GCAP> pb(lw, T, sk, 0u);
             CountAcc A;
             count_init(A, 0);
@@ -1085,21 +1081,11 @@ __global__ void __launch_bounds__(VS_BLOCK) k_keyspace_vsub(KsArgs a) {
             const Plan& P = pb.P;
             if (!Ls || !vs_fast(A, P, Ls, s == 0 ? cmin : 0u, rs, cnt, byt) || P.np != np || rs != rs0)
               atomicOr(a.err, A5X_DERR_STATE);
-            sk.rec[0] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
-            rso = rs0;
-            dst = (u64)wb + ro;
+            rb[ro] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
           }
           rb[Q.rtot[l] + s] = cnt | ((u64)rs << 24) | (byt << 32);
         }
       }
-      WAVE_SYNC();
-      for (u32 l = 0; l < 64; l++) {
-        const u32 n2 = readlane_u32(rso, l);
-        if (!n2) continue;
-        const u64 d2 = readlane_u64(dst, l);
-        if (lane < n2) a.vrec[d2 + lane] = Q.stage[l * VS_RST + lane];
-      }
-      WAVE_SYNC();
     }
     // ---- word lane: results ----
     if (room) {
@@ -3101,7 +3087,7 @@ size_t a5x_keyspace_rprobe_lds(u32 table_bytes) {
 }
 
 size_t a5x_keyspace_vsub_lds(u32 table_bytes) {
-  return ((table_bytes + 15u) & ~15u) + VS_BLOCK * (VS_WSLOT + VS_SLOT + VS_OCC * 2) +
+  return ((table_bytes + 15u) & ~15u) + VS_BLOCK * (KS_GCAP * 8 + VS_WSLOT + VS_SLOT + VS_OCC * 2) +
          (VS_BLOCK / 64) * sizeof(VsWave);
 }
 

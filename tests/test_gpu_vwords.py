@@ -166,3 +166,24 @@ def test_virtual_fused_md5_hits(vtab, mode, mn):
         if plain.startswith(b"$HEX[") and plain.endswith(b"]"):
             plain = binascii.unhexlify(plain[5:-1])
         assert hashlib.md5(plain).hexdigest().encode() == hx, line
+
+
+@pytest.mark.parametrize("mode,mn", [(2, 0), (2, 1), (3, 0), (3, 1)])
+def test_virtual_one_byte_ties(tmp_path, mode, mn):
+    """One-byte keys with one-byte values (every sub-word shares one layout: one build
+    writes all sub-word records, patching the tied bytes), words whose pieces hold many
+    tied occurrences (runs of one letter) -- against the C oracle."""
+    from hashcat_a5_table_generator_amd import Context
+    p = tmp_path / "ascii.table"
+    p.write_bytes(b"a=@\na=4\ns=$\ne=3\no=0\ni=!\nt=7\n")
+    rng = np.random.default_rng(7 + mode + 10 * mn)
+    alpha = "aseoitxyz"
+    words = ["".join(alpha[int(x)] for x in rng.integers(0, len(alpha), size=int(rng.integers(1, 20)))).encode()
+             for _ in range(1500)]
+    words += [b"a" * n for n in range(1, 30)] + [b"sassafras", b"essentials", b"tattoo", b"aaaaeeeeoooo"]
+    want = _oracle(str(p), words, mode, mn, 15)
+    with Context(0) as c:
+        c.load_tables([str(p)])
+        got = c.expand_words(words, mode, mn, 15)
+    for w, g, e in zip(words, got, want):
+        assert sorted(g) == e, (mode, mn, w, len(g), len(e))

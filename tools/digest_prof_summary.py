@@ -8,7 +8,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from bench import digest_src_sha  # noqa: E402
+from bench import MODE_NAMES, digest_src_sha  # noqa: E402
 
 
 def breakdown(algos):
@@ -61,10 +61,14 @@ for line in open(os.path.join(out, "dpmc1_%s.log" % algo)):
         bench = json.loads(line)
 cands = bench["config"]["candidates_per_gpu_step"]
 stats = list(csv.DictReader(open(glob.glob(os.path.join(out, "dprof_" + algo, "run_kernel_stats.csv"))[0])))
-dig = next((r for r in stats if kname in r["Name"]), None)
+# (kname "a+b": the digest stage's kernels, a = the first; their VALU counters summed)
+dig = next((r for r in stats if kname.split("+")[0] in r["Name"]), None)
 valu = sum(c1.get("SQ_INSTS_VALU", [0]))
+mode = next((k for k, v in MODE_NAMES.items() if v == bench["config"].get("mode")), 0)
+mn = int(bench["config"].get("table_min", 0))
 res = {
     "workload": "c5", "words": words, "algo": algo, "kernel": kname, "kernel_src_sha": digest_src_sha(),
+    "mode": mode, "min": mn,
     "candidates_per_step": cands,
     "valu_wave_insts_per_cand": valu / cands,
     "int_ops_per_cand": valu * 64 / cands,
@@ -77,5 +81,6 @@ res = {
     "note": "SQ_INSTS_VALU summed over the %s dispatches of one step (1 step, 0 warmup; the "
             "planted-target setup adds ~1e6 candidates); int_ops = wave instructions x 64 lanes" % kname,
 }
-json.dump(res, open(os.path.join(out, "pmc_digest_%s_%s_c5.json" % (algo, kname)), "w"), indent=1)
+tag = kname.replace("+", "_").replace("*", "") + ("_m%d_min%d" % (mode, mn) if mode else "")
+json.dump(res, open(os.path.join(out, "pmc_digest_%s_%s_c5.json" % (algo, tag)), "w"), indent=1)
 print(json.dumps(res))

@@ -13,7 +13,9 @@
 #   traffic     PMC WRITE_SIZE / FETCH_SIZE of k_expand_fast -> gpurun_out/pmc_$TAG_$WL.json
 #               [WL, WORDS, KRE]
 #   pmc         PMC counter groups, one pass each (PMC="group\ngroup", KRE, BENCH_ARGS)
-#   digestprof  fused-digest kernel stats + VALU counters [ALGOS, KRE, WORDS]
+#   digestprof  fused-digest kernel stats + VALU counters [ALGOS, KRE, KNAME, WORDS, DARGS]
+#               (modes: KRE="k_expand_fast_md5|k_mode_digest" KNAME="k_expand_fast_md5+k_mode_digest_*"
+#               DARGS="--mode 3 --min 1")
 #   stamps      per-phase cycle stamps (diagnostic build _build_diag) [WL, SW]
 #   final       test + C3 bench (+ steady state, CPU baseline)/prof/traffic + C4 + C2a
 #   final2      fused digests (+ dabl op breakdown) + C5 modes (+ rocprof) + stdout path
@@ -90,15 +92,17 @@ for r in list(csv.DictReader(open("$R/gpurun_out/prof_$T/run_kernel_stats.csv"))
 PY
 }
 
-step_traffic() {
-  local W=${WORDS:-10000000} WLx=${WL:-c3}
-  local ARGS="--steps 1 --warmup 0 --no-cpu-baseline --words $W --workload $WLx"
+step_traffic() {  # [WL, WORDS, KRE, TMODE: -r / -s / -s -r (the expansion's k_expand_fast + item kernels summed)]
+  local W=${WORDS:-10000000} WLx=${WL:-c3} M=${TMODE:-0}
+  local ARGS="--steps 1 --warmup 0 --no-cpu-baseline --words $W --workload $WLx --mode $M --steady-batches 0"
+  local K=${KRE:-k_expand_fast}
+  [ "$M" != 0 ] && K=${KRE:-'k_expand_fast|k_mode_items_fast|k_mode_items_pos|k_mode_items_b\('}
   for grp in WRITE_SIZE FETCH_SIZE; do
-    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-k_expand_fast}" \
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "$K" \
         -d $R/gpurun_out/pmct_${T}_$grp -o run --output-format csv -- python3 $R/bench.py $ARGS \
         > $R/gpurun_out/pmct_${T}_$grp.log 2>&1 ) || { echo "pmc $grp failed"; tail -5 gpurun_out/pmct_${T}_$grp.log; return 14; }
   done
-  python3 tools/pmc_summary.py traffic "$T" "$WLx" "$W" "${KRE:-k_expand_fast}"
+  python3 tools/pmc_summary.py traffic "$T" "$WLx" "$W" "$K" "$M"
 }
 
 step_pmc() {
@@ -121,7 +125,7 @@ GROUPS
 step_digestprof() {
   local W=${WORDS:-2000000}
   for A in ${ALGOS:-md5 ntlm}; do
-    local K=${KRE:-k_expand_fast_$A}
+    local K=${KRE:-k_expand_fast_$A} KN=${KNAME:-${KRE:-k_expand_fast_$A}}
     local ARGS="--digest $A --workload c5 --words $W --no-cpu-baseline --targets 1000000 ${DARGS}"
     ( cd /tmp && export TMPDIR=/tmp &&
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/dprof_$A -o run --output-format csv -- \
@@ -134,7 +138,7 @@ step_digestprof() {
         --kernel-include-regex $K -d $R/gpurun_out/dpmc2_$A -o run --output-format csv -- \
         python3 $R/bench.py $ARGS --steps 1 --warmup 0 > $R/gpurun_out/dpmc2_$A.log 2>&1 ) \
       || echo "derived VALUBusy pass $A failed (raw counters only)"
-    python3 tools/digest_prof_summary.py $A $W $K || return 16
+    python3 tools/digest_prof_summary.py $A $W "$KN" || return 16
   done
 }
 

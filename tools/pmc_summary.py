@@ -48,21 +48,26 @@ def mix(prefix):
             print(f"   LDS bank-conflict share       {d['SQ_LDS_BANK_CONFLICT'] / d['SQ_LDS_IDX_ACTIVE']:.3f}")
 
 
-def traffic(tag, wl, words, kernel):
+def traffic(tag, wl, words, kernel, mode=0):
+    """Default mode: per k_expand_fast dispatch (average).  -r / -s / -s -r (mode > 0): the
+    expansion is k_expand_fast beside the mode engine's item kernels, so the traffic of the
+    step (1 step, 0 warmup: one expansion) is the sum over all the matched dispatches."""
     sys.path.insert(0, ROOT)
     from bench import kernel_src_sha
     vals = {}
     for grp in ("WRITE_SIZE", "FETCH_SIZE"):
         f = glob.glob(os.path.join(ROOT, "gpurun_out", f"pmct_{tag}_{grp}", "run_counter_collection.csv"))[0]
         v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if r["Counter_Name"] == grp]
-        vals[grp] = sum(v) / len(v)  # per dispatch (KiB)
+        vals[grp] = sum(v) if mode else sum(v) / len(v)  # KiB per dispatch / per step
     write_b = vals["WRITE_SIZE"] * 1024
     fetch_b = vals["FETCH_SIZE"] * 1024 * 2
-    out = {"workload": wl, "words": words, "kernel": kernel, "kernel_src_sha": kernel_src_sha(),
+    out = {"workload": wl, "words": words, "kernel": kernel, "kernel_src_sha": kernel_src_sha(), "mode": mode,
            "write_size_kib": vals["WRITE_SIZE"], "fetch_size_kib": vals["FETCH_SIZE"],
            "bytes_per_launch": write_b + fetch_b, "write_bytes": write_b, "fetch_bytes_corrected": fetch_b,
            "note": "rocprofv3 --pmc WRITE_SIZE / FETCH_SIZE in separate passes; KiB; FETCH_SIZE x2 (gfx950)"}
-    with open(os.path.join(ROOT, "gpurun_out", f"pmc_{tag}_{wl}.json"), "w") as fh:
+    if mode:
+        out["note"] += "; summed over the step's dispatches (k_expand_fast + mode-engine item kernels)"
+    with open(os.path.join(ROOT, "gpurun_out", f"pmc_{tag}_{wl}{'_mode%d' % mode if mode else ''}.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))
 
@@ -71,6 +76,7 @@ if __name__ == "__main__":
     if sys.argv[1] == "mix":
         mix(sys.argv[2])
     elif sys.argv[1] == "traffic":
-        traffic(sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5] if len(sys.argv) > 5 else "k_expand_fast")
+        traffic(sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5] if len(sys.argv) > 5 else "k_expand_fast",
+                int(sys.argv[6]) if len(sys.argv) > 6 else 0)
     else:
         raise SystemExit(__doc__)
