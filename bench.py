@@ -721,7 +721,8 @@ def main():
                 "traffic": traffic,
                 "kernel": ("k_expand_fast+k_expand_slow+k_expand_b (launched when present)" if args.mode == 0
                            else "k_expand_fast (-r FAST words) + k_mode_items_* (the other words), one stream each"
-                           if args.mode == 1 else "k_mode_items_* (expansion pass)"),
+                           if args.mode == 1 else
+                           "k_expand_fast (FAST-probe and virtual words) + k_mode_items_* (the other words), one stream each"),
                 "ms_per_launch": ms_exp,
                 "ms_per_launch_max_rank": ms_exp_max,
                 "ms_keyspace_scan_plan": ms_ks,
