@@ -91,7 +91,9 @@ class Dist:
         self.device = 0 if same_device else self.local  # the GPU this rank drives
         self.backend = backend
         self.dist = None
-        if self.world > 1:
+        # (A5X_FORCE_DIST=1 under torchrun: the process group and every collective of the
+        # multi-rank path also at WORLD_SIZE=1 -- an RCCL rehearsal on a one-GPU box)
+        if self.world > 1 or os.environ.get("A5X_FORCE_DIST") == "1":
             import torch
             import torch.distributed as dist
             if backend == "nccl":
@@ -142,7 +144,7 @@ def shard_for_rank(args, D, ctx, intra_word=True):
     n_total = args.words * D.world
     b0, b1 = hd.block_bounds(n_total, D.world, D.rank)
     tables, (bd, bo) = synth.global_words(args.workload, b0, b1, seed=SEED)
-    if D.world == 1:
+    if D.dist is None:
         return tables, bd, bo, (0, n_total), (0, None)
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw, do = DeviceBuffer.from_array(ctx, bd), DeviceBuffer.from_array(ctx, bo)
@@ -350,7 +352,7 @@ def plant_targets(args, D, ctx, data, offs, w0, algo):
         dig = db.to_array(count=16 * len(mine)).reshape(-1, 16)
         rows = hd.hits_to_rows([(g, k, bytes(dig[i])) for i, (g, k) in enumerate(mine)])
     allrows = rows
-    if D.world > 1:  # every rank gets every rank's planted rows (an all-gather)
+    if D.dist is not None:  # every rank gets every rank's planted rows (an all-gather)
         allrows = _allgather_rows(D, rows, hd.allgather_u64(D.dist, [len(rows)], D.backend)[:, 0])
     planted = hd.rows_to_hits(allrows)
     pd = np.frombuffer(b"".join(d for _, _, d in planted), dtype=np.uint8).reshape(-1, 16)
@@ -646,7 +648,7 @@ def main():
     dt = time.perf_counter() - t0
     dt_max = D.reduce(dt, "max")
     cands_all = D.reduce(float(tc) * args.steps, "sum")
-    bytes_per_rank = [tb] if D.world == 1 else \
+    bytes_per_rank = [tb] if D.dist is None else \
         [int(x) for x in __import__("hashcat_a5_table_generator_amd.dist", fromlist=["x"]).allgather_u64(
             D.dist, [tb], D.backend)[:, 0]]
     ms_exp = float(np.mean([s["ms_expand"] for s in stats]))

@@ -112,3 +112,27 @@ def test_two_ranks_digest_hits_gathered(tmp_path, algo):
     key = lambda h: sorted(map(tuple, h.tolist()))
     assert key(h2) == key(h1)
     assert r2["config"]["hits_gathered_on_rank0"] == len(h1) and r2["config"]["planted"] == r1["config"]["planted"]
+
+
+@pytest.mark.parametrize("wl,mode", [("c3", 0), ("c5", 3)])
+def test_rccl_world1_rehearsal(tmp_path, wl, mode):
+    """The RCCL branch (backend nccl: process group with device_id, cuda-tensor all-gather /
+    all-reduce, candidate-granular split) under torchrun at WORLD_SIZE=1 (A5X_FORCE_DIST):
+    per-word digests equal the plain single-process run -- the N>1 code path executed on
+    the one-GPU box (the driver runs N = 2..8 on a full node)."""
+    args = ["--workload", wl, "--mode", str(mode), "--steady-batches", "0", "--words", "60000",
+            "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+    d1 = tmp_path / "rccl"
+    env = dict(os.environ, A5X_FORCE_DIST="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--dump", str(d1), *args]
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert r["n_gpus"] == 1 and r["config"]["candidates_per_gpu_step"] > 0
+    _bench(1, ["--workload", wl, "--mode", str(mode), "--steady-batches", "0", "--words", "60000"], tmp_path / "plain")
+    a0, a1, dr = _digests(d1)
+    b0, b1, dp = _digests(tmp_path / "plain")
+    assert (a0, a1) == (b0, b1) == (0, 60000)
+    assert np.array_equal(dr, dp)
