@@ -187,3 +187,30 @@ def test_virtual_one_byte_ties(tmp_path, mode, mn):
         got = c.expand_words(words, mode, mn, 15)
     for w, g, e in zip(words, got, want):
         assert sorted(g) == e, (mode, mn, w, len(g), len(e))
+
+
+@pytest.mark.parametrize("mode,mn", [(2, 0), (3, 1)])
+def test_virtual_fused_ntlm_every_candidate(mode, mn):
+    """Fused NTLM over C5-shaped words (virtual words in k_expand_fast_ntlm: Go's UTF-16LE of
+    sub-word entries, hits mapped back to (word, index)), every candidate a target: each
+    reported once with the RFC 1320 MD4 of its UTF-16LE (oracle/digest_oracle.py)."""
+    from hashcat_a5_table_generator_amd import Context, pack_words
+    from oracle import digest_oracle as dg
+    rng = np.random.default_rng(120 + mode)
+    words = [("".join(LETTERS[int(x)] for x in rng.integers(0, 12, size=int(rng.integers(3, 10))))).encode()
+             for _ in range(800)]
+    with Context(0) as ctx:
+        ctx.load_tables([table_path("greek-hebrew")])
+        per_word = ctx.expand_words(words, mode, mn, 15)
+        want = {}
+        for w, cs in enumerate(per_word):
+            for i, c in enumerate(cs):
+                want.setdefault(dg.ntlm(c), set()).add((w, i))
+        ctx.set_targets(1, b"".join(want))
+        hits, _ = ctx.expand_digest(*pack_words(words), mode, mn, 15, hit_cap=1 << 20)
+    got = {}
+    for w, c, d in hits:
+        assert dg.ntlm(per_word[w][c]) == d, (mode, w, c)
+        got.setdefault(d, set()).add((w, c))
+    assert sum(len(v) for v in got.values()) == len(hits)
+    assert got == want
