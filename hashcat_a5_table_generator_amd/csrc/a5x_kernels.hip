@@ -706,6 +706,11 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
 #define VS_ABL 0     // k_keyspace_vsub timing ablations (variant builds only, wrong output): 1 no build
                      // pass, 2 no count pass, 4 no tasks (walk + pattern analysis only)
 #endif
+#ifndef VS_GCAP
+#define VS_GCAP 4    // entries per open group of the sub-word planner (C5 -s A/B, 4 vs 8 = KS_GCAP:
+                     // keyspace 27.1 vs 29.2 ms, the same words split, expansion unchanged; 2: most
+                     // words past 8 pieces)
+#endif
 #define VS_BLOCK 64  // k_keyspace_vsub workgroup (LDS per lane ~340 B: 7 one-wave workgroups per CU)
 
 struct VsWord {
@@ -1009,7 +1014,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
         CountAcc A;
         count_init(A, 0);
         NullSink ns;
-        Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
+        Planner<false, LWord, NullSink, VS_GCAP> pl(lw, T, ns);
         const u32 Ls = vs_build(T, W, wsl + wl * VS_WSLOT, sub, occ0 + wl, s, a.rmode, pl, A);
         u32 rs = 0;
         u64 cnt = 0, byt = 0;
@@ -1073,7 +1078,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
           if (np) {
             VsRecSink sk;
             sk.g = gbuf + tid; sk.rec = rb + ro; sk.np = np;
-            Planner<true, LWord, VsRecSink, KS_GCAP> pb(lw, T, sk, 0u);
+            Planner<true, LWord, VsRecSink, VS_GCAP> pb(lw, T, sk, 0u);
             CountAcc A;
             count_init(A, 0);
             const u32 Ls = vs_build(T, W, wsl + wl * VS_WSLOT, sub, occ0 + wl, s, a.rmode, pb, A);
