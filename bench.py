@@ -86,6 +86,8 @@ class Dist:
 
     def __init__(self, n_gpus: int, backend: str = "nccl", same_device: bool = False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        if n_gpus != self.world:  # (launch_ranks sets WORLD_SIZE = --gpus; a launcher must agree)
+            raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={self.world} from the launcher")
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.device = 0 if same_device else self.local  # the GPU this rank drives
@@ -102,8 +104,6 @@ class Dist:
             else:
                 dist.init_process_group(backend)
             self.dist, self.torch = dist, torch
-        if n_gpus != self.world and self.rank == 0:
-            log(f"note: --gpus {n_gpus} but WORLD_SIZE={self.world}; using WORLD_SIZE")
 
     def barrier(self):
         if self.dist:
@@ -608,8 +608,62 @@ def run_stdout(args, D):
     print(json.dumps(line), flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """``bench.py --gpus N`` with no launcher (WORLD_SIZE unset): this process starts N
+    child ranks of itself -- RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1
+    and a free MASTER_PORT, i.e. what ``torch.distributed.run --nproc-per-node N`` gives
+    them -- relays rank 0's stdout (the one JSON line) and returns non-zero if any rank
+    fails (the others are then terminated).  The parent never touches the GPU: the ranks
+    initialise it, one process per GPU (main.go:70-95's data parallelism over words, here
+    over devices)."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    log(f"launched {n} ranks (pids {[p.pid for p in procs]}, master 127.0.0.1:{port})")
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            if p.poll() is not None:
+                live.remove(p)
+                if p.returncode and not rc:
+                    rc = p.returncode
+                    log(f"rank {procs.index(p)} exited with {p.returncode}; stopping the other ranks")
+                    for q in live:
+                        q.terminate()
+        if live:
+            time.sleep(0.2)
+    out = procs[0].stdout.read().decode(errors="replace")
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return rc if rc > 0 else (1 if rc else 0)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus))
+    probe = os.environ.get("A5X_LAUNCH_PROBE")  # (tests: the rank environment, before any GPU work)
+    if probe:
+        if probe == "fail" and os.environ.get("RANK") == "1":
+            raise SystemExit(3)
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                         "MASTER_PORT")}), flush=True)
+        return
     D = Dist(args.gpus, args.backend, args.same_device)
     if args.stdout:
         return run_stdout(args, D)
@@ -618,7 +672,8 @@ def main():
     from hashcat_a5_table_generator_amd import Context, DeviceBuffer, synth
 
     ctx = Context(D.device)
-    tables, data, offs, (w0, w1), (cb, ncand) = shard_for_rank(args, D, ctx)
+    # (--verify checks whole words against the oracle on every rank: word-boundary shards)
+    tables, data, offs, (w0, w1), (cb, ncand) = shard_for_rank(args, D, ctx, intra_word=not args.verify)
     n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)

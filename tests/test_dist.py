@@ -263,3 +263,41 @@ def test_candidate_split_cuts_huge_words(tmp_path, world):
     assert max(sizes) / min(sizes) < 1.01, sizes
     split = res[0]["split"]
     assert any(c > 0 for c in split[2]), split  # at least one split falls inside a word
+
+
+def _bench_cmd(*args):
+    return [sys.executable, os.path.join(ROOT, "bench.py"), *args]
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """``bench.py --gpus 3`` with no launcher starts 3 ranks itself (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* as torch.distributed.run sets them) and relays rank 0's stdout
+    line only; the parent touches no GPU (A5X_LAUNCH_PROBE: the ranks stop before it)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(_bench_cmd("--gpus", "3"), env=dict(env, A5X_LAUNCH_PROBE="1"), stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    import json
+    r0 = json.loads(lines[0])
+    assert r0["RANK"] == "0" and r0["LOCAL_RANK"] == "0" and r0["WORLD_SIZE"] == "3"
+    assert r0["MASTER_ADDR"] == "127.0.0.1" and int(r0["MASTER_PORT"]) > 0
+    others = [json.loads(ln) for ln in p.stderr.splitlines() if ln.startswith("{")]
+    assert sorted(o["RANK"] for o in others) == ["1", "2"]
+    assert {o["MASTER_PORT"] for o in others} == {r0["MASTER_PORT"]}
+
+
+def test_bench_launch_fails_if_a_rank_fails():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(_bench_cmd("--gpus", "2"), env=dict(env, A5X_LAUNCH_PROBE="fail"), stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=120)
+    assert p.returncode != 0
+    assert "rank 1 exited with 3" in p.stderr
+
+
+def test_bench_refuses_gpus_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="1")
+    p = subprocess.run(_bench_cmd("--gpus", "3", "--backend", "gloo"), env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=120)
+    assert p.returncode != 0 and "--gpus 3 but WORLD_SIZE=2" in p.stderr

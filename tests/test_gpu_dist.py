@@ -136,3 +136,21 @@ def test_rccl_world1_rehearsal(tmp_path, wl, mode):
     b0, b1, dp = _digests(tmp_path / "plain")
     assert (a0, a1) == (b0, b1) == (0, 60000)
     assert np.array_equal(dr, dp)
+
+
+def test_bench_gpus_2_without_launcher(tmp_path):
+    """``bench.py --gpus 2`` with no torchrun starts its own two ranks (gloo, both
+    on device 0 here), reports n_gpus 2, and their per-word digests equal a one-rank run."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    args = ["--workload", "c3", "--steady-batches", "0", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--same-device",
+           "--words", "20000", "--dump", str(tmp_path / "w2"), *args]
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r2 = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert r2["n_gpus"] == 2
+    _bench(1, ["--workload", "c3", "--steady-batches", "0", "--words", "40000"], tmp_path / "w1")
+    a0, a1, d2 = _digests(tmp_path / "w2")
+    b0, b1, d1 = _digests(tmp_path / "w1")
+    assert (a0, a1) == (b0, b1) == (0, 40000)
+    assert np.array_equal(d2, d1)
