@@ -234,26 +234,41 @@ def cpu_model() -> str:
 
 
 def cpu_threads() -> int:
-    """Host threads for the CPU baseline: every core this process may use, capped at the
-    GPU box's per-GPU CPU share (16; nproc there shows the whole machine)."""
+    """Every core this process may use (its CPU affinity; on the GPU box nproc shows the
+    whole machine, of which one GPU's share is 16)."""
     try:
-        n = len(os.sched_getaffinity(0))
+        return max(1, len(os.sched_getaffinity(0)))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        return os.cpu_count() or 1
+
+
+def cpu_quota() -> str:
+    """The cgroup CPU quota (cpu.max), if one limits this process."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+        return "none" if q == "max" else f"{int(q) / int(p):g} CPUs"
+    except (OSError, ValueError):
+        return "unknown"
+
+
+def thread_counts() -> list:
+    """1 worker, the GPU box's per-GPU share (16) and all cores the process may use."""
+    n = cpu_threads()
+    return sorted({1, min(16, n), n})
 
 
 def cpu_baseline(tables, args):
     """The reference algorithm restated in C (oracle/a5_oracle.c) with main.go:58-98's
     structure -- one worker per word from a pool, every candidate sent on a 1000-slot
-    channel, one writer with a 4 KiB buffer -- timed at 1 thread and at all host threads."""
+    channel, one writer with a 4 KiB buffer -- timed at 1 thread, 16 threads and every core
+    the process may use (all runs reported; value = the best)."""
     from oracle import c_oracle as co
     from hashcat_a5_table_generator_amd import synth
     t = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", x + ".table") for x in tables])
     fd = os.open(os.devnull, os.O_WRONLY)
     runs = []
-    nmax = cpu_threads()
-    for th in sorted({1, nmax}):
+    for th in thread_counts():
         nwords = args.cpu_sample_words
         _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
         t0 = time.perf_counter()
@@ -264,34 +279,39 @@ def cpu_baseline(tables, args):
     os.close(fd)
     best = max(runs, key=lambda r: r["value"])
     return {"value": best["value"], "unit": "candidates/s", "cores": best["threads"], "kind": "port",
-            "cpu_model": cpu_model(), "runs": runs,
+            "cpu_model": cpu_model(), "cpu_affinity": cpu_threads(), "cpu_quota": cpu_quota(), "runs": runs,
             "sample": f"{args.cpu_sample_words} words of workload {args.workload} (seed 0xC0FFEE) to /dev/null; "
                       f"C restatement of main.go (oracle/a5_oracle.c) with its goroutine pool, 1000-slot channel "
-                      f"(lock-free ring; a blocked sender or receiver spins briefly, then parks on a futex like a goroutine) and one 4 KiB writer; best of 1 and "
-                      f"{nmax} worker thread(s) ({cpu_model()})"}
+                      f"(lock-free ring; a blocked sender or receiver spins briefly, then parks on a futex like a "
+                      f"goroutine) and one 4 KiB writer; runs at {[r['threads'] for r in runs]} worker thread(s), "
+                      f"the best reported ({cpu_model()}, affinity {cpu_threads()} CPUs, quota {cpu_quota()})"}
 
 
-def digest_cpu_baseline(tables, args):
-    """Reference algorithm restated in C (oracle/a5_oracle.c) + per-candidate digest on one host core."""
+def digest_cpu_baseline(tables, args, targets):
+    """The reference expansion restated in C (oracle/a5_oracle.c) with every candidate
+    digested (MD5 / NTLM = MD4 of Go's UTF-16LE, in C) and probed in the same target set,
+    one word per worker task (main.go:77-93's goroutines), timed at 1 thread, 16 and every
+    core the process may use."""
     from oracle import c_oracle as co
-    from oracle import digest_oracle as dg
     from hashcat_a5_table_generator_amd import synth
     t = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", x + ".table") for x in tables])
-    nwords = max(50, args.cpu_sample_words // (50 if args.digest == "md5" else 2000))
+    nwords = max(50, args.cpu_sample_words // 10)
     _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
-    f = dg.ALGOS[0 if args.digest == "md5" else 1]
-    t0 = time.perf_counter()
-    out, _ = t.expand_batch(data, offs, args.mode, args.min, args.max)
-    n = 0
-    for line in bytes(out).split(b"\n")[:-1]:
-        f(line)
-        n += 1
-    dt = time.perf_counter() - t0
-    log(f"cpu digest baseline: {n / dt / 1e6:.3f} Mcand/s ({dt:.2f} s)")
-    return {"value": n / dt, "unit": "candidates/s", "cores": 1, "kind": "port",
-            "sample": f"{nwords} words of workload {args.workload} (seed 0xC0FFEE): {n} candidates; C restatement "
-                      f"of main.go expansion + {'hashlib MD5' if args.digest == 'md5' else 'RFC 1320 MD4 in Python (NTLM)'}"
-                      f" per candidate, 1 thread"}
+    algo = 0 if args.digest == "md5" else 1
+    runs = []
+    for th in thread_counts():
+        t0 = time.perf_counter()
+        n, hits = t.digest_run(data, offs, args.mode, args.min, args.max, algo, targets, th)
+        dt = time.perf_counter() - t0
+        runs.append({"threads": th, "value": n / dt, "seconds": dt, "candidates": n, "hits": hits})
+        log(f"cpu digest baseline threads={th}: {n / dt / 1e6:.3f} Mcand/s ({dt:.2f} s)")
+    best = max(runs, key=lambda r: r["value"])
+    return {"value": best["value"], "unit": "candidates/s", "cores": best["threads"], "kind": "port", "runs": runs,
+            "cpu_model": cpu_model(), "cpu_affinity": cpu_threads(), "cpu_quota": cpu_quota(),
+            "sample": f"{nwords} words of workload {args.workload} (seed 0xC0FFEE): C restatement of main.go's "
+                      f"expansion + {args.digest.upper()} in C ({'RFC 1321' if algo == 0 else 'RFC 1320 MD4 of Go UTF-16LE'})"
+                      f" + probe of the same {len(targets)} targets per candidate; runs at {[r['threads'] for r in runs]}"
+                      f" thread(s), the best reported"}
 
 
 def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
@@ -438,7 +458,7 @@ def run_digest(args, D):
                                       "digests all-gathered); hit counts all-reduced, hit records gathered on rank 0 "
                                       "with global word indices"},
             "roofline": digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, dt_max / args.steps * 1e3),
-            "cpu_baseline": None if args.no_cpu_baseline else digest_cpu_baseline(tables, args),
+            "cpu_baseline": None if args.no_cpu_baseline else digest_cpu_baseline(tables, args, targets),
         }
         print(json.dumps(res_line), flush=True)
     D.barrier()

@@ -13,6 +13,7 @@
 // the hex digests of <file> and print what hashcat would report, "hash:plain" (plains
 // that hashcat would hexify as $HEX[...]), each target once, at its first candidate in
 // stream order (README.MD:74-106, :168).
+#include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -388,7 +389,10 @@ int main(int argc, char** argv) {
     th1.join();
     rc = failed.load();
     fclose(f);
-    fflush(stdout);
+    if (fflush(stdout) != 0 || ferror(stdout)) {  // (ENOSPC / EPIPE on the last buffer: not a success)
+      if (!rc) emsg = std::string("writing stdout: ") + strerror(errno);
+      rc = 1;
+    }
     TL("all batches written");
     if (rc) fprintf(stderr, "a5_generator: %s\n", emsg.c_str());
     fflush(stderr);

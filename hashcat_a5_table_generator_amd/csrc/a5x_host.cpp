@@ -1542,7 +1542,8 @@ int a5x_create(int device, a5x_ctx** out) {
     return A5X_E_HIP;
   }
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
-  if (const char* e = getenv("A5X_MSEG")) c->mseg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+  // (< 2^24: k_keyspace_vsub packs a sub-word count <= mseg into 24 bits)
+  if (const char* e = getenv("A5X_MSEG")) c->mseg = std::min<uint64_t>((1u << 24) - 1, std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
   if (const char* e = getenv("A5X_SEG")) c->seg = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
   // (tuning knobs; a5x_launch_expand clamps each launch to the kernel's compiled launch bound)
   if (const char* e = getenv("A5X_WAVES")) c->waves_per_block = std::max(1u, std::min(16u, (unsigned)atoi(e)));
@@ -1833,27 +1834,17 @@ int a5x_split_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff,
       else lo[i] = q[k];
     }
   }
-  // the word of each split candidate: binary search over the candidate offsets
-  const uint64_t* co = J.B.cand_off;
-  auto cand_at = [&](uint64_t w, uint64_t* v) -> int {
-    HIPCHK(c, hipMemcpyAsync(v, co + w, 8, hipMemcpyDeviceToHost, J.st));
-    HIPCHK(c, hipStreamSynchronize(J.st));
-    return A5X_OK;
-  };
+  // the word of each split candidate and its index there: one device binary search per target
+  if ((rc = grow(c, c->loc_q, nt)) || (rc = grow(c, c->loc_r, 2 * (size_t)nt))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->loc_q.p, hi.data(), 8 * (size_t)nt, hipMemcpyHostToDevice, J.st));
+  HIPCHK(c, a5x_launch_word_of(J.B.cand_off, nw, c->loc_q.p, nt, c->loc_r.p, c->loc_r.p + nt, J.st));
+  std::vector<uint64_t> wc(2 * (size_t)nt);
+  HIPCHK(c, hipMemcpyAsync(wc.data(), c->loc_r.p, 16 * (size_t)nt, hipMemcpyDeviceToHost, J.st));
+  if ((rc = job_check(c, J))) return rc;
   for (uint32_t i = 0; i < nt; i++) {
     cand_out[i] = hi[i];
-    if (hi[i] >= T) { word_out[i] = nw; ciw_out[i] = 0; continue; }
-    uint64_t a = 0, b = nw;  // cand_off[a] <= g < cand_off[b]
-    while (b - a > 1) {
-      const uint64_t m = a + (b - a) / 2;
-      uint64_t v = 0;
-      if ((rc = cand_at(m, &v))) return rc;
-      if (v <= hi[i]) a = m; else b = m;
-    }
-    uint64_t base = 0;
-    if ((rc = cand_at(a, &base))) return rc;
-    word_out[i] = a;
-    ciw_out[i] = hi[i] - base;
+    word_out[i] = wc[i];
+    ciw_out[i] = wc[nt + i];
   }
   return A5X_OK;
 }

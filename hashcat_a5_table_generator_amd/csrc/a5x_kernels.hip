@@ -808,8 +808,8 @@ __device__ __forceinline__ bool vs_fast(const CountAcc& A, const Plan& PL, u32 L
                                         u64& byt) {
   if (!A.ok || A.ovf || !PL.ok) return false;
   if (!(PL.np <= FW_PMAX && PL.ne <= 255 && 1 + PL.np + PL.ne <= FW_RMAX && PL.maxl <= FW_MAXL && PL.minl >= 3 &&
-        A.P <= FW_PMAX_CNT && PL.nbig <= FB_NMAX && PL.bent <= FB_EMAX))
-    return false;
+        A.P < FW_PMAX_CNT && PL.nbig <= FB_NMAX && PL.bent <= FB_EMAX))
+    return false;  // (A.P < 2^24: the sub-word's meta entry packs its count into 24 bits)
   cnt = A.P - cmin;
   byt = A.P * (u64)(Ls + 1) + A.Dp - A.Dn - (cmin ? (u64)(Ls + 1) : 0ull);
   rs = cnt ? 1u + PL.np + PL.ne : 0u;
@@ -3241,6 +3241,30 @@ hipError_t a5x_launch_locate(const A5xExpLaunch& L, const u64* cands, u32 n, u64
   u32 grid = n < 1024 ? (n ? n : 1) : 1024;
   if (L.gscr && L.gslots) grid = grid < L.gslots ? grid : L.gslots;  // one pass G slot per workgroup
   hipLaunchKernelGGL(k_locate, dim3(grid), dim3(64), a5x_keyspace_wave_lds(L.table_bytes), st, a, cands, n, out_bytes);
+  return hipGetLastError();
+}
+
+// The word of each global candidate g[i] (largest w with cand_off[w] <= g[i]) and its
+// index in that word; g[i] >= cand_off[nw] -> (nw, 0).  One lane per target
+// (a5x_split_device: one launch instead of a host binary search of device reads).
+__global__ void __launch_bounds__(256) k_word_of(const u64* cand_off, u64 nw, const u64* g, u32 nt, u64* word,
+                                                 u64* ciw) {
+  const u32 i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= nt) return;
+  const u64 x = g[i];
+  if (x >= cand_off[nw]) { word[i] = nw; ciw[i] = 0; return; }
+  u64 a = 0, b = nw;  // cand_off[a] <= x < cand_off[b]
+  while (b - a > 1) {
+    const u64 m = a + (b - a) / 2;
+    if (cand_off[m] <= x) a = m; else b = m;
+  }
+  word[i] = a;
+  ciw[i] = x - cand_off[a];
+}
+
+hipError_t a5x_launch_word_of(const u64* cand_off, u64 nw, const u64* g, uint32_t nt, u64* word, u64* ciw,
+                              hipStream_t st) {
+  if (nt) hipLaunchKernelGGL(k_word_of, dim3((nt + 255) / 256), dim3(256), 0, st, cand_off, nw, g, nt, word, ciw);
   return hipGetLastError();
 }
 

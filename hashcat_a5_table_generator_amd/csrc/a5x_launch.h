@@ -143,6 +143,8 @@ size_t a5x_expand_lds(uint32_t table_bytes, int kind, uint32_t waves);
 hipError_t a5x_launch_expand(const A5xExpLaunch& L, int kind, hipStream_t st);
 hipError_t a5x_launch_locate(const A5xExpLaunch& L, const uint64_t* cands, uint32_t n, uint64_t* out_bytes,
                              hipStream_t st);
+hipError_t a5x_launch_word_of(const uint64_t* cand_off, uint64_t nw, const uint64_t* g, uint32_t nt, uint64_t* word,
+                              uint64_t* ciw, hipStream_t st);
 hipError_t a5x_launch_digest(const uint8_t* out, const uint64_t* byte_off, uint64_t out_base, uint64_t nw,
                              uint64_t* dig, hipStream_t st);
 

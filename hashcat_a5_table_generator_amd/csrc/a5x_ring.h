@@ -74,6 +74,20 @@ __device__ __forceinline__ void fx7_put(const uint4 e, uint32_t& P, uint32_t& si
       if (t > 16u) put(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
     }
   }
+#elif defined(FX_WRS)
+  // (timing variants, wrong output: 1 slots >= 1 plain writes of the lanes reaching them,
+  // 2 slots >= 1 plain writes of every lane, 3 every slot a plain write)
+  if (FX_WRS == 3) fx6_st(base, __builtin_amdgcn_perm(e.x, 0u, sel));
+  else put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
+  if (FX_WRS != 1 || t > 4u) fx6_st(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
+  if (__builtin_amdgcn_ballot_w64(t > 8u)) {
+    if (FX_WRS != 1 || t > 8u) fx6_st(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
+    if (__builtin_amdgcn_ballot_w64(t > 12u)) {
+      if (FX_WRS != 1 || t > 12u) fx6_st(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
+      if (__builtin_amdgcn_ballot_w64(t > 16u))
+        if (FX_WRS != 1 || t > 16u) fx6_st(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
+    }
+  }
 #else
   put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
   put(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));

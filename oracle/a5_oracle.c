@@ -904,3 +904,211 @@ A5O_EXPORT int a5o_run_pipeline(const a5o_table *t, const uint8_t *words, const 
     free(j);
     return rc;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Digest baseline: the reference expansion with   */
+/* every candidate hashed where it is produced and probed in a target set --   */
+/* the CPU shape of `a5_generator ... | hashcat -m 0/1000` without the pipe.   */
+/* MD5 = RFC 1321 (Go crypto/md5); NTLM = RFC 1320 MD4 over Go's               */
+/* utf16.Encode([]rune(s)) as UTF-16LE (invalid UTF-8 byte -> U+FFFD).         */
+/* ------------------------------------------------------------------------ */
+#define ROTL32(x, s) (((x) << (s)) | ((x) >> (32 - (s))))
+
+static void md5_block(uint32_t h[4], const uint32_t M[16]) {
+    static const uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+    static const int S[64] = {7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22,
+                              5, 9, 14, 20, 5, 9, 14, 20, 5, 9, 14, 20, 5, 9, 14, 20,
+                              4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23,
+                              6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21};
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+    for (int i = 0; i < 64; i++) {
+        uint32_t f; int g;
+        if (i < 16) { f = (b & c) | (~b & d); g = i; }
+        else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) & 15; }
+        else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) & 15; }
+        else { f = c ^ (b | ~d); g = (7 * i) & 15; }
+        uint32_t t = d; d = c; c = b;
+        uint32_t x = a + f + K[i] + M[g];
+        b = b + ROTL32(x, S[i]);
+        a = t;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+}
+
+static void md4_block(uint32_t h[4], const uint32_t X[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+#define F4(x, y, z) (((x) & (y)) | (~(x) & (z)))
+#define G4(x, y, z) (((x) & (y)) | ((x) & (z)) | ((y) & (z)))
+#define H4(x, y, z) ((x) ^ (y) ^ (z))
+    static const int r2[16] = {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15};
+    static const int r3[16] = {0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15};
+    static const int s1[4] = {3, 7, 11, 19}, s2[4] = {3, 5, 9, 13}, s3[4] = {3, 9, 11, 15};
+    for (int i = 0; i < 16; i++) {
+        uint32_t t;
+        switch (i & 3) {
+        case 0: t = a + F4(b, c, d) + X[i]; a = ROTL32(t, s1[0]); break;
+        case 1: t = d + F4(a, b, c) + X[i]; d = ROTL32(t, s1[1]); break;
+        case 2: t = c + F4(d, a, b) + X[i]; c = ROTL32(t, s1[2]); break;
+        default: t = b + F4(c, d, a) + X[i]; b = ROTL32(t, s1[3]); break;
+        }
+    }
+    for (int i = 0; i < 16; i++) {
+        uint32_t t, k = (uint32_t)r2[i];
+        switch (i & 3) {
+        case 0: t = a + G4(b, c, d) + X[k] + 0x5A827999u; a = ROTL32(t, s2[0]); break;
+        case 1: t = d + G4(a, b, c) + X[k] + 0x5A827999u; d = ROTL32(t, s2[1]); break;
+        case 2: t = c + G4(d, a, b) + X[k] + 0x5A827999u; c = ROTL32(t, s2[2]); break;
+        default: t = b + G4(c, d, a) + X[k] + 0x5A827999u; b = ROTL32(t, s2[3]); break;
+        }
+    }
+    for (int i = 0; i < 16; i++) {
+        uint32_t t, k = (uint32_t)r3[i];
+        switch (i & 3) {
+        case 0: t = a + H4(b, c, d) + X[k] + 0x6ED9EBA1u; a = ROTL32(t, s3[0]); break;
+        case 1: t = d + H4(a, b, c) + X[k] + 0x6ED9EBA1u; d = ROTL32(t, s3[1]); break;
+        case 2: t = c + H4(d, a, b) + X[k] + 0x6ED9EBA1u; c = ROTL32(t, s3[2]); break;
+        default: t = b + H4(c, d, a) + X[k] + 0x6ED9EBA1u; b = ROTL32(t, s3[3]); break;
+        }
+    }
+#undef F4
+#undef G4
+#undef H4
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+}
+
+/* Merkle-Damgard over msg (little-endian words, 0x80 pad, 64-bit bit length): MD5 or MD4 */
+static __attribute__((noinline)) void md_message(int md5, const uint8_t *msg, size_t n, uint8_t out[16]) {
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    uint32_t M[16];
+    const size_t full = n / 64;
+    for (size_t b = 0; b < full; b++) {
+        memcpy(M, msg + 64 * b, 64);
+        if (md5) md5_block(h, M); else md4_block(h, M);
+    }
+    uint8_t tail[128];
+    memset(tail, 0, sizeof tail);
+    const size_t r = n - 64 * full;
+    memcpy(tail, msg + 64 * full, r);
+    tail[r] = 0x80;
+    const size_t tb = r < 56 ? 64 : 128;
+    const uint64_t bits = (uint64_t)n * 8;
+    memcpy(tail + tb - 8, &bits, 8);
+    for (size_t o = 0; o < tb; o += 64) {
+        memcpy(M, tail + o, 64);
+        if (md5) md5_block(h, M); else md4_block(h, M);
+    }
+    memcpy(out, h, 16);
+}
+
+/* Go utf16.Encode([]rune(s)) as UTF-16LE bytes; returns the byte count (out >= 4 n) */
+static size_t go_utf16le(const uint8_t *s, size_t n, uint8_t *out) {
+    size_t i = 0, o = 0;
+    while (i < n) {
+        int sz, r = decode_rune(s + i, n - i, &sz);
+        i += (size_t)sz;
+        if (r >= 0x10000) {
+            uint32_t v = (uint32_t)r - 0x10000u, hi = 0xD800u + (v >> 10), lo = 0xDC00u + (v & 0x3FFu);
+            out[o++] = (uint8_t)hi; out[o++] = (uint8_t)(hi >> 8); out[o++] = (uint8_t)lo; out[o++] = (uint8_t)(lo >> 8);
+        } else {
+            out[o++] = (uint8_t)r; out[o++] = (uint8_t)((unsigned)r >> 8);
+        }
+    }
+    return o;
+}
+
+/* algo 0: MD5(s); 1: NTLM(s) = MD4(UTF-16LE(s)) */
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wmaybe-uninitialized"  /* (stackbuf: written by go_utf16le first) */
+A5O_EXPORT int a5o_digest(int algo, const uint8_t *s, size_t n, uint8_t out[16]) {
+    if (algo == 0) { md_message(1, s, n, out); return A5O_OK; }
+    if (algo != 1) return A5O_E_ARG;
+    uint8_t stackbuf[1024];
+    uint8_t *u = 4 * n <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc(4 * n + 1);
+    if (!u) return A5O_E_NOMEM;
+    size_t m = go_utf16le(s, n, u);
+    md_message(0, u, m, out);
+    if (u != stackbuf) free(u);
+    return A5O_OK;
+}
+#pragma GCC diagnostic pop
+
+/* target set: open addressing on the first 8 digest bytes */
+typedef struct {
+    const a5o_table *t; const uint8_t *words; const uint64_t *off; size_t nw;
+    int mode, mn, mx, algo;
+    const uint8_t *tg; const int64_t *slot; size_t smask;
+    _Atomic size_t next; _Atomic int err;
+    _Atomic uint64_t cands, hits;
+} dg_job;
+typedef struct { dg_job *j; uint64_t cands, hits; } dg_local;
+
+static void emit_hash_probe(void *u, const uint8_t *s, size_t n) {
+    dg_local *L = (dg_local *)u;
+    uint8_t d[16];
+    a5o_digest(L->j->algo, s, n, d);
+    uint64_t k; memcpy(&k, d, 8);
+    for (size_t i = fmix64(k) & L->j->smask;; i = (i + 1) & L->j->smask) {
+        int64_t x = L->j->slot[i];
+        if (x < 0) break;
+        if (!memcmp(L->j->tg + 16 * (size_t)x, d, 16)) { L->hits++; break; }
+    }
+    L->cands++;
+}
+
+static void *dg_worker(void *arg) {
+    dg_job *j = (dg_job *)arg;
+    dg_local L = {j, 0, 0};
+    for (;;) {
+        size_t i = atomic_fetch_add(&j->next, 16);
+        if (i >= j->nw) break;
+        size_t e = i + 16 < j->nw ? i + 16 : j->nw;
+        for (; i < e; i++) {
+            int rc = a5o_expand_word(j->t, j->words + j->off[i], (size_t)(j->off[i + 1] - j->off[i]), j->mode, j->mn,
+                                     j->mx, emit_hash_probe, &L);
+            if (rc) atomic_store(&j->err, rc);
+        }
+    }
+    atomic_fetch_add(&j->cands, L.cands);
+    atomic_fetch_add(&j->hits, L.hits);
+    return NULL;
+}
+
+/* nthreads workers (one word at a time, like the reference's goroutines), each candidate
+ * digested and probed in a hash set of the nt 16-B targets; returns candidates and hits */
+A5O_EXPORT int a5o_digest_run(const a5o_table *t, const uint8_t *words, const uint64_t *off, size_t nw, int mode,
+                              int mn, int mx, int algo, const uint8_t *targets, size_t nt, int nthreads,
+                              uint64_t *out_cands, uint64_t *out_hits) {
+    if (algo != 0 && algo != 1) return A5O_E_ARG;
+    size_t ns = 16;
+    while (ns < 2 * nt + 16) ns <<= 1;
+    int64_t *slot = (int64_t *)malloc(ns * sizeof(int64_t));
+    if (!slot) return A5O_E_NOMEM;
+    for (size_t i = 0; i < ns; i++) slot[i] = -1;
+    for (size_t x = 0; x < nt; x++) {
+        uint64_t k; memcpy(&k, targets + 16 * x, 8);
+        size_t i = fmix64(k) & (ns - 1);
+        while (slot[i] >= 0) i = (i + 1) & (ns - 1);
+        slot[i] = (int64_t)x;
+    }
+    dg_job j;
+    j.t = t; j.words = words; j.off = off; j.nw = nw; j.mode = mode; j.mn = mn; j.mx = mx; j.algo = algo;
+    j.tg = targets; j.slot = slot; j.smask = ns - 1;
+    atomic_init(&j.next, 0); atomic_init(&j.err, 0); atomic_init(&j.cands, 0); atomic_init(&j.hits, 0);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, dg_worker, &j);
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    free(slot);
+    *out_cands = atomic_load(&j.cands);
+    *out_hits = atomic_load(&j.hits);
+    return atomic_load(&j.err);
+}

@@ -55,6 +55,10 @@ def lib():
         L.a5o_run_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        _u64p, _u64p]
+        L.a5o_digest.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+        L.a5o_digest_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_int, _u64p, _u64p]
         L.a5o_cand_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.a5o_cand_hash.restype = ctypes.c_uint64
         _lib = L
@@ -145,6 +149,27 @@ class CTable:
         if rc:
             raise RuntimeError(f"oracle pipeline rc={rc}")
         return c.value, b.value
+
+
+    def digest_run(self, words: np.ndarray, offs: np.ndarray, mode: int, mn: int, mx: int, algo: int,
+                   targets: np.ndarray, nthreads: int) -> Tuple[int, int]:
+        """The reference expansion with every candidate digested (algo 0 MD5, 1 NTLM) and probed
+        in the set of 16-B targets (n, 16) u8 by nthreads workers; returns (candidates, hits)."""
+        t = np.ascontiguousarray(targets, dtype=np.uint8).reshape(-1, 16)
+        c = ctypes.c_uint64(); h = ctypes.c_uint64()
+        rc = lib().a5o_digest_run(self.h, words.ctypes.data, offs.ctypes.data, len(offs) - 1, mode, mn, mx, algo,
+                                  t.ctypes.data, len(t), nthreads, ctypes.byref(c), ctypes.byref(h))
+        if rc:
+            raise RuntimeError(f"oracle digest run rc={rc}")
+        return c.value, h.value
+
+
+def digest(algo: int, b: bytes) -> bytes:
+    """MD5 (algo 0) or NTLM (algo 1, MD4 of Go's UTF-16LE) in C (oracle/a5_oracle.c)."""
+    out = ctypes.create_string_buffer(16)
+    if lib().a5o_digest(algo, b, len(b), out):
+        raise ValueError(algo)
+    return out.raw
 
 
 def cand_hash(b: bytes) -> int:

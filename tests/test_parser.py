@@ -93,3 +93,30 @@ def test_split_words(data):
     words, offs = split_words(data)
     got = [bytes(words[int(offs[i]):int(offs[i + 1])]) for i in range(len(offs) - 1)]
     assert got == o.read_words(data)
+
+
+def _plan_rc(nkeys):
+    """Compile a table of nkeys 2-byte keys (one 2-byte value each) on a host-only context."""
+    import ctypes
+    from hashcat_a5_table_generator_amd import _lib
+    L = _lib.load()
+    h = ctypes.c_void_p()
+    assert L.a5x_create(-1, ctypes.byref(h)) == 0
+    keys = [bytes([97 + i // 26, 97 + i % 26]) for i in range(nkeys)]
+    txt = b"".join(k + b"=" + k.upper() + b"\n" for k in keys)
+    assert L.a5x_parse_table(h, txt, len(txt)) == 0
+    info = np.zeros(4, dtype=np.uint64)
+    rc = L.a5x_debug_plan_word(h, b"ab" + b"\0" * 16, 2, 0, 15, None, 0, info.ctypes.data)
+    err = L.a5x_last_error(h)
+    L.a5x_destroy(h)
+    return rc, err
+
+
+def test_device_table_size_cap():
+    """the compiled device table (keys, choices, the lookup arrays, blob) is staged
+    into LDS per workgroup and capped at 32 KiB (A5X_TABLE_LDS_MAX): 409 two-byte keys with
+    one two-byte value each fit, 410 are refused with A5X_E_UNSUPPORTED naming the size (no
+    silent fallback); every shipped table and the czech+german merge are far below."""
+    assert _plan_rc(409)[0] == 0
+    rc, err = _plan_rc(410)
+    assert rc == -9 and b"LDS staging max 32768" in err
