@@ -138,14 +138,14 @@ def shard_for_rank(args, D, ctx, intra_word=True):
     exactly on the device (a5x_split_device / a5x_locate_device), so a word larger than a
     rank's share is cut inside (dist.candidate_split); else word boundaries
     (dist.distributed_split, a5x_partition semantics: the fused-digest path).
-    Returns (tables, data, offs, (w0, w1), (cand_begin, cand_count)) -- candidates of the
-    local batch [w0, w1); (0, None) = all of them."""
+    Returns (tables, data, offs, (w0, w1), (cand_begin, cand_count, shard_bytes)) -- candidates
+    of the local batch [w0, w1); (0, None, None) = all of them."""
     from hashcat_a5_table_generator_amd import DeviceBuffer, dist as hd, synth
     n_total = args.words * D.world
     b0, b1 = hd.block_bounds(n_total, D.world, D.rank)
     tables, (bd, bo) = synth.global_words(args.workload, b0, b1, seed=SEED)
     if D.dist is None:
-        return tables, bd, bo, (0, n_total), (0, None)
+        return tables, bd, bo, (0, n_total), (0, None, None)
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw, do = DeviceBuffer.from_array(ctx, bd), DeviceBuffer.from_array(ctx, bo)
     lp = DeviceBuffer(ctx, (b1 - b0 + 1) * 8)
@@ -158,12 +158,12 @@ def shard_for_rank(args, D, ctx, intra_word=True):
         w0, w1, c0, ncand, _, nbytes = hd.shard_of(split, D.rank)
     else:
         ws = hd.distributed_split(D.dist, lp.to_array(np.uint64, count=b1 - b0 + 1), b0, n_total, D.world, D.backend)
-        w0, w1, c0, ncand = int(ws[D.rank]), int(ws[D.rank + 1]), 0, None
+        w0, w1, c0, ncand, nbytes = int(ws[D.rank]), int(ws[D.rank + 1]), 0, None, None
     for b in (dw, do, lp):
         b.free()
     ctx.clear_table()
     _, (data, offs) = synth.global_words(args.workload, w0, w1, seed=SEED)
-    return tables, data, offs, (w0, w1), (c0, ncand)
+    return tables, data, offs, (w0, w1), (c0, ncand, nbytes)
 
 
 def kernel_src_sha() -> str:
@@ -347,7 +347,7 @@ def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
     return r
 
 
-def plant_targets(args, D, ctx, data, offs, w0, algo):
+def plant_targets(args, D, ctx, data, offs, w0, algo, skip_first=False):
     """Targets of the C5 lookup: one candidate of each sampled word of the GLOBAL list
     (every stride-th global word index, candidate chosen by a generator seeded with that
     index, so the planted set does not depend on how the list is sharded), digested on
@@ -358,7 +358,7 @@ def plant_targets(args, D, ctx, data, offs, w0, algo):
     from hashcat_a5_table_generator_amd import DeviceBuffer, dist as hd
     n = len(offs) - 1
     stride = max(1, (args.words * D.world) // 1000)
-    first = (w0 + stride - 1) // stride * stride
+    first = (w0 + (1 if skip_first else 0) + stride - 1) // stride * stride
     sample = list(range(first - w0, n, stride))
     sw = [bytes(data[int(offs[i]):int(offs[i + 1])]) for i in sample]
     cands = ctx.expand_words(sw, args.mode, args.min, args.max)
@@ -400,22 +400,32 @@ def run_digest(args, D):
     from hashcat_a5_table_generator_amd import ALGO_MD5, ALGO_NTLM, Context, DeviceBuffer, dist as hd, synth
     algo = ALGO_MD5 if args.digest == "md5" else ALGO_NTLM
     ctx = Context(D.device)
-    # (word-granular shards: a5x_expand_digest_device takes whole batches)
-    tables, data, offs, (w0, w1), _ = shard_for_rank(args, D, ctx, intra_word=False)
+    # (shards cut inside words at candidate split points, SURVEY 8(e) e1: each rank digests
+    # the candidates [cb, ce) of its local word range, a5x_expand_digest_range_device)
+    tables, data, offs, (w0, w1), (cb, ncand, nbytes) = shard_for_rank(args, D, ctx)
     n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)
     do = DeviceBuffer.from_array(ctx, offs)
-    tc, tb = ctx.keyspace_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max)
-    planted, targets = plant_targets(args, D, ctx, data, offs, w0, algo)
+    tc_all, tb_all = ctx.keyspace_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max)
+    bytes_per_rank = [tb_all if nbytes is None else nbytes] if D.dist is None else [
+        int(x) for x in hd.allgather_u64(D.dist, [tb_all if nbytes is None else nbytes], D.backend)[:, 0]]
+    ce = tc_all if ncand is None else cb + ncand
+    tc = ce - cb
+    rng = None if (cb, ce) == (0, tc_all) else (cb, ce)
+    # (a word cut between two ranks is planted by the rank holding its start)
+    planted, targets = plant_targets(args, D, ctx, data, offs, w0, algo, skip_first=cb > 0)
     ctx.set_targets(algo, targets)
     scratch = int(args.scratch_gb * (1 << 30))
-    log(f"rank {D.rank}: words [{w0}, {w1}) -> {tc} candidates, {tb / 1e9:.2f} GB; {len(targets)} targets "
-        f"({len(planted)} planted over all ranks)")
+    log(f"rank {D.rank}: words [{w0}, {w1}) candidates [{cb}, {ce}) of the local batch -> {tc} candidates; "
+        f"{len(targets)} targets ({len(planted)} planted over all ranks)")
 
     def step():
+        if rng is None:
+            return ctx.expand_digest_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max, scratch_bytes=scratch,
+                                            hit_cap=1 << 20)
         return ctx.expand_digest_device(dw.ptr, do.ptr, n, args.mode, args.min, args.max, scratch_bytes=scratch,
-                                        hit_cap=1 << 20)
+                                        hit_cap=1 << 20, cand_begin=rng[0], cand_end=rng[1])
 
     for _ in range(args.warmup):
         step()
@@ -449,8 +459,8 @@ def run_digest(args, D):
             "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8/u32", "data": "synthetic",
             "config": {"workload": f"{args.workload}: {desc} + fused {args.digest.upper()} lookup (configs[4])",
-                       "tables": tables, "words_per_gpu": n, "candidates_per_gpu_step": tc, "bytes_per_gpu_step": tb,
-                       "targets": len(targets), "planted": len(planted), "hits_all_ranks": hits_all,
+                       "tables": tables, "words_per_gpu": n, "candidates_per_gpu_step": tc,
+                       "candidate_range": [cb, ce], "bytes_per_rank": bytes_per_rank, "targets": len(targets), "planted": len(planted), "hits_all_ranks": hits_all,
                        "hits_gathered_on_rank0": len(gathered),
                        "mode": MODE_NAMES[args.mode], "table_min": args.min, "table_max": args.max,
                        "scratch_bytes": scratch,
@@ -693,7 +703,7 @@ def main():
 
     ctx = Context(D.device)
     # (--verify checks whole words against the oracle on every rank: word-boundary shards)
-    tables, data, offs, (w0, w1), (cb, ncand) = shard_for_rank(args, D, ctx, intra_word=not args.verify)
+    tables, data, offs, (w0, w1), (cb, ncand, _) = shard_for_rank(args, D, ctx, intra_word=not args.verify)
     n = len(offs) - 1
     ctx.load_tables([os.path.join(ROOT, "tests", "golden", "tables", t + ".table") for t in tables])
     dw = DeviceBuffer.from_array(ctx, data)

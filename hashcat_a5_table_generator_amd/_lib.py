@@ -28,7 +28,8 @@ EXPORTS = (
     "a5x_split_words", "a5x_keyspace", "a5x_expand", "a5x_expand_device", "a5x_keyspace_device",
     "a5x_digest_device", "a5x_partition", "a5x_dev_alloc", "a5x_dev_free", "a5x_memcpy_h2d",
     "a5x_memcpy_d2h", "a5x_synchronize", "a5x_debug_stamps", "a5x_debug_plan_word",
-    "a5x_set_targets", "a5x_expand_digest", "a5x_expand_digest_device", "a5x_digest_lines_device",
+    "a5x_set_targets", "a5x_expand_digest", "a5x_expand_digest_device", "a5x_expand_digest_range_device",
+    "a5x_digest_lines_device",
     "a5x_format_plain", "a5x_format_hits", "a5x_locate_device", "a5x_split_device",
     "a5x_stream_reserve",
 )
@@ -108,6 +109,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     L.a5x_expand_digest.argtypes = [vp, vp, vp, u64, i, i, i, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(Stats)]
     L.a5x_expand_digest_device.argtypes = [vp, vp, vp, u64, i, i, i, u64, vp, u64, ctypes.POINTER(u64),
                                            ctypes.POINTER(Stats), vp]
+    L.a5x_expand_digest_range_device.argtypes = [vp, vp, vp, u64, i, i, i, u64, u64, u64, vp, u64, ctypes.POINTER(u64),
+                                                 ctypes.POINTER(Stats), vp]
     L.a5x_digest_lines_device.argtypes = [vp, i, vp, u64, vp, u64, ctypes.POINTER(u64), vp]
     L.a5x_format_plain.argtypes = [ctypes.c_char_p, sz, vp, sz, ctypes.POINTER(sz)]
     L.a5x_format_hits.argtypes = [vp, vp, vp, u64, i, i, i, vp, u64, SINK, vp]

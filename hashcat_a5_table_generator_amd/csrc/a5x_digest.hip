@@ -252,10 +252,12 @@ __global__ void __launch_bounds__(64) k_hits_resolve(A5xHitRaw* hits, u32 n, con
 // Hybrid fused digest: the candidate-bearing words the fused kernel leaves out (not
 // FAST: slow / BIG / pass-G words) are listed, then gathered into a compact sub-batch
 // that the two-pass path digests.
-__global__ void __launch_bounds__(256) k_nonfast_list(const u32* flags, const u64* cand_off, u64 nw, u32* list,
-                                                       u32* n) {
+__global__ void __launch_bounds__(256) k_nonfast_list(const u32* flags, const u64* cand_off, u64 nw, u64 cb, u64 ce,
+                                                       u32* list, u32* n) {
+  // (words with candidates inside [cb, ce))
   for (u64 w = (u64)blockIdx.x * 256 + threadIdx.x; w < nw; w += (u64)gridDim.x * 256)
-    if (cand_off[w + 1] > cand_off[w] && !(flags[w] & A5X_WF_FAST)) list[atomicAdd(n, 1u)] = (u32)w;
+    if (cand_off[w + 1] > cand_off[w] && cand_off[w] < ce && cand_off[w + 1] > cb && !(flags[w] & A5X_WF_FAST))
+      list[atomicAdd(n, 1u)] = (u32)w;
 }
 
 __global__ void __launch_bounds__(256) k_gather_lens(const u64* woff, const u32* idx, u32 m, u64* lens) {
@@ -272,11 +274,12 @@ __global__ void __launch_bounds__(64) k_gather_words(const uint8_t* words, const
 
 }  // namespace
 
-hipError_t a5x_launch_nonfast_list(const uint32_t* flags, const uint64_t* cand_off, uint64_t nw, uint32_t* list,
-                                   uint32_t* n, hipStream_t st) {
+hipError_t a5x_launch_nonfast_list(const uint32_t* flags, const uint64_t* cand_off, uint64_t nw, uint64_t cb,
+                                   uint64_t ce, uint32_t* list, uint32_t* n, hipStream_t st) {
   if (!nw) return hipSuccess;
   const u64 b = (nw + 255) / 256;
-  hipLaunchKernelGGL(k_nonfast_list, dim3((u32)(b < 16384 ? b : 16384)), dim3(256), 0, st, flags, cand_off, nw, list, n);
+  hipLaunchKernelGGL(k_nonfast_list, dim3((u32)(b < 16384 ? b : 16384)), dim3(256), 0, st, flags, cand_off, nw, cb, ce,
+                     list, n);
   return hipGetLastError();
 }
 

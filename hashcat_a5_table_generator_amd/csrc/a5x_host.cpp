@@ -1046,19 +1046,28 @@ Range range_of(const Job& J, uint64_t cb, uint64_t ce, const uint64_t* lb, const
 
 // Cut [0, total) into ranges of at most cap output bytes: candidate boundaries spaced for
 // ~3/4 cap each, located in one call; ranges that still exceed cap are halved.
-int plan_ranges(a5x_ctx* c, const Job& J, uint64_t cap, std::vector<Range>& out) {
+// (cb, ce: only the candidates [cb, ce) of the batch, cut into ranges the same way)
+int plan_ranges(a5x_ctx* c, const Job& J, uint64_t cap, std::vector<Range>& out, uint64_t cb = 0,
+                uint64_t ce = ~0ull) {
   out.clear();
   const uint64_t T = J.B.total_cands, TB = J.B.total_bytes;
-  if (!T) return A5X_OK;
-  if (TB <= cap) {
-    Range R{0, T, 0, TB, 0, J.mode != A5X_MODE_DEFAULT ? c->m_items : 0};
-    out.push_back(R);
+  ce = std::min(ce, T);
+  if (cb >= ce) return A5X_OK;
+  int rc;
+  uint64_t RB = TB;  // the bytes of [cb, ce)
+  std::vector<uint64_t> ends;
+  if (cb != 0 || ce != T) {
+    if ((rc = job_locate(c, J, {cb, ce}, ends))) return rc;
+    RB = ends[3] - ends[0];
+  }
+  if (RB <= cap) {
+    if (cb == 0 && ce == T) out.push_back(Range{0, T, 0, TB, 0, J.mode != A5X_MODE_DEFAULT ? c->m_items : 0});
+    else out.push_back(range_of(J, cb, ce, &ends[0], &ends[3]));
     return A5X_OK;
   }
-  const uint64_t K = std::max<uint64_t>(2, (TB + cap * 3 / 4 - 1) / std::max<uint64_t>(1, cap * 3 / 4));
+  const uint64_t K = std::max<uint64_t>(2, (RB + cap * 3 / 4 - 1) / std::max<uint64_t>(1, cap * 3 / 4));
   std::vector<uint64_t> q(K + 1), res;
-  for (uint64_t k = 0; k <= K; k++) q[k] = (uint64_t)((unsigned __int128)T * k / K);
-  int rc;
+  for (uint64_t k = 0; k <= K; k++) q[k] = cb + (uint64_t)((unsigned __int128)(ce - cb) * k / K);
   if ((rc = job_locate(c, J, q, res))) return rc;
   std::vector<Range> work;
   for (uint64_t k = 0; k < K; k++)
@@ -1240,16 +1249,43 @@ static_assert(sizeof(a5x_hit) == sizeof(A5xHitRaw), "resolved device hits are co
 // a5x_expand_digest_device.  allow_fused: default-mode batches take the fused kernel
 // (the hybrid's sub-batch of non-FAST words passes false: those words are exactly the
 // ones the fused kernel skips).
+// The item range [*i0, *i1) of the -r / -s engines holding candidates [cb, ce) (ce <= the
+// batch's count, cb < ce): the words of cb and ce - 1 from k_word_of, their first items.
+int mode_item_bounds(a5x_ctx* c, const Job& J, uint64_t cb, uint64_t ce, uint64_t* i0, uint64_t* i1) {
+  int rc;
+  if ((rc = grow(c, c->loc_q, 2)) || (rc = grow(c, c->loc_r, 4))) return rc;
+  const uint64_t q[2] = {cb, ce - 1};
+  HIPCHK(c, hipMemcpyAsync(c->loc_q.p, q, 16, hipMemcpyHostToDevice, J.st));
+  HIPCHK(c, a5x_launch_word_of(J.B.cand_off, J.nw, c->loc_q.p, 2, c->loc_r.p, c->loc_r.p + 2, J.st));
+  uint64_t wc[4], so[2];
+  HIPCHK(c, hipMemcpyAsync(wc, c->loc_r.p, 32, hipMemcpyDeviceToHost, J.st));
+  HIPCHK(c, hipStreamSynchronize(J.st));
+  for (int k = 0; k < 2; k++) {
+    if (wc[k] >= J.nw) return fail(c, A5X_E_ARG, "candidate %llu past the batch", (unsigned long long)q[k]);
+    HIPCHK(c, hipMemcpyAsync(&so[k], c->m_seg_off.p + wc[k], 8, hipMemcpyDeviceToHost, J.st));
+  }
+  HIPCHK(c, hipStreamSynchronize(J.st));
+  *i0 = so[0] + wc[2] / c->mseg;
+  *i1 = so[1] + wc[3] / c->mseg + 1;
+  return A5X_OK;
+}
+
+// Fused (or two-pass) expansion + digest + lookup of the batch's candidates [rb, re)
+// (clipped to the batch; [0, ~0) = all): hits as (word, candidate in word).
 int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode, int mn, int mx,
-                  uint64_t scratch_bytes, a5x_hit* hits, uint64_t hit_cap, uint64_t* n_hits, a5x_stats* stats,
-                  hipStream_t st, bool allow_fused) {
+                  uint64_t rb, uint64_t re, uint64_t scratch_bytes, a5x_hit* hits, uint64_t hit_cap,
+                  uint64_t* n_hits, a5x_stats* stats, hipStream_t st, bool allow_fused, uint64_t trim = 0) {
   int rc;
   Job J;
   job_open(c, J, d_words, d_woff, nw, mode, mn, mx, st);
   J.lengths = mode == A5X_MODE_DEFAULT || !allow_fused;  // the fused -r / -s digest needs no layout
   if ((rc = grow(c, c->dg_cand_off, nw + 1)) || (rc = grow(c, c->dg_byte_off, nw + 1))) return rc;
   if ((rc = job_prepare(c, J, c->dg_cand_off.p, c->dg_byte_off.p, true))) return rc;
-  const uint64_t tc = J.B.total_cands, tb = J.B.total_bytes;
+  const uint64_t tc_all = J.B.total_cands, tb = J.B.total_bytes;
+  re = std::min(re, tc_all - std::min(trim, tc_all));  // (trim: candidates dropped at the end)
+  rb = std::min(rb, re);
+  const bool whole = rb == 0 && re == tc_all;
+  const uint64_t tc = re - rb;  // the candidates this call digests
   // Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm hash each FAST
   // word's candidates in the LDS ring where they are built -- no HBM scratch, no second
   // pass, hits already (word, candidate).  The other candidate-bearing words (slow / BIG
@@ -1262,23 +1298,27 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
     if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
     uint64_t nh = 0;
     float ms = 0;
+    uint64_t it0 = 0, it1 = c->m_items;  // the items holding [rb, re)
+    if (!whole && tc && (rc = mode_item_bounds(c, J, rb, re, &it0, &it1))) return rc;
     for (;;) {
       A5xModeLaunch M = mode_launch(c, J.w, J.wo, J.nw, J.mode, J.mn, J.mx, J.B.rfast);
       const A5xDigLaunch D = dig_launch(c);
       M.cand_off = J.B.cand_off;
-      M.item_begin = 0;
-      M.item_end = c->m_items;
+      M.item_begin = it0;
+      M.item_end = tc ? it1 : it0;
+      M.cand_begin = rb;
+      M.cand_end = re;
       M.dg_algo = c->t_algo;
       M.dg_bitmap = D.bitmap; M.dg_bm_mask = D.bm_mask; M.dg_has_zero = D.has_zero_target;
       M.dg_table = D.table; M.dg_tmask = D.tmask;
       M.dg_hits = c->dg_hits.p; M.dg_hit_cap = (uint32_t)dev_hits; M.dg_nhits = c->d_scalars + 8;
       HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
       HIPCHK(c, hipEventRecord(c->ev[1], J.st));
-      if (J.B.nmode) HIPCHK(c, a5x_launch_mode_items(M, 2, J.st));
+      if (J.B.nmode && tc) HIPCHK(c, a5x_launch_mode_items(M, 2, J.st));
       if (J.B.rfast && tc) {  // -r FAST words: hashed in k_expand_fast_md5 / _ntlm's ring
         A5xExpLaunch E = exp_launch_mode(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
-        E.cand_begin = 0;
-        E.cand_end = tc;
+        E.cand_begin = rb;
+        E.cand_end = re;
         E.dg_bitmap = D.bitmap; E.dg_bm_mask = D.bm_mask; E.dg_has_zero = D.has_zero_target;
         E.dg_table = D.table; E.dg_tmask = D.tmask;
         E.dg_hits = c->dg_hits.p; E.dg_hit_cap = (uint32_t)dev_hits; E.dg_nhits = c->d_scalars + 8;
@@ -1325,8 +1365,8 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
     for (;;) {
       A5xExpLaunch E = exp_launch(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
       const A5xDigLaunch D = dig_launch(c);
-      E.cand_begin = 0;
-      E.cand_end = tc;
+      E.cand_begin = rb;
+      E.cand_end = re;
       E.dg_bitmap = D.bitmap; E.dg_bm_mask = D.bm_mask; E.dg_has_zero = D.has_zero_target;
       E.dg_table = D.table; E.dg_tmask = D.tmask;
       E.dg_hits = c->dg_hits.p; E.dg_hit_cap = (uint32_t)dev_hits; E.dg_nhits = c->d_scalars + 8;
@@ -1358,7 +1398,7 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
       // m, itself bounded by nw) and the caller's hits[take, take + got) with got <= room.
       if ((rc = grow(c, c->hy_list, std::max<uint64_t>(1, nw)))) return rc;
       HIPCHK(c, hipMemsetAsync(c->d_scalars + 9, 0, 4, J.st));
-      HIPCHK(c, a5x_launch_nonfast_list(c->flags.p, J.B.cand_off, nw, c->hy_list.p, c->d_scalars + 9, J.st));
+      HIPCHK(c, a5x_launch_nonfast_list(c->flags.p, J.B.cand_off, nw, rb, re, c->hy_list.p, c->d_scalars + 9, J.st));
       HIPCHK(c, hipMemcpyAsync(c->h_scalars + 9, c->d_scalars + 9, 4, hipMemcpyDeviceToHost, J.st));
       HIPCHK(c, hipStreamSynchronize(J.st));
       const uint32_t m = c->h_scalars[9];
@@ -1380,13 +1420,24 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
       HIPCHK(c, hipMemcpyAsync(c->hy_off.p, off.data(), ((size_t)m + 1) * 8, hipMemcpyHostToDevice, J.st));
       HIPCHK(c, hipMemsetAsync(c->hy_words.p, 0, off[m] + 16, J.st));
       HIPCHK(c, a5x_launch_gather_words(J.w, J.wo, c->hy_list.p, m, nullptr, c->hy_off.p, c->hy_words.p, J.st));
-      // their candidates through the two-pass path; hit word indices mapped back to the batch
+      // their candidates through the two-pass path; hit word indices mapped back to the batch.
+      // A word cut by [rb, re) (the first / last listed): only its part inside the range --
+      // the sub-batch range drops the candidates before rb and after re.
+      uint64_t sb = 0, se_cut = 0;
+      if (m && !whole) {
+        uint64_t c0 = 0, c1 = 0;
+        HIPCHK(c, hipMemcpyAsync(&c0, J.B.cand_off + idx[0], 8, hipMemcpyDeviceToHost, J.st));
+        HIPCHK(c, hipMemcpyAsync(&c1, J.B.cand_off + idx[m - 1] + 1, 8, hipMemcpyDeviceToHost, J.st));
+        HIPCHK(c, hipStreamSynchronize(J.st));
+        sb = rb > c0 ? rb - c0 : 0;
+        se_cut = c1 > re ? c1 - re : 0;
+      }
       const uint64_t room = hit_cap > take ? hit_cap - take : 0;
       uint64_t nh2 = 0;
       a5x_stats st2;
       memset(&st2, 0, sizeof st2);
-      rc = expand_digest(c, c->hy_words.p, c->hy_off.p, m, mode, mn, mx, scratch_bytes, room ? hits + take : nullptr,
-                         room, &nh2, &st2, J.st, false);
+      rc = expand_digest(c, c->hy_words.p, c->hy_off.p, m, mode, mn, mx, sb, ~0ull, scratch_bytes,
+                         room ? hits + take : nullptr, room, &nh2, &st2, J.st, false, se_cut);
       if (rc && rc != A5X_E_CAPACITY) return rc;
       const uint64_t got = std::min(nh2, room);
       for (uint64_t i = take; i < take + got; i++) {
@@ -1417,7 +1468,7 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
   uint64_t cap = scratch_bytes ? scratch_bytes : ((uint64_t)2 << 30);
   cap = std::max<uint64_t>(4096, std::min<uint64_t>(cap, tb + 64));
   std::vector<Range> ranges;
-  if ((rc = plan_ranges(c, J, cap, ranges))) return rc;
+  if ((rc = plan_ranges(c, J, cap, ranges, rb, re))) return rc;
   if ((rc = grow(c, c->dg_scratch, cap + 64))) return rc;
   uint64_t dev_hits = std::max<uint64_t>(1024, std::min<uint64_t>(hit_cap, 1u << 20));
   if ((rc = grow(c, c->dg_hits, dev_hits))) return rc;
@@ -2156,8 +2207,22 @@ int a5x_expand_digest_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t*
   if ((rc = check_mode(c, mode))) return rc;
   HIPCHK(c, hipSetDevice(c->device));
   const bool fused = !getenv("A5X_NO_FUSED_DIGEST");
-  return expand_digest(c, d_words, d_woff, nw, mode, mn, mx, scratch_bytes, hits, hit_cap, n_hits, stats,
+  return expand_digest(c, d_words, d_woff, nw, mode, mn, mx, 0, ~0ull, scratch_bytes, hits, hit_cap, n_hits, stats,
                        stream ? (hipStream_t)stream : c->stream, fused);
+}
+
+int a5x_expand_digest_range_device(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uint64_t nw, int mode,
+                                   int mn, int mx, uint64_t cand_begin, uint64_t cand_end, uint64_t scratch_bytes,
+                                   a5x_hit* hits, uint64_t hit_cap, uint64_t* n_hits, a5x_stats* stats, void* stream) {
+  if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
+  if (!c || (nw && (!d_words || !d_woff)) || (hit_cap && !hits) || cand_end < cand_begin) return A5X_E_ARG;
+  if (c->t_algo < 0) return fail(c, A5X_E_ARG, "no target set (a5x_set_targets)");
+  int rc;
+  if ((rc = check_mode(c, mode))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool fused = !getenv("A5X_NO_FUSED_DIGEST");
+  return expand_digest(c, d_words, d_woff, nw, mode, mn, mx, cand_begin, cand_end, scratch_bytes, hits, hit_cap,
+                       n_hits, stats, stream ? (hipStream_t)stream : c->stream, fused);
 }
 
 int a5x_expand_digest(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,

@@ -250,8 +250,8 @@ uint64_t a5x_digest_blocks(uint64_t nbytes, int algo);  // 4 KiB (MD5) / 2 KiB (
 hipError_t a5x_launch_digest_stream(const A5xDigLaunch& L, int op, uint32_t grid, hipStream_t st);
 // hybrid fused digest: list the candidate-bearing non-FAST words (n: device counter),
 // then gather them into a sub-batch (lens != null: their lengths; else the bytes at sub_off)
-hipError_t a5x_launch_nonfast_list(const uint32_t* flags, const uint64_t* cand_off, uint64_t nw, uint32_t* list,
-                                   uint32_t* n, hipStream_t st);
+hipError_t a5x_launch_nonfast_list(const uint32_t* flags, const uint64_t* cand_off, uint64_t nw, uint64_t cb,
+                                   uint64_t ce, uint32_t* list, uint32_t* n, hipStream_t st);
 hipError_t a5x_launch_gather_words(const uint8_t* words, const uint64_t* woff, const uint32_t* idx, uint32_t m,
                                    uint64_t* lens, const uint64_t* sub_off, uint8_t* out, hipStream_t st);
 hipError_t a5x_launch_hits_resolve(A5xHitRaw* hits, uint32_t n, const uint64_t* blk_pre, uint64_t cand_base,

@@ -1660,7 +1660,7 @@ __global__ void __launch_bounds__(64) k_mode_count_g(A5xModeLaunch a) {
 // (g0 + t) is inside [cand_begin, cand_end).
 template <class SL>
 __device__ u64 m_run(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a, u64 t0, u32 nc, int op,
-                     u64 g0, u64 base, u32& err, u32 ntok = 0) {
+                     u64 g0, u64 base, u32& err, u32 ntok = 0, u64 cw0 = 0) {
   const u32 lane = m_lane();
   u64 run = 0;
   for (u32 k0 = 0; k0 < nc; k0 += 64) {
@@ -1685,7 +1685,8 @@ __device__ u64 m_run(SL& S, const MT& T, const MInfo& I, const A5xModeLaunch& a,
     }
     if (op == 2) {  // fused digest: the candidate where the builder left it (len - 1 bytes)
       const uint8_t* base = p ? p : S.word;
-      m_digest_probe(a, base, 0, len ? len - 1 : 0u, v && len > 0, g0, t0 + k);
+      const u64 g = cw0 + t0 + k;  // (op 2: g0 is the word; hashed only inside [cand_begin, cand_end))
+      m_digest_probe(a, base, 0, len ? len - 1 : 0u, v && len > 0 && g >= a.cand_begin && g < a.cand_end, g0, t0 + k);
       continue;
     }
     const u32 incl = m_incl_scan(len);
@@ -1737,8 +1738,11 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
     } else {
       u64 biasm = 0;
       const u32 np = (MF_ABL & 2) ? 0u : m_piece_setup(S, I, a.mode, ntok, biasm);
-      if (op == 2) {
-        m_fast_expand<SL, true>(S, I, a, t0, t0 + nc, 0, np, biasm, err, w);
+      if (op == 2) {  // (the item's candidates inside [cand_begin, cand_end))
+        const u64 rb = a.cand_begin > cw0 ? a.cand_begin - cw0 : 0;
+        const u64 re = a.cand_end - cw0 < t0 + nc ? a.cand_end - cw0 : t0 + nc;
+        const u64 tb = rb > t0 ? rb : t0;
+        if (a.cand_end > cw0 && tb < re) m_fast_expand<SL, true>(S, I, a, tb, re, 0, np, biasm, err, w);
         m_err(a.err, m_wave_or(err));
         return;
       }
@@ -1755,7 +1759,10 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
     ntok = a.mode != A5X_MODE_DEFAULT ? m_pos_setup(S, T, I, a.mode) : 0u;
     if (op == 2) {  // fused digest: positional items here, the others to the byte builder
       if constexpr (SL::RING) {
-        if (ntok) m_pos_digest(S, T, I, a, w, t0, t0 + nc, ntok, err);
+        const u64 rb = a.cand_begin > cw0 ? a.cand_begin - cw0 : 0;  // (inside [cand_begin, cand_end))
+        const u64 re = a.cand_end - cw0 < t0 + nc ? a.cand_end - cw0 : t0 + nc;
+        const u64 tb = rb > t0 ? rb : t0;
+        if (ntok && a.cand_end > cw0 && tb < re) m_pos_digest(S, T, I, a, w, tb, re, ntok, err);
         if (m_lane() == 0) a.item_fl[i] = ntok ? MI_POS : MI_BUILD;
       }
       m_err(a.err, m_wave_or(err));
@@ -1790,7 +1797,7 @@ __device__ void m_item(SL& S, const MT& T, const A5xModeLaunch& a, u64 i, int op
     if (op == 0 && m_lane() == 0) a.item_fl[i] = MI_BUILD;
   const u64 base = op == 1 ? a.seg_boff[i] : 0;
   // (op 2: m_run's g0 carries the word index for the hit records)
-  const u64 run = m_run(S, T, I, a, t0, nc, op, op == 2 ? w : cw0, base, err, ntok);
+  const u64 run = m_run(S, T, I, a, t0, nc, op, op == 2 ? w : cw0, base, err, ntok, cw0);
   if (op == 0 && m_lane() == 0) a.seg_bytes[i] = run;
   m_err(a.err, m_wave_or(err));
 }

@@ -233,7 +233,10 @@ class Context:
 
     def expand_digest_device(self, d_words: int, d_offs: int, n_words: int, mode: int = MODE_DEFAULT, mn: int = 0,
                              mx: int = 15, scratch_bytes: int = 0, hit_cap: int = 1 << 16,
-                             stream: int = 0) -> Tuple[List[Tuple[int, int, bytes]], dict]:
+                             stream: int = 0, cand_begin: int = 0,
+                             cand_end: Optional[int] = None) -> Tuple[List[Tuple[int, int, bytes]], dict]:
+        """Fused expansion + digest + target lookup of the batch's candidates (all of them,
+        or the global candidates [cand_begin, cand_end): a5x_expand_digest_range_device)."""
         # (one hit buffer per context, grown on demand: a fresh 1M-entry ctypes array costs
         # milliseconds of host zeroing per call)
         buf = getattr(self, "_hit_buf", None)
@@ -242,9 +245,14 @@ class Context:
         arr = buf
         nh = ctypes.c_uint64()
         st = Stats()
-        self._chk(self._L.a5x_expand_digest_device(self.h, d_words, d_offs, n_words, mode, mn, mx, scratch_bytes,
-                                                   arr, hit_cap, ctypes.byref(nh), ctypes.byref(st),
-                                                   stream or None))
+        if cand_begin == 0 and cand_end is None:
+            self._chk(self._L.a5x_expand_digest_device(self.h, d_words, d_offs, n_words, mode, mn, mx, scratch_bytes,
+                                                       arr, hit_cap, ctypes.byref(nh), ctypes.byref(st),
+                                                       stream or None))
+        else:
+            self._chk(self._L.a5x_expand_digest_range_device(
+                self.h, d_words, d_offs, n_words, mode, mn, mx, cand_begin, (1 << 64) - 1 if cand_end is None else cand_end,
+                scratch_bytes, arr, hit_cap, ctypes.byref(nh), ctypes.byref(st), stream or None))
         return self._hits(arr, min(nh.value, hit_cap)), st.as_dict()
 
     def format_hits(self, words: np.ndarray, offs: np.ndarray, hits, mode: int = MODE_DEFAULT, mn: int = 0,

@@ -178,6 +178,14 @@ A5X_API int a5x_expand_digest_device(a5x_ctx* ctx, const uint8_t* d_words, const
                                      uint64_t n_words, int mode, int min, int max, uint64_t scratch_bytes,
                                      a5x_hit* hits, uint64_t hit_cap, uint64_t* n_hits, a5x_stats* stats,
                                      void* stream);
+/* The same for the batch's global candidates [cand_begin, cand_end) only (clipped to the
+ * batch): a shard whose ends cut words (a5x_split_device gives the cut
+ * points), as a5x_expand_device's range.  Hits name (word, candidate in word) of the
+ * batch; stats->candidates counts the range. */
+A5X_API int a5x_expand_digest_range_device(a5x_ctx* ctx, const uint8_t* d_words, const uint64_t* d_word_off,
+                                           uint64_t n_words, int mode, int min, int max, uint64_t cand_begin,
+                                           uint64_t cand_end, uint64_t scratch_bytes, a5x_hit* hits,
+                                           uint64_t hit_cap, uint64_t* n_hits, a5x_stats* stats, void* stream);
 /* Host-buffer version (stages the words into HBM first). */
 A5X_API int a5x_expand_digest(a5x_ctx* ctx, const uint8_t* words, const uint64_t* word_off, uint64_t n_words,
                               int mode, int min, int max, a5x_hit* hits, uint64_t hit_cap, uint64_t* n_hits,

@@ -232,3 +232,56 @@ def test_fused_slot_path_every_candidate_mixed_utf8(gpu_ctx, algo):
         got.setdefault(d, set()).add((w, c))
     assert sum(len(v) for v in got.values()) == len(hits)  # each (word, candidate) once
     assert got == want
+
+
+@pytest.mark.parametrize("algo,mode,tabs", [(0, 0, ["czech", "german"]), (1, 0, ["czech", "german"]),
+                                            (0, 1, ["greek-hebrew"]), (0, 2, ["greek-hebrew"]),
+                                            (1, 3, ["greek-hebrew"])])
+def test_digest_ranges_partition_the_hits(gpu_ctx, algo, mode, tabs):
+    """a5x_expand_digest_range_device: the batch's
+    candidates cut into ranges at arbitrary candidates -- inside FAST words, slow / BIG
+    words and mode-engine items -- give exactly the whole batch's hits, each range only
+    the hits of its own candidates (every 7th candidate of the batch is a target)."""
+    from hashcat_a5_table_generator_amd import DeviceBuffer, pack_words
+    from oracle import digest_oracle as dg
+    gpu_ctx.clear_table()
+    gpu_ctx.load_tables([table_path(t) for t in tabs])
+    greek = tabs == ["greek-hebrew"]
+    words = _words(31 + algo + 3 * mode, 600, greek=greek)
+    if greek:
+        words += ["αλφαβητα".encode() * 2, "ααααααααα".encode()]  # repeated patterns (-s virtual words)
+    else:
+        words += [b"stras" * 14, b"a" * 70, b"strasse" * 45, b"abcdefghijklmnopqrstuvwxyz"[:20]]  # slow / BIG / big
+    data, offs = pack_words(words)
+    cnt, _ = gpu_ctx.keyspace(data, offs, mode, 0, 15)
+    coff = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])
+    tc = int(coff[-1])
+    per_word = gpu_ctx.expand_words(words, mode, 0, 15)
+    f = dg.ALGOS[algo]
+    flat = [c for w in per_word for c in w]
+    assert len(flat) == tc
+    targets = {f(flat[g]) for g in range(0, tc, 7)}
+    gpu_ctx.set_targets(algo, b"".join(sorted(targets)) + bytes(range(16)))
+    dw = DeviceBuffer.from_array(gpu_ctx, data)
+    do = DeviceBuffer.from_array(gpu_ctx, offs)
+
+    def hits(cb=0, ce=None):
+        h, st = gpu_ctx.expand_digest_device(dw.ptr, do.ptr, len(words), mode, 0, 15, hit_cap=1 << 18,
+                                             cand_begin=cb, cand_end=ce)
+        assert st["candidates"] == (tc if ce is None else ce) - cb
+        return {(int(w), int(c)) for w, c, _ in h}
+
+    full = hits()
+    want = {(w, c) for w, cs in enumerate(per_word) for c, x in enumerate(cs) if f(x) in targets}
+    assert full == want
+    rng = np.random.default_rng(5 + mode)
+    cuts = sorted({0, tc, *(int(x) for x in rng.integers(1, tc, size=5))})
+    big = int(np.argmax(cnt))  # also cut inside the largest word
+    cuts = sorted(set(cuts) | {int(coff[big]) + int(cnt[big]) // 3})
+    union = set()
+    for a, b in zip(cuts, cuts[1:]):
+        part = hits(a, b)
+        assert all(a <= coff[w] + c < b for w, c in part), (a, b)
+        assert not (part & union)
+        union |= part
+    assert union == full

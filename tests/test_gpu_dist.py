@@ -154,3 +154,20 @@ def test_bench_gpus_2_without_launcher(tmp_path):
     b0, b1, d1 = _digests(tmp_path / "w1")
     assert (a0, a1) == (b0, b1) == (0, 40000)
     assert np.array_equal(d2, d1)
+
+
+def test_two_ranks_digest_cut_huge_words(tmp_path):
+    """the fused digest cuts words too -- 24-letter words (2^24 - 1
+    candidates each) larger than a rank's share are split at candidates
+    (a5x_expand_digest_range_device), the ranks' shard bytes differ by < 1 %, and the hits
+    gathered on rank 0 equal the single-rank run's."""
+    args = ["--workload", "c4h", "--digest", "md5", "--targets", "20000"]
+    r2 = _bench(2, args + ["--words", "30000"], tmp_path / "h2")
+    r1 = _bench(1, args + ["--words", "60000"], tmp_path / "h1")
+    h2 = np.load(tmp_path / "h2" / "hits.npy")
+    h1 = np.load(tmp_path / "h1" / "hits.npy")
+    assert len(h1) >= r1["config"]["planted"] > 0
+    key = lambda h: sorted(map(tuple, h.tolist()))
+    assert key(h2) == key(h1)
+    shares = r2["config"]["bytes_per_rank"]
+    assert max(shares) / min(shares) < 1.01, shares  # (word-granular shards could not: a word is ~20 % of one)
