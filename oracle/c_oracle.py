@@ -14,8 +14,8 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_SO = os.path.join(_HERE, "_build", "liba5oracle.so")
-_lib = None
+_SO = os.environ.get("A5X_ORACLE_LIB") or os.path.join(_HERE, "_build", "liba5oracle.so")
+_lib = None  # (A5X_ORACLE_LIB: tools/sanitize.sh points it at the ASan/UBSan build)
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
