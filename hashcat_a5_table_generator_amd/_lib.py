@@ -25,7 +25,7 @@ E_CAPACITY = -8
 EXPORTS = (
     "a5x_abi_version", "a5x_create", "a5x_destroy", "a5x_last_error", "a5x_device_info",
     "a5x_load_table_file", "a5x_parse_table", "a5x_set_table", "a5x_clear_table", "a5x_table_export",
-    "a5x_split_words", "a5x_keyspace", "a5x_expand", "a5x_expand_device", "a5x_keyspace_device",
+    "a5x_split_words", "a5x_keyspace", "a5x_expand", "a5x_expand_range", "a5x_expand_device", "a5x_keyspace_device",
     "a5x_digest_device", "a5x_partition", "a5x_dev_alloc", "a5x_dev_free", "a5x_memcpy_h2d",
     "a5x_memcpy_d2h", "a5x_synchronize", "a5x_debug_stamps", "a5x_debug_plan_word",
     "a5x_set_targets", "a5x_expand_digest", "a5x_expand_digest_device", "a5x_expand_digest_range_device",
@@ -93,6 +93,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     L.a5x_split_words.argtypes = [vp, sz, vp, vp, u64, ctypes.POINTER(u64)]
     L.a5x_keyspace.argtypes = [vp, vp, vp, u64, i, i, i, vp, vp]
     L.a5x_expand.argtypes = [vp, vp, vp, u64, i, i, i, SINK, vp, ctypes.POINTER(Stats)]
+    L.a5x_expand_range.argtypes = [vp, vp, vp, u64, i, i, i, u64, u64, SINK, vp, ctypes.POINTER(Stats)]
     L.a5x_expand_device.argtypes = [vp, vp, vp, u64, i, i, i, u64, u64, vp, u64, vp, vp, ctypes.POINTER(Stats), vp]
     L.a5x_keyspace_device.argtypes = [vp, vp, vp, u64, i, i, i, vp, vp, ctypes.POINTER(u64),
                                       ctypes.POINTER(u64), vp]

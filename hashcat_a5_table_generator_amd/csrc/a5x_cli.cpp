@@ -7,12 +7,20 @@
 //   a5x_generator <dict-file> -t <table> [-t <table> ...] [-m N] [-x N]
 //                 [--threads N] [-s] [-r] [--device N]
 //                 [--hashes <file> [--algo md5|ntlm]]
+//                 [--skip N] [--limit N] [--keyspace]
 //
 // --hashes (a5x extension): instead of printing the candidates for a
 // hashcat pipe (README.MD:69), hash them on the GPU (fused MD5 / NTLM + lookup) against
 // the hex digests of <file> and print what hashcat would report, "hash:plain" (plains
 // that hashcat would hexify as $HEX[...]), each target once, at its first candidate in
 // stream order (README.MD:74-106, :168).
+//
+// --skip / --limit / --keyspace (a5x extension, SURVEY §5 checkpoint / resume): the
+// stream's candidate order does not depend on batching (a word's candidates are
+// numbered alike in any batch), so a candidate index is a resume cursor: --skip N
+// --limit M prints candidates [N, N + M) of the full stream, as hashcat's -s / -l would
+// on the pipe; --keyspace prints the number of candidates the run would print.  Whole
+// batches before the window cost only their keyspace pass.
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -48,7 +56,10 @@ static void usage(FILE* f) {
           "  -r, --reverse-sub                 Reverse substitution direction\n"
           "      --device=0                    GPU ordinal (a5x extension)\n"
           "      --hashes=FILE                 Crack: print hash:plain for the digests in FILE (a5x extension)\n"
-          "      --algo=md5                    Digest of --hashes: md5 (hashcat -m 0) or ntlm (-m 1000)\n");
+          "      --algo=md5                    Digest of --hashes: md5 (hashcat -m 0) or ntlm (-m 1000)\n"
+          "      --skip=0                      Resume: start at candidate N of the stream (a5x extension)\n"
+          "      --limit=N                     Print at most N candidates (a5x extension)\n"
+          "      --keyspace                    Print the number of candidates and exit (a5x extension)\n");
 }
 
 // ---------------------------------------------------------------------------
@@ -193,6 +204,15 @@ static int load_targets(a5x_ctx* ctx, const char* path, int algo) {
   return a5x_set_targets(ctx, algo, dig.empty() ? nullptr : dig.data(), dig.size() / 16);
 }
 
+static bool parse_u64(const char* s, uint64_t* out) {
+  char* e;
+  errno = 0;
+  const unsigned long long v = strtoull(s, &e, 10);
+  if (!*s || *e || *s == '-' || errno) return false;
+  *out = v;
+  return true;
+}
+
 static bool parse_int(const char* s, int* out) {
   char* e;
   long v = strtol(s, &e, 10);
@@ -201,12 +221,68 @@ static bool parse_int(const char* s, int* out) {
   return true;
 }
 
+// --skip / --limit / --keyspace: one context, batches in order; each batch's keyspace
+// gives its candidate total T, so the window [skip, skip + limit) maps to a candidate
+// range of the batches it meets (a5x_expand_range), and the batches past it are not read.
+static int run_cursor(const std::string& dict, const std::vector<std::string>& tables, int device, int mode, int tmin,
+                      int tmax, uint64_t B, size_t BB, size_t chunk, uint64_t skip, uint64_t limit, bool keyspace_only) {
+  a5x_ctx* ctx = nullptr;
+  int rc = a5x_create(device, &ctx);
+  if (rc) { fprintf(stderr, "a5_generator: no usable GPU (a5x_create=%d)\n", rc); return 1; }
+  for (auto& t : tables)
+    if ((rc = a5x_load_table_file(ctx, t.c_str()))) {
+      fprintf(stderr, "%s\n", a5x_last_error(ctx));  // log.Fatal (main.go:43-45)
+      a5x_destroy(ctx);
+      return 1;
+    }
+  FILE* f = fopen(dict.c_str(), "rb");
+  if (!f) { perror(dict.c_str()); a5x_destroy(ctx); return 1; }
+  const uint64_t end = limit > ~0ull - skip ? ~0ull : skip + limit;  // (saturating)
+  DictStream ds(f, chunk);
+  std::vector<uint8_t> words;
+  std::vector<uint64_t> off, cnt;
+  uint64_t G = 0;  // stream candidates before this batch
+  bool ovf = false;
+  while (rc == 0 && (keyspace_only || G < end) && ds.next(words, off, B, BB)) {
+    const uint64_t nb = off.size() - 1;
+    cnt.assign(nb, 0);
+    if ((rc = a5x_keyspace(ctx, words.data(), off.data(), nb, mode, tmin, tmax, cnt.data(), nullptr))) break;
+    uint64_t T = 0;
+    for (uint64_t x : cnt) {
+      ovf |= T + x < T;
+      T += x;
+    }
+    if (!keyspace_only) {
+      const uint64_t lo = skip > G ? std::min(T, skip - G) : 0, hi = end - G < T ? end - G : T;
+      if (lo < hi)
+        rc = a5x_expand_range(ctx, words.data(), off.data(), nb, mode, tmin, tmax, lo, hi, sink_stdout, nullptr,
+                              nullptr);
+    }
+    ovf |= G + T < G;
+    G += T;
+  }
+  fclose(f);
+  if (rc == 0 && keyspace_only) {
+    if (ovf) { fprintf(stderr, "a5_generator: the keyspace exceeds 2^64 - 1 candidates\n"); rc = A5X_E_OVERFLOW; }
+    else printf("%llu\n", (unsigned long long)G);
+  }
+  if (fflush(stdout) != 0 || ferror(stdout)) {
+    if (!rc) fprintf(stderr, "a5_generator: writing stdout: %s\n", strerror(errno));
+    rc = rc ? rc : 1;
+  } else if (rc && rc != A5X_E_OVERFLOW) {
+    fprintf(stderr, "a5_generator: %s\n", a5x_last_error(ctx));
+  }
+  a5x_destroy(ctx);
+  return rc ? 2 : 0;
+}
+
 int main(int argc, char** argv) {
   std::vector<std::string> tables;
   std::string dict;
   int tmin = 0, tmax = 15, threads = -1, device = 0, algo = A5X_ALGO_MD5;
   std::string hashes;
-  bool suball = false, rev = false;
+  bool suball = false, rev = false, keyspace_only = false, cursor = false;
+  uint64_t skip = 0, limit = ~0ull;
   auto need = [&](int& i, const char* flag) -> const char* {
     if (i + 1 >= argc) {
       fprintf(stderr, "a5_generator: error: %s: expected value\n", flag);
@@ -255,7 +331,14 @@ int main(int argc, char** argv) {
       if (v == "md5" || v == "0") algo = A5X_ALGO_MD5;
       else if (v == "ntlm" || v == "1000") algo = A5X_ALGO_NTLM;
       else { fprintf(stderr, "a5_generator: error: --algo: md5 or ntlm\n"); return 80; }
-    } else if (s == "--substitute-all") suball = true;
+    } else if (s.rfind("--skip", 0) == 0) {
+      if (!parse_u64(val_of("--skip"), &skip)) { fprintf(stderr, "a5_generator: error: --skip: bad count\n"); return 80; }
+      cursor = true;
+    } else if (s.rfind("--limit", 0) == 0) {
+      if (!parse_u64(val_of("--limit"), &limit)) { fprintf(stderr, "a5_generator: error: --limit: bad count\n"); return 80; }
+      cursor = true;
+    } else if (s == "--keyspace") keyspace_only = true;
+    else if (s == "--substitute-all") suball = true;
     else if (s == "--reverse-sub") rev = true;
     else if (s.size() > 1 && s[0] == '-' && s[1] != '-') {
       bool ok = true;  // combined boolean shorts, e.g. -sr
@@ -283,6 +366,12 @@ int main(int argc, char** argv) {
   if (const char* e = getenv("A5X_CLI_CHUNK")) chunk = std::max<size_t>(1, strtoull(e, nullptr, 10));
   static char obuf[1 << 22];
   setvbuf(stdout, obuf, _IOFBF, sizeof obuf);
+  if (!hashes.empty() && (cursor || keyspace_only)) {
+    fprintf(stderr, "a5_generator: error: --skip / --limit / --keyspace select the candidate stream, not --hashes\n");
+    return 80;
+  }
+  if (hashes.empty() && (cursor || keyspace_only)) return run_cursor(dict, tables, device, mode, tmin, tmax, B, BB, chunk,
+                                                                     skip, limit, keyspace_only);
   if (hashes.empty()) {
     // The stdout pipeline.  The GPU contexts are created (and their stream buffers made)
     // on a second thread while this one reads the first batch, which is small so output

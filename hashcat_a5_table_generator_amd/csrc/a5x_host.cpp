@@ -1989,6 +1989,13 @@ int a5x_stream_reserve(a5x_ctx* c, uint64_t words, uint64_t word_bytes) {
 // range expands, and the sink consumes range k while range k + 1 is being copied.
 int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
                a5x_sink_fn sink, void* user, a5x_stats* stats) {
+  return a5x_expand_range(c, words, woff, nw, mode, mn, mx, 0, ~0ull, sink, user, stats);
+}
+
+// a5x_expand over the batch's global candidates [cb, ce) only (the CLI's --skip / --limit
+// resume cursor): the same keyspace, the ranges cut at the window's ends.
+int a5x_expand_range(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t nw, int mode, int mn, int mx,
+                     uint64_t cb, uint64_t ce, a5x_sink_fn sink, void* user, a5x_stats* stats) {
   if (c && c->device < 0) return fail(c, A5X_E_HIP, "host-only context (device -1) cannot run kernels");
   if (!c || !sink || (nw && (!words || !woff))) return A5X_E_ARG;
   int rc;
@@ -2003,7 +2010,7 @@ int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t 
   if ((rc = job_prepare(c, J, nullptr, nullptr, true))) return rc;
   const size_t cap = stream_cap();
   std::vector<Range> ranges;
-  if ((rc = plan_ranges(c, J, cap, ranges))) return rc;
+  if ((rc = plan_ranges(c, J, cap, ranges, cb, ce))) return rc;
   if (!ranges.empty() && (rc = stream_buffers(c, cap))) return rc;
   // error word of each range, copied behind its launch (valid once its copy event fired)
   uint32_t* herr = c->h_scalars + 32;
@@ -2033,8 +2040,13 @@ int a5x_expand(a5x_ctx* c, const uint8_t* words, const uint64_t* woff, uint64_t 
   if (stats) {
     memset(stats, 0, sizeof *stats);
     stats->words = nw;
-    stats->candidates = J.B.total_cands;
+    stats->candidates = J.B.total_cands;  // (the whole batch; the window's: its ranges below)
     stats->bytes = J.B.total_bytes;
+    if (cb != 0 || ce < J.B.total_cands) {
+      stats->candidates = 0;
+      stats->bytes = 0;
+      for (const Range& R : ranges) stats->candidates += R.ce - R.cb, stats->bytes += R.b1 - R.b0;
+    }
     float a = 0, t = 0;
     HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
     HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[2]));

@@ -168,8 +168,9 @@ class Context:
         return cnt[:n], byt[:n]
 
     def expand(self, words: np.ndarray, offs: np.ndarray, mode: int = MODE_DEFAULT, mn: int = 0, mx: int = 15,
-               sink=None) -> Tuple[bytes, dict]:
-        """Expand a packed batch; returns the output bytes (words in order) unless a sink is given."""
+               sink=None, cand_begin: int = 0, cand_end: Optional[int] = None) -> Tuple[bytes, dict]:
+        """Expand a packed batch; returns the output bytes (words in order) unless a sink is given.
+        cand_begin / cand_end: only the batch's candidates [cand_begin, cand_end) (a5x_expand_range)."""
         chunks: List[bytes] = []
 
         def _cb(_u, p, n):
@@ -181,8 +182,9 @@ class Context:
 
         st = Stats()
         cb = _lib.SINK(_cb)
-        self._chk(self._L.a5x_expand(self.h, words.ctypes.data, offs.ctypes.data, len(offs) - 1, mode, mn, mx,
-                                     cb, None, ctypes.byref(st)))
+        ce = (1 << 64) - 1 if cand_end is None else cand_end
+        self._chk(self._L.a5x_expand_range(self.h, words.ctypes.data, offs.ctypes.data, len(offs) - 1, mode, mn, mx,
+                                           cand_begin, ce, cb, None, ctypes.byref(st)))
         return b"".join(chunks), st.as_dict()
 
     def expand_words(self, words: Sequence[bytes], mode: int = MODE_DEFAULT, mn: int = 0, mx: int = 15) -> List[List[bytes]]:

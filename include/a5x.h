@@ -134,6 +134,15 @@ A5X_API int a5x_keyspace(a5x_ctx* ctx, const uint8_t* words, const uint64_t* wor
  * contiguous.  Replaces the goroutine-per-word dispatch + channel of main.go:70-98. */
 A5X_API int a5x_expand(a5x_ctx* ctx, const uint8_t* words, const uint64_t* word_off, uint64_t n_words, int mode,
                        int min, int max, a5x_sink_fn sink, void* user, a5x_stats* stats);
+/* a5x_expand of the batch's global candidates [cand_begin, cand_end) only (cand_end =
+ * UINT64_MAX: to the end): a resume cursor over the stream (CLI --skip / --limit, the
+ * role of hashcat's own -s / -l on the pipe the reference feeds, README.MD:69).  A
+ * word's candidate order does not depend on the batch it is in, so (batch offset +
+ * index) names one candidate of the dictionary's stream.  stats->candidates / bytes
+ * count the window. */
+A5X_API int a5x_expand_range(a5x_ctx* ctx, const uint8_t* words, const uint64_t* word_off, uint64_t n_words,
+                             int mode, int min, int max, uint64_t cand_begin, uint64_t cand_end, a5x_sink_fn sink,
+                             void* user, a5x_stats* stats);
 
 /* Make a5x_expand's buffers ahead of the first call (pinned double buffer, HBM range
  * buffers, copy stream, the keyspace state of a batch of `words` words / `word_bytes`

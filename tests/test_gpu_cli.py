@@ -143,3 +143,44 @@ def test_cli_hashes_long_potfile_line(tmp_path):
     assert r.returncode == 0, r.stderr.decode(errors="replace")[-2000:]
     assert r.stdout == d.hex().encode() + b":aa\n"
     assert b"line(s)" not in r.stderr
+
+
+@pytest.mark.parametrize("mode,flags", [(0, []), (2, ["-s"]), (3, ["-s", "-r"])])
+def test_cli_resume_cursor(dict_file, mode, flags):
+    """--keyspace prints the stream's candidate count; --skip N --limit M prints exactly
+    lines [N, N + M) of the full stream (SURVEY §5 checkpoint / resume), whatever the
+    batching: the cursor run uses other batch sizes than the full run, so this also pins
+    the batch-independent candidate order of every word."""
+    path, _ = dict_file
+    base = [CLI, path, "-t", table_path("qwerty-azerty"), *flags]
+    full = subprocess.run(base, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert full.returncode == 0, full.stderr.decode(errors="replace")[-2000:]
+    lines = full.stdout.split(b"\n")[:-1]
+    env = dict(os.environ, A5X_CLI_BATCH="1500", A5X_CLI_CHUNK="9001")
+    ks = subprocess.run(base + ["--keyspace"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120, env=env)
+    assert ks.returncode == 0 and int(ks.stdout) == len(lines)
+    n = len(lines)
+    for skip, limit in [(0, 1), (1, 1000), (n // 3, n // 2), (n - 7, 100), (n + 5, 10), (12345, None)]:
+        args = ["--skip", str(skip)] + ([] if limit is None else [f"--limit={limit}"])
+        r = subprocess.run(base + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120, env=env)
+        assert r.returncode == 0, r.stderr.decode(errors="replace")[-2000:]
+        want = lines[skip:] if limit is None else lines[skip:skip + limit]
+        assert r.stdout == b"".join(x + b"\n" for x in want), (skip, limit)
+    bad = subprocess.run(base + ["--skip", "-3"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=60)
+    assert bad.returncode == 80
+
+
+def test_expand_range_windows_concatenate(dict_file):
+    """Context.expand over candidate windows (a5x_expand_range) cut inside words: the
+    windows concatenate to the full batch output."""
+    from hashcat_a5_table_generator_amd import Context, split_words
+    _, body = dict_file
+    words, offs = split_words(body)
+    with Context(0) as c:
+        c.load_tables([table_path("qwerty-azerty")])
+        for mode in (0, 1, 2):
+            full, st = c.expand(words, offs, mode)
+            T = st["candidates"]
+            cuts = sorted({0, T, 1, T // 7, T // 2 + 3, T - 1})
+            parts = [c.expand(words, offs, mode, cand_begin=a, cand_end=b)[0] for a, b in zip(cuts, cuts[1:])]
+            assert b"".join(parts) == full, mode
