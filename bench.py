@@ -317,9 +317,13 @@ def digest_cpu_baseline(tables, args, targets):
 def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
     """Digest stage: VALU-bound.  achieved = integer lane-ops/s of the digest kernel (int
     ops per candidate from the PMC profile (tools/gpu.sh digestprof) x candidates / stage
-    time); peak = 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz 32-bit VALU ops (a
-    wave64 VALU instruction issues over 2 cycles: MI355X_MICROARCH.md; = the 157.3 TF f32
-    FMA peak / 2).  Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm
+    time); peak = 256 CUs x 4 SIMDs x 16 lanes/cycle x 2.4 GHz = 39.3 T int32 lane-ops/s:
+    the issue rate of the VOP3 instructions the MD5 / MD4 rounds are made of (v_add3_u32,
+    v_bfi_b32, v_alignbit_b32, v_xor3_b32), 4 cycles per wave64 instruction -- measured on
+    MI355X (tools/mb_valu.hip, profiles/r05_mb_valu.txt: v_perm / v_alignbyte 1.93 ns per
+    wave-instruction per SIMD, twice v_add_u32's 1.13 ns: VOP2 ops issue in 2 cycles, VOP3
+    in 4).  Round 4 priced every op at the VOP2 rate (78.6 T), which halved frac against the
+    PMC's VALUBusy; peak_vop2 keeps that figure.  Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm
     expand, hash and probe in one kernel, so the stage time is the expansion time.  The
     step's time is accounted as keyspace + stage (+ two-pass digest) + the rest (host)."""
     fused = ms_dig < 1e-3
@@ -329,9 +333,10 @@ def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
               if fused else "k_digest_stream")
     ms_stage = ms_exp if fused else ms_dig
     prof = digest_profile(args.digest, args.words, kernel, args.mode, args.min)
-    peak = 256 * 4 * 32 * 2.4e9 / 1e12  # Tops/s
+    peak = 256 * 4 * 16 * 2.4e9 / 1e12  # Tops/s at the VOP3 issue rate
     r = {"bound": "valu", "kernel": kernel + ("" if fused else f"<{args.digest}>"), "fused": fused,
-         "unit": "Tops/s (int32 lane ops)", "peak": peak, "ms_digest_per_step": ms_stage if not fused else 0.0,
+         "unit": "Tops/s (int32 lane ops)", "peak": peak, "peak_vop2": 2 * peak,
+         "ms_digest_per_step": ms_stage if not fused else 0.0,
          "ms_expand_per_step": ms_exp, "ms_keyspace_per_step": ms_ks, "ms_step": ms_step,
          "ms_step_unaccounted": ms_step - ms_ks - ms_exp - (0.0 if fused else ms_dig),
          "digest_cand_per_s": tc / (ms_stage * 1e-3), "achieved": None, "frac": None, "profile": None}

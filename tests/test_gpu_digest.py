@@ -251,7 +251,10 @@ def test_digest_ranges_partition_the_hits(gpu_ctx, algo, mode, tabs):
     if greek:
         words += ["αλφαβητα".encode() * 2, "ααααααααα".encode()]  # repeated patterns (-s virtual words)
     else:
-        words += [b"stras" * 14, b"a" * 70, b"strasse" * 45, b"abcdefghijklmnopqrstuvwxyz"[:20]]  # slow / BIG / big
+        # cluster words, a 20-letter word past the FAST piece limits (slow path), words
+        # longer than 64 B (BIG path); keyspaces of 11..3455 candidates
+        words += [b"sassas", b"abcdefghijklmnopqrst", b"q" * 64 + b"abcdes", b"qq" * 40 + b"strasse",
+                  b"q" * 100 + b"sss" + b"q" * 30]
     data, offs = pack_words(words)
     cnt, _ = gpu_ctx.keyspace(data, offs, mode, 0, 15)
     coff = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])
