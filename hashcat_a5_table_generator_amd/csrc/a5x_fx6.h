@@ -1,22 +1,18 @@
 // a5x_fx6.h -- round machinery of k_expand_fast (device only; included by
 // a5x_kernels.hip and tools/mb_rounds.hip).
 //
-// A window holds the big-piece entries of up to FX6_WW consecutive FAST words in LDS
+// A window holds the big-piece entries of up to FX_WW consecutive FAST words in LDS
 // (a5x_plan.h: a word's candidate n <-> the mixed-radix digits of n + 1 over its big
 // pieces, piece 0 least significant).  A round covers 64 * K consecutive candidates of
 // the window: lane L takes the RUN of candidates [K L, K L + K) (consecutive ranks of
-// one word, or crossing into the next word), so after one division per run the digits
-// advance as an odometer.  Per round:
-//   pass 1  digits -> entry indices -> candidate lengths (length bytes only);
+// one word), so after one division per run the digits advance as an odometer.  Per round:
+//   pass 1  digits -> entry indices -> candidate lengths;
 //   scan    DPP wave prefix sum of the run lengths -> byte offset of every run;
-//   pass 2  every piece appended to the per-wave LDS ring as whole aligned dwords:
-//           5 dwords per piece (v_perm byte shift), written unconditionally; the
-//           pending partial dword is carried in a register.  Writes past a run's last
-//           dword are clamped onto it and issued highest first, so the run's own later
-//           bytes (or its final merge) always land last.  The dword a run shares with
-//           the next lane's run is written once at the end, merged with that lane's
-//           head bytes (one cross-lane move per round);
-//   flush   complete 16-B ring blocks -> global_store_dwordx4 (1 KiB per instruction).
+//   pass 2  every piece ORed into the per-wave LDS ring at its byte offset (a5x_ring.h
+//           fx7_put: the ring is zero between flushes and entries are zero past their
+//           length, so no ordering or cross-lane merge is needed);
+//   flush   complete 16-B ring blocks -> global_store_dwordx4 (1 KiB per instruction),
+//           the ring zeroed behind them.
 #pragma once
 
 #ifndef FX_HOLDNB
@@ -25,51 +21,10 @@
 #ifndef FX6_ZBE
 #define FX6_ZBE 255      // the window entry that holds the empty piece (set by the includer)
 #endif
-#ifndef FX_PIPE
-#define FX_PIPE 1        // fx7_round, > FX_HOLDNB pieces: entry reads one candidate ahead of the ORs
-#endif
 
 // (FxRun, the wave's staging state, and the ring flush are defined by the includer.)
 
 #include "a5x_ring.h"
-
-// One piece (entry e: 15 content bytes + length in byte 15) appended at LDS byte
-// address P.  Only the piece's complete dwords are written (t = (P & 3) + length:
-// dwords k < t / 4), never bytes past it, so no clamping or write ordering is needed;
-// dwords that are not due go to the lane's trash dword (branch-free, no exec masking).
-// The run's first dword, when the run starts inside a dword (dfirst = its address,
-// else ~0), is shared with the previous lane's run: it is kept in hd for that lane's
-// final merged write instead.  acc = pending bytes of the dword holding P.
-template <bool FIRST>
-__device__ __forceinline__ void fx6_put(const uint4 e, u32& P, u32& acc, u32 dfirst, u32& hd, u32 trash) {
-  const u32 n = P & 3u, base = P & ~3u;
-  const u32 l = e.w >> 24, e3 = e.w & 0xFFFFFFu;
-  const u32 sel = fx6_sel(n);
-  const u32 w0 = (e.x << (8u * n)) | acc;
-  const u32 w1 = __builtin_amdgcn_perm(e.y, e.x, sel);
-  const u32 w2 = __builtin_amdgcn_perm(e.z, e.y, sel);
-  const u32 w3 = __builtin_amdgcn_perm(e3, e.z, sel);
-  const u32 w4 = __builtin_amdgcn_perm(0u, e3, sel);
-  const u32 t = n + l;
-  const bool c4 = t >= 4u, c8 = t >= 8u, c12 = t >= 12u, c16 = t >= 16u;
-  // only the run's first candidate can touch its shared first dword (candidates >= 3 B)
-  const bool shared = FIRST && base == dfirst;
-  // (opaque addresses, so the +4 / +8 / +12 stay DS immediate offsets)
-  u32 a1 = c8 ? base : trash - 4u, a2 = c12 ? base : trash - 8u, a3 = c16 ? base : trash - 12u;
-  asm volatile("" : "+v"(a1), "+v"(a2), "+v"(a3));
-  fx6_st((c4 && !shared) ? base : trash, w0);
-  fx6_st(a1 + 4u, w1);
-  if (__builtin_amdgcn_ballot_w64(c12)) {  // pieces reaching a third dword (wave-uniform)
-    fx6_st(a2 + 8u, w2);
-    fx6_st(a3 + 12u, w3);
-  }
-  if (FIRST) hd = shared ? w0 : hd;
-  u32 x = c4 ? w1 : w0;
-  x = c8 ? w2 : x;
-  x = c12 ? w3 : x;
-  acc = c16 ? w4 : x;
-  P += l;
-}
 
 // Per window word j: q0 = {magic of big pieces 0..3}, q1 = {R-1 of pieces 0..3 (6 bits
 // each), entry base of pieces 0/1 (16 bits each), pieces 2/3, first run of the word
@@ -104,80 +59,6 @@ __device__ __forceinline__ u32 fx6_eb(const uint4 q1, int b) {
   return b == 0 ? (q1.y & 0xFFFFu) : b == 1 ? (q1.y >> 16) : b == 2 ? (q1.z & 0xFFFFu) : (q1.z >> 16);
 }
 
-// One round: window runs [rr, rr + nl): lane L < nl takes run rr + L of window word j
-// (ranks rb[j] + K (run - first run of j) .. + K, clipped to the word's rank end
-// re[j]; words start on run boundaries, so a run never crosses words).  be / wq /
-// rb / re: the window's entries and per-word info in LDS; ring = LDS byte address of
-// ring byte 0, trash = the lane's trash dword.  Needs nl K (longest candidate) + 32
-// <= the ring size and every candidate >= 3 bytes.  Runs are taken while they fit cap
-// ring bytes (the rest wait for the next round); returns the runs taken (uniform).
-template <int NB, int K, class FLUSH>
-__device__ __forceinline__ u32 fx6_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
-                                         u32 trash, u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush) {
-  const u32 lane = lane_id();
-  const uint4 q0 = wq[j][0], q1 = wq[j][1];
-  const u32 st = act ? (rr + lane - q1.w) * K + rb[j] : 0u;  // first rank of the run
-  const u32 cw = act ? re[j] : 0u;
-  const u32 nc = cw > st ? min((u32)K, cw - st) : 0u;
-  u32 d[4];
-  fx6_digits<NB>(st + 1u, q0, q1.x, d);
-  // pass 1: entry indices and lengths; <= 2 pieces: the entries stay in registers,
-  // else (register budget) pass 2 reads them again
-  constexpr bool HOLD = NB <= FX_HOLDNB;
-  uint4 ent[HOLD ? K : 1][HOLD ? NB : 1];
-  u32 idx[HOLD ? 1 : K][HOLD ? 1 : NB];
-  u32 len = 0;
-  const uint8_t* lenb = (const uint8_t*)be + 15;
-#pragma unroll
-  for (int c = 0; c < K; c++) {
-    if (c > 0) fx6_step<NB>(q1.x, d);
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-      const u32 ix = c < (int)nc ? fx6_eb(q1, b) + d[b] : (u32)FX6_ZBE;  // past the run: empty
-      if constexpr (HOLD) {
-        ent[c][b] = be[ix];
-        len += ent[c][b].w >> 24;
-      } else {
-        idx[c][b] = ix;
-        len += lenb[16u * ix];
-      }
-    }
-  }
-  u32 incl = wave_incl_scan_u32(len);
-  // the runs that fit the ring this round (a prefix: the scan is monotonic); the rest
-  // are taken by the next round
-  const u32 used = (u32)(R.pos - R.B);
-  const bool fit = nc > 0 && used + incl <= cap;
-  const u32 nact = uniform((u32)__popcll(__ballot(fit)));
-  const u32 tot = nact ? readlane_u32(incl, nact - 1u) : 0u;
-  const u32 o = ring + used + incl - len;
-  u32 P = o, acc = lane == 0 ? R.carry : 0u, hd = 0;
-  // lane 0 continues the previous round's carried dword itself
-  const u32 dfirst = (lane == 0 || (o & 3u) == 0) ? ~0u : (o & ~3u);
-  if (fit) {
-#pragma unroll
-  for (int c = 0; c < K; c++) {
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-      uint4 e;
-      if constexpr (HOLD) e = ent[c][b];
-      else e = be[idx[c][b]];
-      if (c == 0) fx6_put<true>(e, P, acc, dfirst, hd, trash);
-      else fx6_put<false>(e, P, acc, dfirst, hd, trash);
-    }
-  }
-  }
-  // the dword shared with the next lane's run (or carried to the next round): my
-  // pending bytes | that lane's head bytes
-  const u32 hnext = (u32)__shfl_down((int)hd, 1);
-  if (fit && (P & 3u)) fx6_st(P & ~3u, acc | (lane + 1 < nact ? hnext : 0u));
-  if (nact) R.carry = readlane_u32(acc, nact - 1u);
-  R.pos = uniform64(R.pos + tot);
-  WAVE_SYNC();
-  flush(R);
-  return nact;
-}
-
 // Window word of each lane's run: j = last word whose first run <= rr + lane.
 // rw = the per-lane register holding word lane's first run (lanes >= k: ~0);
 // jcur (uniform, in/out) = word of run rr; nl = runs in the round.
@@ -193,7 +74,12 @@ __device__ __forceinline__ u32 fx6_word(u32 rw, u32 k, u32 rr, u32 nl, u32& jcur
   return j;
 }
 
-// fx6_round with OR placement (same run / fit / scan logic; ring zero past R.pos)
+// One round: window runs [rr, rr + nl): lane L < nl takes run rr + L of window word j
+// (ranks rb[j] + K (run - first run of j) .. + K, clipped to the word's rank end re[j];
+// words start on run boundaries, so a run never crosses words).  be / wq / rb / re: the
+// window's entries and per-word info in LDS; ring = LDS byte address of ring byte 0.
+// Runs are taken while they fit cap ring bytes (a prefix: the scan is monotonic; the
+// rest wait for the next round); returns the runs taken (uniform).
 // A lane's run of the last round, for the fused digest (FLUSH::DIGEST): ring byte
 // offset of its first candidate, candidate lengths ('\n' included), window word, rank.
 #ifndef FX6_KMAX
@@ -204,11 +90,9 @@ struct FxLaneRun {
   u32 clen[FX6_KMAX];
 };
 
-// nsm: fx8_put slot counts of big pieces 0-3 (4 bits each, wave-uniform)
-template <int NB, int K, bool NOOR = false, class FLUSH>
+template <int NB, int K, class FLUSH>
 __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
-                                         u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush, FxLaneRun& lr,
-                                         u32 nsm) {
+                                         u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush, FxLaneRun& lr) {
   static_assert(K <= FX6_KMAX, "FxLaneRun holds FX6_KMAX candidates");
   const u32 lane = lane_id();
   const uint4 q0 = wq[j][0], q1 = wq[j][1];
@@ -244,34 +128,13 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
   const bool fit = nc > 0 && used + incl <= cap;
   const u32 nact = uniform((u32)__popcll(__ballot(fit)));
   const u32 tot = nact ? readlane_u32(incl, nact - 1u) : 0u;
-  u32 P = ring + used + incl - len, sink = 0;
+  u32 P = ring + used + incl - len;
   if (fit) {
-#if FX_AB
-    if constexpr (!NOOR) {
-      u32 P1 = P - 1u;
-      asm volatile("" : "+s"(nsm));  // slot tests stay scalar branches here (not hoisted lane masks)
-#pragma unroll
-      for (int c = 0; c < K; c++) {
-#pragma unroll
-        for (int b = 0; b < NB; b++) {
-          uint4 e;
-          if constexpr (HOLD) e = ent[c][b];
-          else e = be[idx[c][b]];
-          fx8_put(e, P1, (nsm >> (4 * b)) & 15u);
-        }
-      }
-    } else
-#endif
     if constexpr (HOLD) {
 #pragma unroll
       for (int c = 0; c < K; c++)
 #pragma unroll
-        for (int b = 0; b < NB; b++) fx7_put<NOOR>(ent[c][b], P, sink);
-    } else if constexpr (!FX_PIPE) {
-#pragma unroll
-      for (int c = 0; c < K; c++)
-#pragma unroll
-        for (int b = 0; b < NB; b++) fx7_put<NOOR>(be[idx[c][b]], P, sink);
+        for (int b = 0; b < NB; b++) fx7_put(ent[c][b], P);
     } else {
       // Entries read again here, one candidate ahead: candidate c + 1's NB reads are
       // issued before candidate c's ORs (in the same basic block, ahead of the puts'
@@ -288,17 +151,13 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
           for (int b = 0; b < NB; b++) nxt[b] = be[idx[c + 1][b]];
         }
 #pragma unroll
-        for (int b = 0; b < NB; b++) fx7_put<NOOR>(cur[b], P, sink);
+        for (int b = 0; b < NB; b++) fx7_put(cur[b], P);
         if (c + 1 < K) {
 #pragma unroll
           for (int b = 0; b < NB; b++) cur[b] = nxt[b];
         }
       }
     }
-  }
-  (void)nsm;
-  if constexpr (NOOR) {
-    if (sink == 0x9E3779B9u) fx7_or(ring, 1u);  // keeps the folded dwords live
   }
   R.pos = uniform64(R.pos + tot);
   WAVE_SYNC();

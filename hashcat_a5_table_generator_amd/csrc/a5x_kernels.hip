@@ -2066,11 +2066,11 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 // Non-FAST words are holes, written by k_expand_slow / k_expand_b.
 // ---------------------------------------------------------------------------
 #ifndef FX_RING
-#define FX_RING 4096  // per-wave linear output staging (bytes), then one trash dword per lane;
+#define FX_RING 4096  // per-wave linear output staging (bytes)
 #endif
                       // during the window setup bytes [16, 16 + 8 FX_WREC) hold the window's
                       // small records (ring block 0 keeps the run's partial block)
-#define FX_TRASH 256  // 64 lanes x 4 B
+#define FX_TRASH 256  // (unused gap in front of the ring; keeps the measured LDS layout)
 #ifndef FX_WW
 #define FX_WW 32      // window words
 #endif
@@ -2084,25 +2084,13 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #ifndef FX_K
 #define FX_K 4        // candidates per lane run (a5x_fx6.h)
 #endif
-#ifndef FX_PFM
-#define FX_PFM 1      // next window's metadata loaded before the current window's rounds
-#endif
 #ifndef FX_ABL
 #define FX_ABL 0      // timing ablations (variant builds only; output is garbage when set):
                       // 4 no global stores, 8 no rounds, 16 no big entries, 32 no prefix,
-                      // 64 no placement stores, 128 no ring re-zeroing
-#endif
-#ifndef FX_NOOR
-#define FX_OR         // OR placement into a zeroed ring (a5x_fx6.h fx7_round)
-#endif
-#ifndef FX_HOLESKIP
-#define FX_HOLESKIP 0 // 1: skip a run of hole words in one window step (A/B: C5 -s -1 %, C3 +0.8 %: off)
+                      // 128 no ring re-zeroing
 #endif
 #ifndef FX_DABL
 #define FX_DABL 0     // fused-digest ablations (variant builds, wrong hits): 1 no MD rounds, 2 no probe
-#endif
-#ifndef FX_AB
-#define FX_AB 0       // 1: fx8_put (alignbyte shifts, per-window scalar slot counts; A/B: 1 % slower)
 #endif
 
 // The window's small-piece records live in the ring (from byte 16) during the window
@@ -2161,21 +2149,12 @@ struct FxRun {
 
 // Stream the complete 16-B blocks of [B, pos) and move the partial last block to
 // ring block 0.  The first block of a run may start before lo: byte-exact.
-#ifndef FX_NT
-#define FX_NT 1  // nontemporal output stores (write-once stream)
-#endif
-#ifndef FX_FLB
-#define FX_FLB 0 // flush: batch the ring block reads before the stores
-#endif
-static_assert(!FX_FLB || FX_RING / 16 <= 256, "fx_flush (FX_FLB): at most 4 ring blocks per lane");
+// (nontemporal: the stream is written once; plain stores measured +4-8 % expansion time,
+// profiles/r05ce_ab_chunk_stores_occupancy_c3.txt)
 __device__ __forceinline__ void fx_store16(uint8_t* p, const uint4 v) {
-#if FX_NT
   typedef u32 v4u __attribute__((ext_vector_type(4)));
   v4u x = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(x, (v4u*)p);
-#else
-  *(uint4*)p = v;
-#endif
 }
 
 __device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) {
@@ -2185,78 +2164,34 @@ __device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) 
   const u64 B = uniform64(R.B);
   if (B + 16ull * nb > a.out_cap) { guard_trip(a, 1, B, R.lo, R.pos, a.out_cap); R.B = B + 16ull * nb; return; }
   uint4* r4 = (uint4*)ring;
-#if FX_FLB
-  // all (<= 4) block reads in flight together, then the stores; block 0 of a run that
-  // starts inside it is stored byte-exact
-  uint4 v[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const u32 b = lane + 64u * i;
-    if (b < nb) v[i] = r4[b];
-  }
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const u32 b = lane + 64u * i;
-    if (b < nb && !(FX_ABL & 4)) {
-      const u64 gb = B + 16ull * b;
-      if (i == 0 && gb < R.lo) store_block(a, gb, v[i], R.lo, R.pos);
-      else fx_store16(a.out + gb, v[i]);
-    }
-  }
-#ifdef FX_OR
-  // (OR placement: the flushed blocks back to zero)
-  if (!(FX_ABL & 128)) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const u32 b = lane + 64u * i;
-      if (b < nb) r4[b] = make_uint4(0, 0, 0, 0);
-    }
-  }
-#endif
-#else
   // (OR placement: every flushed block is zeroed again behind its read)
   if (B >= R.lo) {
     for (u32 b = lane; b < nb; b += 64) {
       if (!(FX_ABL & 4)) fx_store16(a.out + B + 16ull * b, r4[b]);
-#ifdef FX_OR
       if (!(FX_ABL & 128)) r4[b] = make_uint4(0, 0, 0, 0);
-#endif
     }
   } else {
     for (u32 b = lane; b < nb; b += 64) {
       if (!(FX_ABL & 4)) store_block(a, B + 16ull * b, r4[b], R.lo, R.pos);
-#ifdef FX_OR
       if (!(FX_ABL & 128)) r4[b] = make_uint4(0, 0, 0, 0);
-#endif
     }
   }
-#endif
   if (lane == 0) {
     const uint4 t = r4[nb];
-#ifdef FX_OR
     r4[nb] = make_uint4(0, 0, 0, 0);
-#endif
     r4[0] = t;
   }
   R.B = B + 16ull * nb;
   WAVE_SYNC();
 }
 
-// write the carried partial dword, flush everything up to pos (tail block byte-exact)
+// flush everything up to pos (tail block byte-exact)
 __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) {
   if (!R.open) return;
-#ifndef FX_OR
-  if (R.pos & 3u) {
-    if (lane_id() == 0) ring[(u32)(R.pos - R.B) >> 2] = R.carry;
-    WAVE_SYNC();
-  }
-#endif
   fx_flush(R, ring, a);
   if (R.pos > R.B && lane_id() == 0) {
     store_block(a, R.B, ((const uint4*)ring)[0], max(R.lo, R.B), R.pos);
-#ifdef FX_OR
     ((uint4*)ring)[0] = make_uint4(0, 0, 0, 0);
-#endif
   }
   WAVE_SYNC();
   R.open = false;
@@ -2435,9 +2370,9 @@ __device__ __forceinline__ void fxd_round(const uint4* be, const uint4 (*wq)[2],
     len += ent[b].w >> 24;
   }
   const u32 slot = ring + 64u * lane;
-  u32 P = slot, sink = 0;
+  u32 P = slot;
 #pragma unroll
-  for (int b = 0; b < NB; b++) fx7_put(ent[b], P, sink);
+  for (int b = 0; b < NB; b++) fx7_put(ent[b], P);
   constexpr u32 TL = MD5 ? 1u : 2u;  // the '\n' ("\n\0" in UTF-16LE) becomes the 0x80 pad
   if (on) {
     const u32 pb = slot + len - TL;
@@ -2503,9 +2438,9 @@ __device__ __forceinline__ void fxd_rounds(FXWin& F, u32* ring, const ExpArgs& a
 // with >= 2 / 3 / 4 big pieces).
 template <int K, class FL>
 __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FL& fl, u32 T, u32 k, u32 rw, u64 m2,
-                                          u64 m3, u64 m4, u32 nsm) {
+                                          u64 m3, u64 m4) {
   const u32 lane = lane_id();
-  const u32 ringa = fx6_addr(ring), trash = ringa - FX_TRASH + 4u * lane;
+  const u32 ringa = fx6_addr(ring);
   const u32 cap = FX_RING - 32u;
   u32 jcur = 0;
   for (u32 rr = 0; rr < T;) {
@@ -2516,26 +2451,10 @@ __device__ __forceinline__ void fx_rounds(FXWin& F, u32* ring, FxRun& R, FL& fl,
     const u64 span = ((2ull << (jl - jcur)) - 1ull) << jcur;  // words jcur .. jl
     u32 took;
     FxLaneRun lr;
-#ifdef FX_OR
-    (void)trash;
-#if FX_ABL & 64
-    if (true) {
-      if (span & m4) took = fx7_round<4, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
-      else if (span & m3) took = fx7_round<3, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
-      else if (span & m2) took = fx7_round<2, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
-      else took = fx7_round<1, K, true>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
-    } else
-#endif
-    if (span & m4) took = fx7_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
-    else if (span & m3) took = fx7_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
-    else if (span & m2) took = fx7_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
-    else took = fx7_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr, nsm);
-#else
-    if (span & m4) took = fx6_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
-    else if (span & m3) took = fx6_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
-    else if (span & m2) took = fx6_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
-    else took = fx6_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, trash, cap, R, rr, j, act, fl);
-#endif
+    if (span & m4) took = fx7_round<4, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+    else if (span & m3) took = fx7_round<3, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+    else if (span & m2) took = fx7_round<2, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
+    else took = fx7_round<1, K>(F.be, F.wq, F.rb, F.re, ringa, cap, R, rr, j, act, fl, lr);
     if constexpr (FL::DIGEST) {
       fl.digest(lr);
       fl(R);
@@ -2601,9 +2520,7 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
   while (w < a.nw && a.cand_off[w + 1] <= g0) w++;
   if (w >= a.nw) { guard_trip(a, 3, chunk, w, g0, a.nw); return; }
   if (lane == 0) F.be[FX_ZBE] = make_uint4(0, 0, 0, 0);
-#ifdef FX_OR
   for (u32 i = lane; i < FX_RING / 16; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
-#endif
   F.mag[lane] = fr_magic(lane);
   if (lane == 0) F.mag[FB_RMAX] = fr_magic(FB_RMAX);
   u64 g = g0;
@@ -2630,7 +2547,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     const u64 badm = __ballot(!ok);
     u32 k = badm ? (u32)__builtin_ctzll(badm) : 64u;
     STAMP(0);
-#if !FX_HOLESKIP
     if (k == 0) {  // (A/B: one hole word per step)
       const u64 w0c1 = uniform64(c1);
       if (w0c1 > g && w0c1 != ~0ull) {
@@ -2638,23 +2554,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
         g = min(w0c1, g1);
       }
       w++;
-      M = fx_meta(a, w);
-      continue;
-    }
-#endif
-    if (k == 0) {
-      // word w is a hole here (slow / BIG / a mode-engine word) or empty: skip every loaded
-      // word before the next FAST word with candidates in one step (holes come in runs
-      // when the mode engines share the batch)
-      const u64 fmk = __ballot(fast && hasc);
-      const u64 vmk = __ballot(c0 != ~0ull);
-      const u32 ns = fmk ? (u32)__builtin_ctzll(fmk) : (vmk ? 64u - (u32)__builtin_clzll(vmk) : 1u);
-      const u64 cend = uniform64(shfl_u64(c1, (int)(ns ? ns - 1u : 0u)));
-      if (cend > g && cend != ~0ull) {
-        if (!DIG) fx_close(R, ring, a);
-        g = min(cend, g1);
-      }
-      w += ns ? ns : 1u;
       M = fx_meta(a, w);
       continue;
     }
@@ -2740,7 +2639,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     STAMP(5);
     // ---- build the big entries: lanes over the window's entries (conv: as UTF-16LE, the
     // NTLM slot path; returns whether an entry could not be converted) ----
-    u32 thr = 0;  // bit 5 b + ceil(len / 4): the entry lengths of big piece b (fx8_slots)
     auto build_entries = [&](bool conv) -> bool {
       bool bad = false;
       const u32 etot = readlane_u32(incE, k - 1);
@@ -2781,7 +2679,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
           bad = bad || (on && !ok);
         }
         if (on) F.be[t] = e;
-        thr |= on ? (1u << ((((e.w >> 24) + 3u) >> 2) + 5u * b)) : 0u;
       }
       return wave_or_u32(bad ? 1u : 0u) != 0u;
     };
@@ -2789,7 +2686,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
       // an entry cut inside a rune (or too long as UTF-16LE): UTF-8 entries, K-candidate runs
       WAVE_SYNC();
       dslot = false;
-      thr = 0;
       (void)build_entries(false);
       K = FX_K * winmax + 16u <= FX_RING - 32u ? FX_K : 1u;
       nrun = inw && rs ? (rew - rbw + K - 1u) / K : 0u;
@@ -2797,15 +2693,6 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
       rw = inw ? incr - nrun : 0xffffffffu;
       T = readlane_u32(incr, k - 1);
       if (inw) F.wq[lane][1].w = rw;
-    }
-    // slot counts of the window's big pieces (wave-uniform)
-    const u32 thm = uniform(wave_or_u32(thr));
-    u32 nsm = 0;
-#pragma unroll
-    for (u32 b = 0; b < 4; b++) {
-      const u32 f = (thm >> (5u * b)) & 31u;
-      const u32 hb = f ? 31u - (u32)__builtin_clz(f) : 0u;  // ceil(lmax / 4)
-      nsm |= (hb <= 1u ? 2u : 1u + hb) << (4u * b);
     }
     WAVE_SYNC();
     STAMP(1);
@@ -2821,34 +2708,24 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
       }
     }
     fl.wbase = w;
-#ifdef FX_OR
     // the records' ring bytes [16, 16 + 8 ntot) back to zero for the OR rounds
     for (u32 i = 1 + lane; i <= (ntot + sh + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
     WAVE_SYNC();
-#endif
     STAMP(2);
-#if FX_PFM
     // the next window's metadata, loaded under this window's rounds (the window's own
     // metadata registers are dead from here on)
     const u64 gnext = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
     M = fx_meta(a, w + k);
-#endif
     // ---- rounds ----
     if (!(FX_ABL & 8))
     {
       if (DIG != 0 && dslot) fxd_rounds<DIG == 1>(F, ring, a, w, T, k, rw, m2, m3, m4);
-      else if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4, nsm);
-      else fx_rounds<1>(F, ring, R, fl, T, k, rw, m2, m3, m4, nsm);
+      else if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4);
+      else fx_rounds<1>(F, ring, R, fl, T, k, rw, m2, m3, m4);
     }
     STAMP(3);
-#if FX_PFM
     g = gnext;
     w += k;
-#else
-    g = min(g1, uniform64(shfl_u64(c1, (int)k - 1)));
-    w += k;
-    M = fx_meta(a, w);
-#endif
     WAVE_SYNC();
   }
   if (!DIG) fx_close(R, ring, a);
@@ -2863,7 +2740,7 @@ __device__ __forceinline__ void expand_fast_body(const ExpArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 wv = threadIdx.x / 64, nwv = blockDim.x / 64;
   uint8_t* mine = smem + wv * lds_per_wave_fast();
-  u32* ring = (u32*)(mine + FX_TRASH);  // (fx8_put: 4 writable bytes in front of the ring)
+  u32* ring = (u32*)(mine + FX_TRASH);
   FXWin& F = *(FXWin*)(mine + FX_TRASH + FX_RING);
   const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
   if (chunk * a.CH >= a.cand_end) return;

@@ -955,14 +955,14 @@ __device__ void m_pos_expand(SL& S, const MT& T, const MInfo& I, const A5xModeLa
     }
     const u32 incl = m_incl_scan(len);
     const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
-    u32 P = ringa + (u32)(pos - B) + incl - len, sink = 0;
+    u32 P = ringa + (u32)(pos - B) + incl - len;
     if (len) {
       for (u32 k = 0; k < ntok; k++) {
         const u32 d = S.tok[k], pi = d >> 16;
         const u32 ix = (d & 0xFFFFu) + (pi ? (rev ? (u32)(sel >> (pi - 1)) & 1u : (u32)(sel >> (4 * (pi - 1))) & 15u) : 0u);
-        fx7_put(S.ent[ix], P, sink);
+        fx7_put(S.ent[ix], P);
       }
-      fx7_put(nl, P, sink);
+      fx7_put(nl, P);
     }
     pos += tot;
     M_WAVE_SYNC();
@@ -1454,12 +1454,12 @@ __device__ void m_pos_digest(SL& S, const MT& T, const MInfo& I, const A5xModeLa
     }
     if (a.dg_algo == A5X_ALGO_MD5 && !__builtin_amdgcn_ballot_w64(t < te && len > 55u)) {
       // every leaf fits one MD5 block: one 64-byte slot per lane (m_slot_md5_probe)
-      u32 P = ringa + 64u * lane, sink = 0;
+      u32 P = ringa + 64u * lane;
       if (t < te && len) {
         for (u32 k = 0; k < ntok; k++) {
           const u32 d = S.tok[k], pi = d >> 16;
           const u32 ix = (d & 0xFFFFu) + (pi ? (rev ? (u32)(sel >> (pi - 1)) & 1u : (u32)(sel >> (4 * (pi - 1))) & 15u) : 0u);
-          fx7_put(S.ent[ix], P, sink);
+          fx7_put(S.ent[ix], P);
         }
       }
       m_slot_md5_probe<64>(a, ringa + 64u * lane, len, t < te, w, t);
@@ -1468,12 +1468,12 @@ __device__ void m_pos_digest(SL& S, const MT& T, const MInfo& I, const A5xModeLa
     const u32 incl = m_incl_scan(len);
     const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
     const u32 o = incl - len;
-    u32 P = ringa + o, sink = 0;
+    u32 P = ringa + o;
     if (t < te && len) {
       for (u32 k = 0; k < ntok; k++) {
         const u32 d = S.tok[k], pi = d >> 16;
         const u32 ix = (d & 0xFFFFu) + (pi ? (rev ? (u32)(sel >> (pi - 1)) & 1u : (u32)(sel >> (4 * (pi - 1))) & 15u) : 0u);
-        fx7_put(S.ent[ix], P, sink);
+        fx7_put(S.ent[ix], P);
       }
     }
     M_WAVE_SYNC();

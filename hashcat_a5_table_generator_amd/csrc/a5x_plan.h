@@ -373,11 +373,19 @@ struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
   A5X_HD void desc(u32 i, u64 v) { rec[1 + i] = v; }
 };
 
-#ifndef PL_FIXED_TRIP
-#define PL_FIXED_TRIP 0  // 1: CAP-iteration entry loops for every group (A/B)
-#endif
 #ifndef PL_SPLIT_CAP
 #define PL_SPLIT_CAP 8   // groups of <= this many entries merge read-all-then-write-all (registers)
+#endif
+// "some lane of the wave still needs iteration t" (the host runs one word: its own test);
+// the unrolled CAP-entry loops of the register merge stop at the wave's largest group
+// instead of running all CAP iterations
+#ifndef PL_EARLY
+#define PL_EARLY 1
+#endif
+#ifdef __HIP_DEVICE_COMPILE__
+#define PL_ANY(x) (!PL_EARLY || __builtin_amdgcn_ballot_w64(x) != 0)
+#else
+#define PL_ANY(x) (x)
 #endif
 
 // Cut a unit-radix word into pieces (see the record format above), one unit at a
@@ -435,7 +443,7 @@ struct Planner {
   }
   A5X_HD void close_group() {
     if constexpr (BUILD) {
-      for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : cR); a++)
+      for (u32 a = 0; a < cR; a++)
         if (a < cR) sk.ent(P.ne + a, sk.gld(P.ne, a));
       sk.desc(cpi, fr_desc(cR, P.ne));
     }
@@ -480,13 +488,15 @@ struct Planner {
         u32 cl[CAP];
 #pragma unroll
         for (u32 t = 0; t < CAP; t++) {
+          cl[t] = 0; ov[t] = 0; cv[t] = 0;
+          if (!PL_ANY(t < nR)) break;
           const u32 a2 = (t * inv) >> 8, a1 = t - a2 * cR;
-          cl[t] = 0;
           ov[t] = t < nR ? sk.gld(P.ne, a1) : 0ull;
           cv[t] = t < nR ? unit_choice_b(wd, U, T, a2, cl[t], cb, cs) : 0ull;
         }
 #pragma unroll
         for (u32 t = 0; t < CAP; t++) {
+          if (!PL_ANY(t < nR)) break;
           if (t < nR) {
             const u32 ol = fw_len(ov[t]);
             const u64 v = (ov[t] & FW_M56) | (rb << (8 * ol)) | (cv[t] << (8 * (ol + run)));
@@ -496,7 +506,7 @@ struct Planner {
       } else if constexpr (BUILD) {
         const u64 rb = run ? wd.ld(prev, run) : 0ull;
         const u32 inv = (256u + cR - 1u) / cR;  // t / cR = (t * inv) >> 8 for t < 16
-        for (int t = (PL_FIXED_TRIP ? CAP : nR) - 1; t >= 0; t--) {
+        for (int t = nR - 1; t >= 0; t--) {
           if ((u32)t >= nR) continue;
           const u32 a2 = ((u32)t * inv) >> 8, a1 = (u32)t - a2 * cR;
           u32 cl = 0;
@@ -524,15 +534,18 @@ struct Planner {
         u32 cl[CAP];
 #pragma unroll
         for (u32 a = 0; a < CAP; a++) {
-          cl[a] = 0;
+          cl[a] = 0; cv[a] = 0;
+          if (!PL_ANY(a < Ru)) break;
           cv[a] = a < Ru ? unit_choice_b(wd, U, T, a, cl[a], cb, cs) : 0ull;
         }
 #pragma unroll
-        for (u32 a = 0; a < CAP; a++)
+        for (u32 a = 0; a < CAP; a++) {
+          if (!PL_ANY(a < Ru)) break;
           if (a < Ru) sk.gst(P.ne, a, ((rb | (cv[a] << (8 * rem))) & FW_M56) | fw_meta(rem + cl[a], Ru));
+        }
       } else if constexpr (BUILD) {
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
-        for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : Ru); a++) {
+        for (u32 a = 0; a < Ru; a++) {
           if (a >= Ru) continue;
           u32 cl = 0;
           const u64 cv = unit_choice_b(wd, U, T, a, cl, cb, cs);
@@ -549,7 +562,7 @@ struct Planner {
     if (open && cmax + tl <= FW_PLEN) {
       if constexpr (BUILD) {
         const u64 tb = (run ? wd.ld(prev, run) : 0ull) | (10ull << (8 * run));
-        for (u32 a = 0; a < (PL_FIXED_TRIP ? CAP : cR); a++) {
+        for (u32 a = 0; a < cR; a++) {
           if (a >= cR) continue;
           const u64 old = sk.gld(P.ne, a);
           const u32 ol = fw_len(old);

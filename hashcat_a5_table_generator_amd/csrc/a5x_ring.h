@@ -9,10 +9,6 @@
 #pragma once
 #include <stdint.h>
 
-#ifndef FX_MASKOR
-#define FX_MASKOR 0  // 1: exec-mask each ds_or slot to the lanes whose piece reaches it
-#endif
-
 // LDS byte addresses as plain uint32_t (ds_* instructions take a VGPR address + an offset)
 typedef __attribute__((address_space(3))) uint32_t fx6_lds32;
 __device__ __forceinline__ uint32_t fx6_addr(const void* p) {
@@ -49,67 +45,31 @@ __device__ __forceinline__ void fx7_or(uint32_t a, uint32_t v) {
   __hip_atomic_fetch_or((fx6_lds32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
-// (NOOR: timing ablation (FX_ABL & 64 builds) -- the dwords are folded into sink
-// instead of stored)
-template <bool NOOR = false>
-__device__ __forceinline__ void fx7_put(const uint4 e, uint32_t& P, uint32_t& sink) {
+__device__ __forceinline__ void fx7_put(const uint4 e, uint32_t& P) {
   const uint32_t n = P & 3u, base = P - n;
   const uint32_t l = e.w >> 24, e3 = e.w & 0xFFFFFFu;
   const uint32_t sel = fx6_sel(n);
   const uint32_t t = n + l;
-  auto put = [&](uint32_t a, uint32_t v) {
-    if constexpr (NOOR) sink ^= v + a;
-    else fx7_or(a, v);
-  };
-#if FX_MASKOR
-  // Only the lanes whose piece reaches a slot take part in its ds_or: masked lanes do not
-  // enter the bank arbitration, so the random-address conflicts of a slot that few lanes
-  // need shrink (ring ORs land on data-dependent addresses: ~3.5-way per 32-lane group).
-  if (l) put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
-  if (t > 4u) put(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
-  if (__builtin_amdgcn_ballot_w64(t > 8u)) {
-    if (t > 8u) put(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
-    if (__builtin_amdgcn_ballot_w64(t > 12u)) {
-      if (t > 12u) put(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
-      if (t > 16u) put(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
-    }
-  }
-#elif defined(FX_WRS)
-  // (timing variants, wrong output: 1 slots >= 1 plain writes of the lanes reaching them,
-  // 2 slots >= 1 plain writes of every lane, 3 every slot a plain write)
-  if (FX_WRS == 3) fx6_st(base, __builtin_amdgcn_perm(e.x, 0u, sel));
-  else put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
-  if (FX_WRS != 1 || t > 4u) fx6_st(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
-  if (__builtin_amdgcn_ballot_w64(t > 8u)) {
-    if (FX_WRS != 1 || t > 8u) fx6_st(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
-    if (__builtin_amdgcn_ballot_w64(t > 12u)) {
-      if (FX_WRS != 1 || t > 12u) fx6_st(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
-      if (__builtin_amdgcn_ballot_w64(t > 16u))
-        if (FX_WRS != 1 || t > 16u) fx6_st(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
-    }
-  }
-#else
-  put(base, __builtin_amdgcn_perm(e.x, 0u, sel));
-  put(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
+  fx7_or(base, __builtin_amdgcn_perm(e.x, 0u, sel));
+  fx7_or(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
   if (__builtin_amdgcn_ballot_w64(t > 8u)) {  // pieces reaching a third dword (wave-uniform)
-    put(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
+    fx7_or(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
     if (__builtin_amdgcn_ballot_w64(t > 12u)) {
-      put(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
-      if (__builtin_amdgcn_ballot_w64(t > 16u)) put(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
+      fx7_or(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
+      if (__builtin_amdgcn_ballot_w64(t > 16u)) fx7_or(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
     }
   }
-#endif
   P += l;
 }
 
-// fx8_put: fx7_put with v_alignbyte shifts and the dword count decided per window.
-// P1 = (LDS byte address of the piece) - 1, so that base = P1 & ~3 and the alignbyte
-// shift (~P1) & 3 = (4 - n) & 3 need no selector build; for n = P & 3 = 0 the five
-// slots cover [P - 4, P + 16) (slot 0 ORs zero into the dword before P: the ring
-// therefore needs 4 writable bytes in front of it).  Slot k >= 2 is written when
-// ns > k (ns: wave-uniform, from the longest entry of the piece over the window,
-// so the compare is scalar); slots past a piece's bytes receive zeros.  The entry's
-// byte 15 (its length) never reaches slots 0-3; slot 4 masks it.
+// fx8_put: fx7_put with v_alignbyte shifts and the dword count decided per piece group
+// (the -s / -s -r positional engine, a5x_modes.hip).  P1 = (LDS byte address of the
+// piece) - 1, so that base = P1 & ~3 and the alignbyte shift (~P1) & 3 = (4 - n) & 3 need
+// no selector build; for n = P & 3 = 0 the five slots cover [P - 4, P + 16) (slot 0 ORs
+// zero into the dword before P: the ring needs 4 writable bytes in front of it).  Slot
+// k >= 2 is written when ns > k (ns: wave-uniform, from the longest entry of the piece,
+// so the compare is scalar); slots past a piece's bytes receive zeros.  The entry's byte
+// 15 (its length) never reaches slots 0-3; slot 4 masks it.
 __device__ __forceinline__ void fx8_put(const uint4 e, uint32_t& P1, uint32_t ns) {
   const uint32_t base = P1 & ~3u, s = ~P1;
   fx7_or(base, __builtin_amdgcn_alignbyte(e.x, 0u, s));
@@ -124,7 +84,8 @@ __device__ __forceinline__ void fx8_put(const uint4 e, uint32_t& P1, uint32_t ns
   P1 += e.w >> 24;
 }
 
-// slots fx8_put needs for a piece whose longest entry has lmax bytes (n + lmax <= 4 ns
-// for every n in [1, 4]: ns = 1 + ceil(lmax / 4), at least 2)
+// ring dwords a piece whose longest entry has lmax bytes can touch after a byte offset
+// n in [1, 4] (n + lmax <= 4 ns: ns = 1 + ceil(lmax / 4), at least 2; the -s / -s -r
+// positional engine sizes its placement loops with it)
 __device__ __forceinline__ uint32_t fx8_slots(uint32_t lmax) { return lmax <= 4u ? 2u : 1u + ((lmax + 3u) >> 2); }
 
