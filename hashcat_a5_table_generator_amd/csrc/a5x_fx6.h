@@ -1,5 +1,5 @@
 // a5x_fx6.h -- round machinery of k_expand_fast (device only; included by
-// a5x_kernels.hip and tools/mb_rounds.hip).
+// a5x_kernels.hip).
 //
 // A window holds the big-piece entries of up to FX_WW consecutive FAST words in LDS
 // (a5x_plan.h: a word's candidate n <-> the mixed-radix digits of n + 1 over its big
