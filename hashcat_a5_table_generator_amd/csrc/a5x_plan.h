@@ -376,17 +376,7 @@ struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
 #ifndef PL_SPLIT_CAP
 #define PL_SPLIT_CAP 8   // groups of <= this many entries merge read-all-then-write-all (registers)
 #endif
-// "some lane of the wave still needs iteration t" (the host runs one word: its own test);
-// the unrolled CAP-entry loops of the register merge stop at the wave's largest group
-// instead of running all CAP iterations
-#ifndef PL_EARLY
-#define PL_EARLY 1
-#endif
-#ifdef __HIP_DEVICE_COMPILE__
-#define PL_ANY(x) (!PL_EARLY || __builtin_amdgcn_ballot_w64(x) != 0)
-#else
-#define PL_ANY(x) (x)
-#endif
+
 
 // Cut a unit-radix word into pieces (see the record format above), one unit at a
 // time (unit() in word order, then finish()).  BUILD: also write the entries and
@@ -488,15 +478,13 @@ struct Planner {
         u32 cl[CAP];
 #pragma unroll
         for (u32 t = 0; t < CAP; t++) {
-          cl[t] = 0; ov[t] = 0; cv[t] = 0;
-          if (!PL_ANY(t < nR)) break;
           const u32 a2 = (t * inv) >> 8, a1 = t - a2 * cR;
+          cl[t] = 0;
           ov[t] = t < nR ? sk.gld(P.ne, a1) : 0ull;
           cv[t] = t < nR ? unit_choice_b(wd, U, T, a2, cl[t], cb, cs) : 0ull;
         }
 #pragma unroll
         for (u32 t = 0; t < CAP; t++) {
-          if (!PL_ANY(t < nR)) break;
           if (t < nR) {
             const u32 ol = fw_len(ov[t]);
             const u64 v = (ov[t] & FW_M56) | (rb << (8 * ol)) | (cv[t] << (8 * (ol + run)));
@@ -534,15 +522,12 @@ struct Planner {
         u32 cl[CAP];
 #pragma unroll
         for (u32 a = 0; a < CAP; a++) {
-          cl[a] = 0; cv[a] = 0;
-          if (!PL_ANY(a < Ru)) break;
+          cl[a] = 0;
           cv[a] = a < Ru ? unit_choice_b(wd, U, T, a, cl[a], cb, cs) : 0ull;
         }
 #pragma unroll
-        for (u32 a = 0; a < CAP; a++) {
-          if (!PL_ANY(a < Ru)) break;
+        for (u32 a = 0; a < CAP; a++)
           if (a < Ru) sk.gst(P.ne, a, ((rb | (cv[a] << (8 * rem))) & FW_M56) | fw_meta(rem + cl[a], Ru));
-        }
       } else if constexpr (BUILD) {
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
         for (u32 a = 0; a < Ru; a++) {
