@@ -2070,7 +2070,9 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #endif
                       // during the window setup bytes [16, 16 + 8 FX_WREC) hold the window's
                       // small records (ring block 0 keeps the run's partial block)
+#ifndef FX_TRASH
 #define FX_TRASH 256  // (unused gap in front of the ring; keeps the measured LDS layout)
+#endif
 #ifndef FX_WW
 #define FX_WW 32      // window words
 #endif
@@ -2294,6 +2296,9 @@ struct FxDigest {
 // the UTF-8 walk of ntlm_stream is left to windows that cannot take the slots.
 // ---------------------------------------------------------------------------
 #define FXD_MAXL 56u  // slot path: candidate + '\n' (NTLM: UTF-16LE bytes + "\n\0") <= 56 B
+#ifndef FXD_NWSPEC
+#define FXD_NWSPEC 1  // slot rounds specialised by the window's message words (8 / 12 / 14)
+#endif
 
 
 // One rune of Go's utf8.DecodeRune from the 4 bytes x (avail of them belong to the
@@ -2352,8 +2357,11 @@ __device__ __forceinline__ uint4 fx_utf16_entry(const uint4 e, bool& ok) {
 }
 
 // One round of the slot path: lane L < nr takes window candidate rr + L (one candidate
-// per run), places it at ring + 64 L, hashes the slot and probes the target set.
-template <int NB, bool MD5>
+// per run), places it at ring + 64 L, hashes the slot and probes the target set.  NW:
+// message words that can be non-zero (the window's longest message, with its pad byte,
+// fits 4 NW bytes): words NW .. 13 are compile-time zeros, so their MD adds fold away
+// and their slot quads are neither read nor cleared.
+template <int NB, bool MD5, int NW>
 __device__ __forceinline__ void fxd_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
                                           u32 rr, u32 j, bool act, const ExpArgs& a, u64 wbase) {
   const u32 lane = lane_id();
@@ -2379,16 +2387,20 @@ __device__ __forceinline__ void fxd_round(const uint4* be, const uint4 (*wq)[2],
     fx7_xor(pb & ~3u, 0x8Au << (8u * (pb & 3u)));
   }
   WAVE_SYNC();
+  static_assert(NW == 8 || NW == 12 || NW == 14, "message word classes");
+  constexpr int NQ = (NW + 3) / 4;  // slot quads that can hold message bytes
   u32 M[16];
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
+  for (int q = 0; q < NQ; q++) {
     const uint4 v = fx6_ld16(slot + 16u * q);
     M[4 * q] = v.x; M[4 * q + 1] = v.y; M[4 * q + 2] = v.z; M[4 * q + 3] = v.w;
   }
+#pragma unroll
+  for (int q = NW; q < 14; q++) M[q] = 0u;
   M[14] = on ? (len - TL) << 3 : 0u;
   M[15] = 0u;
 #pragma unroll
-  for (int q = 0; q < 4; q++) fx6_st16(slot + 16u * q, make_uint4(0, 0, 0, 0));  // zero again for the next round
+  for (int q = 0; q < NQ; q++) fx6_st16(slot + 16u * q, make_uint4(0, 0, 0, 0));  // zero again for the next round
   u32 h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
 #if FX_DABL & 1
   h[0] ^= M[0] + M[14]; h[1] ^= M[1]; h[2] ^= M[2]; h[3] ^= M[3];
@@ -2414,7 +2426,7 @@ __device__ __forceinline__ void fxd_round(const uint4* be, const uint4 (*wq)[2],
 }
 
 // The window's candidates (T of them) in rounds of 64 on the slot path.
-template <bool MD5>
+template <bool MD5, int NW>
 __device__ __forceinline__ void fxd_rounds(FXWin& F, u32* ring, const ExpArgs& a, u64 wbase, u32 T, u32 k, u32 rw,
                                            u64 m2, u64 m3, u64 m4) {
   const u32 lane = lane_id();
@@ -2426,10 +2438,10 @@ __device__ __forceinline__ void fxd_rounds(FXWin& F, u32* ring, const ExpArgs& a
     const bool act = lane < nr;
     const u32 jl = readlane_u32(j, nr - 1u);
     const u64 span = ((2ull << (jl - jcur)) - 1ull) << jcur;  // words jcur .. jl
-    if (span & m4) fxd_round<4, MD5>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
-    else if (span & m3) fxd_round<3, MD5>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
-    else if (span & m2) fxd_round<2, MD5>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
-    else fxd_round<1, MD5>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
+    if (span & m4) fxd_round<4, MD5, NW>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
+    else if (span & m3) fxd_round<3, MD5, NW>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
+    else if (span & m2) fxd_round<2, MD5, NW>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
+    else fxd_round<1, MD5, NW>(F.be, F.wq, F.rb, F.re, ringa, rr, j, act, a, wbase);
   }
 }
 
@@ -2719,7 +2731,13 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     // ---- rounds ----
     if (!(FX_ABL & 8))
     {
-      if (DIG != 0 && dslot) fxd_rounds<DIG == 1>(F, ring, a, w, T, k, rw, m2, m3, m4);
+      if (DIG != 0 && dslot) {
+        // message bytes of the window's longest candidate ('\n' -> pad; NTLM: UTF-16LE)
+        const u32 mb = FXD_NWSPEC ? (DIG == 1 ? winmax : 2u * winmax) : FXD_MAXL;
+        if (mb <= 32u) fxd_rounds<DIG == 1, 8>(F, ring, a, w, T, k, rw, m2, m3, m4);
+        else if (mb <= 48u) fxd_rounds<DIG == 1, 12>(F, ring, a, w, T, k, rw, m2, m3, m4);
+        else fxd_rounds<DIG == 1, 14>(F, ring, a, w, T, k, rw, m2, m3, m4);
+      }
       else if (K == FX_K) fx_rounds<FX_K>(F, ring, R, fl, T, k, rw, m2, m3, m4);
       else fx_rounds<1>(F, ring, R, fl, T, k, rw, m2, m3, m4);
     }
