@@ -27,6 +27,7 @@
 #include "a5x_plan.h"
 #include "a5x_gosem.h"
 #include "a5x_launch.h"
+#include "a5x_md.h"
 
 namespace {
 
@@ -2190,7 +2191,13 @@ int a5x_set_targets(a5x_ctx* c, int algo, const uint8_t* dig, uint64_t n) {
     memcpy(d, dig + 16 * i, 16);
     if ((d[0] | d[1] | d[2] | d[3]) == 0) { has_zero = 1; continue; }
     const uint32_t bi = d[0] & (uint32_t)((1ull << bm_log2) - 1);
-    bm[bi >> 5] |= 1u << (bi & 31);
+    if (MD_BLOOM2) {  // (a5x_md.h md_probe: the 64-bit word of bi, two bits from word 1)
+      const uint64_t m = md_bloom_bits(d[1]);
+      bm[(bi >> 6) * 2] |= (uint32_t)m;
+      bm[(bi >> 6) * 2 + 1] |= (uint32_t)(m >> 32);
+    } else {
+      bm[bi >> 5] |= 1u << (bi & 31);
+    }
     for (uint64_t slot = tgt_slot(d, tmask);; slot = (slot + 1) & tmask) {
       uint4& e = tab[slot];
       if (e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3]) break;  // duplicate

@@ -2551,7 +2551,8 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     const bool fast = (fl_ & A5X_WF_FAST) && c0 < g1;
     const u32 rs = (fast && hasc) ? ff_rsize(fl_) : 0u;
     const u32 incR = wave_incl_scan_u32(rs);
-    // records must be one contiguous range (complex words have slots elsewhere)
+    // records must be one contiguous range (complex words have slots elsewhere; a
+    // gathered per-word copy that let them join windows measured 8.81 vs 8.65 ms on C3)
     const u64 rm = __ballot(rs > 0);
     const u32 rbase = readlane_u32(M.roff, rm ? (u32)__builtin_ctzll(rm) : 0u);
     const bool contig = rs == 0 || M.roff == rbase + (incR - rs);
