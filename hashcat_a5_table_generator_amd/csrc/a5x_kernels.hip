@@ -711,7 +711,10 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
                      // keyspace 27.1 vs 29.2 ms, the same words split, expansion unchanged; 2: most
                      // words past 8 pieces)
 #endif
-#define VS_BLOCK 64  // k_keyspace_vsub workgroup (LDS per lane ~340 B: 7 one-wave workgroups per CU)
+#ifndef VS_BLOCK
+#define VS_BLOCK 128 // k_keyspace_vsub workgroup: two waves share the table copy (C5 -s A/B, profiles/r05r_ab_vsub_block_c5.txt:
+                     // 16.98 ms vs 17.85 ms at 64, 17.19 at 256)
+#endif
 
 struct VsWord {
   u32 L, nocc, nt, S;
@@ -863,8 +866,8 @@ struct VsRecSink {
 __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(VS_WPE))) k_keyspace_vsub(KsArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 tb = (a.table_bytes + 15u) & ~15u;
-  u64* gbuf = (u64*)(smem + tb);                                 // VS_BLOCK x KS_GCAP open-group entries
-  uint8_t* wsl = smem + tb + VS_BLOCK * KS_GCAP * 8;             // VS_BLOCK x VS_WSLOT word bytes
+  u64* gbuf = (u64*)(smem + tb);                                 // VS_BLOCK x VS_GCAP open-group entries
+  uint8_t* wsl = smem + tb + VS_BLOCK * VS_GCAP * 8;             // VS_BLOCK x VS_WSLOT word bytes
   uint8_t* ssl = wsl + VS_BLOCK * VS_WSLOT;                      // VS_BLOCK x VS_SLOT sub-word bytes
   uint16_t* occ0 = (uint16_t*)(ssl + VS_BLOCK * VS_SLOT);        // VS_OCC x VS_BLOCK occurrences
   VsWave* wvs = (VsWave*)(occ0 + VS_BLOCK * VS_OCC);             // one per wave
@@ -2988,7 +2991,7 @@ size_t a5x_keyspace_rprobe_lds(u32 table_bytes) {
 }
 
 size_t a5x_keyspace_vsub_lds(u32 table_bytes) {
-  return ((table_bytes + 15u) & ~15u) + VS_BLOCK * (KS_GCAP * 8 + VS_WSLOT + VS_SLOT + VS_OCC * 2) +
+  return ((table_bytes + 15u) & ~15u) + VS_BLOCK * (VS_GCAP * 8 + VS_WSLOT + VS_SLOT + VS_OCC * 2) +
          (VS_BLOCK / 64) * sizeof(VsWave);
 }
 
