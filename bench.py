@@ -234,12 +234,21 @@ def cpu_model() -> str:
 
 
 def cpu_threads() -> int:
-    """Every core this process may use (its CPU affinity; on the GPU box nproc shows the
-    whole machine, of which one GPU's share is 16)."""
+    """Every core this process may use: its CPU affinity, capped by the cgroup CPU quota
+    (on the GPU box the affinity lists the whole machine, 256 CPUs, but cpu.max grants 16:
+    256 workers on 16 CPUs of quota ran the C port at 0.05 Mcand/s)."""
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        n = max(1, len(os.sched_getaffinity(0)))
     except AttributeError:
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_quota() -> str:
@@ -269,18 +278,22 @@ def cpu_baseline(tables, args):
     fd = os.open(os.devnull, os.O_WRONLY)
     runs = []
     for th in thread_counts():
-        nwords = args.cpu_sample_words
+        # past 16 workers the one shared channel (the reference's) serialises them and every
+        # extra worker only adds contention: the sample shrinks with the worker count so the
+        # all-cores run stays a few seconds (the rate, not the sample, is reported)
+        nwords = max(2000, args.cpu_sample_words * 16 // max(16, th))
         _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
         t0 = time.perf_counter()
         c, b = t.run_pipeline(data, offs, args.mode, args.min, args.max, th, fd)
         dt = time.perf_counter() - t0
-        runs.append({"threads": th, "value": c / dt, "seconds": dt, "candidates": c})
-        log(f"cpu baseline threads={th}: {c / dt / 1e6:.2f} Mcand/s ({dt:.2f} s)")
+        runs.append({"threads": th, "value": c / dt, "seconds": dt, "candidates": c, "words": nwords})
+        log(f"cpu baseline threads={th}: {c / dt / 1e6:.2f} Mcand/s ({dt:.2f} s, {nwords} words)")
     os.close(fd)
     best = max(runs, key=lambda r: r["value"])
     return {"value": best["value"], "unit": "candidates/s", "cores": best["threads"], "kind": "port",
             "cpu_model": cpu_model(), "cpu_affinity": cpu_threads(), "cpu_quota": cpu_quota(), "runs": runs,
-            "sample": f"{args.cpu_sample_words} words of workload {args.workload} (seed 0xC0FFEE) to /dev/null; "
+            "sample": f"{args.cpu_sample_words} words of workload {args.workload} (seed 0xC0FFEE; past 16 workers "
+                      f"{args.cpu_sample_words} x 16 / workers) to /dev/null; "
                       f"C restatement of main.go (oracle/a5_oracle.c) with its goroutine pool, 1000-slot channel "
                       f"(lock-free ring; a blocked sender or receiver spins briefly, then parks on a futex like a "
                       f"goroutine) and one 4 KiB writer; runs at {[r['threads'] for r in runs]} worker thread(s), "
@@ -346,7 +359,11 @@ def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
         if prof["_sha_match"]:  # int ops per candidate count only for the sources they were measured on
             ach = prof["int_ops_per_cand"] * tc / (ms_stage * 1e-3) / 1e12
             r.update(achieved=ach, frac=ach / peak, int_ops_per_cand=prof["int_ops_per_cand"],
-                     valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"))
+                     valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"),
+                     valu_cycles_per_inst=prof.get("valu_cycles_per_inst"), eff_clock_ghz=prof.get("eff_clock_ghz"))
+            if prof.get("eff_clock_ghz"):  # the same VOP3 issue rate at the clock the chip held
+                pk = 256 * 4 * 16 * prof["eff_clock_ghz"] * 1e9 / 1e12
+                r.update(peak_at_eff_clock=pk, frac_at_eff_clock=ach / pk)
         else:
             r.update(frac_from_stale_profile=True, stale_int_ops_per_cand=prof["int_ops_per_cand"])
     return r

@@ -78,6 +78,15 @@ res = {
     "active_valu_per_wave_cycle": sum(c1.get("SQ_ACTIVE_INST_VALU", [0])) / max(1.0, sum(c1.get("SQ_WAVE_CYCLES", [1]))),
     "kernel_avg_us": float(dig["AverageNs"]) / 1e3 if dig else None,
     "kernel_calls": int(dig["Calls"]) if dig else None,
+    # SQ_ACTIVE_INST_VALU counts quad-cycles: x 4 / instructions = issue cycles per wave64
+    # VALU instruction (2 for VOP2 ops, 4 for VOP3: profiles/r05_mb_valu.txt)
+    "valu_cycles_per_inst": 4.0 * sum(c1.get("SQ_ACTIVE_INST_VALU", [0])) / max(1.0, valu),
+    # effective shader clock over the profiled dispatches (GRBM_GUI_ACTIVE sums the 8 XCDs;
+    # MI355X_MICROARCH.md 'DVFS give-back'), from the kernel's average duration in the
+    # kernel-trace pass of the same workload
+    "dispatches_counted": len(c1.get("GRBM_GUI_ACTIVE", [])),
+    "eff_clock_ghz": (sum(c1["GRBM_GUI_ACTIVE"]) / 8.0 / (len(c1["GRBM_GUI_ACTIVE"]) * float(dig["AverageNs"])))
+                     if dig and c1.get("GRBM_GUI_ACTIVE") else None,
     "note": "SQ_INSTS_VALU summed over the %s dispatches of one step (1 step, 0 warmup; the "
             "planted-target setup adds ~1e6 candidates); int_ops = wave instructions x 64 lanes" % kname,
 }
