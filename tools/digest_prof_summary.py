@@ -85,8 +85,9 @@ res = {
     # MI355X_MICROARCH.md 'DVFS give-back'), from the kernel's average duration in the
     # kernel-trace pass of the same workload
     "dispatches_counted": len(c1.get("GRBM_GUI_ACTIVE", [])),
+    # (one kernel only: a "+" stage mixes the durations of different kernels)
     "eff_clock_ghz": (sum(c1["GRBM_GUI_ACTIVE"]) / 8.0 / (len(c1["GRBM_GUI_ACTIVE"]) * float(dig["AverageNs"])))
-                     if dig and c1.get("GRBM_GUI_ACTIVE") else None,
+                     if dig and c1.get("GRBM_GUI_ACTIVE") and "+" not in kname else None,
     "note": "SQ_INSTS_VALU summed over the %s dispatches of one step (1 step, 0 warmup; the "
             "planted-target setup adds ~1e6 candidates); int_ops = wave instructions x 64 lanes" % kname,
 }
