@@ -308,20 +308,25 @@ def digest_cpu_baseline(tables, args, targets):
     from oracle import c_oracle as co
     from hashcat_a5_table_generator_amd import synth
     t = co.CTable([os.path.join(ROOT, "tests", "golden", "tables", x + ".table") for x in tables])
-    nwords = max(50, args.cpu_sample_words // 10)
-    _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
+    # sample sized for ~10 s per run on the EPYC host (one thread: cpu_sample_words / 2 words;
+    # a pool: 4 x cpu_sample_words), the words a prefix of one seeded stream
+    nw1, nwp = max(50, args.cpu_sample_words // 2), max(50, args.cpu_sample_words * 4)
+    _, (data_all, offs_all) = synth.config_words(args.workload, max(nw1, nwp), seed=0xC0FFEE)
     algo = 0 if args.digest == "md5" else 1
     runs = []
     for th in thread_counts():
+        nwords = nw1 if th == 1 else nwp
+        offs = offs_all[:nwords + 1]
+        data = data_all[:int(offs[-1])]
         t0 = time.perf_counter()
         n, hits = t.digest_run(data, offs, args.mode, args.min, args.max, algo, targets, th)
         dt = time.perf_counter() - t0
-        runs.append({"threads": th, "value": n / dt, "seconds": dt, "candidates": n, "hits": hits})
+        runs.append({"threads": th, "value": n / dt, "seconds": dt, "candidates": n, "hits": hits, "words": nwords})
         log(f"cpu digest baseline threads={th}: {n / dt / 1e6:.3f} Mcand/s ({dt:.2f} s)")
     best = max(runs, key=lambda r: r["value"])
     return {"value": best["value"], "unit": "candidates/s", "cores": best["threads"], "kind": "port", "runs": runs,
             "cpu_model": cpu_model(), "cpu_affinity": cpu_threads(), "cpu_quota": cpu_quota(),
-            "sample": f"{nwords} words of workload {args.workload} (seed 0xC0FFEE): C restatement of main.go's "
+            "sample": f"{nw1} words (1 thread) / {nwp} words (pools) of workload {args.workload} (seed 0xC0FFEE): C restatement of main.go's "
                       f"expansion + {args.digest.upper()} in C ({'RFC 1321' if algo == 0 else 'RFC 1320 MD4 of Go UTF-16LE'})"
                       f" + probe of the same {len(targets)} targets per candidate; runs at {[r['threads'] for r in runs]}"
                       f" thread(s), the best reported"}

@@ -33,6 +33,17 @@ __global__ void __launch_bounds__(256) k_region(uint8_t* out, u64 total, u64 R) 
   }
 }
 
+// one wave per region of R bytes, store instructions on the 1 KiB-aligned address grid
+// (the region's first instruction partial): are misaligned 1 KiB instructions the cost?
+template <bool NT>
+__global__ void __launch_bounds__(256) k_region_grid(uint8_t* out, u64 total, u64 R, u64 G) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 wv = blockIdx.x * 4ull + threadIdx.x / 64;
+  const u64 b0 = wv * R, b1 = min(total, b0 + R);
+  for (u64 b = (b0 & ~(G - 1)) + 16ull * lane; b < b1; b += 1024ull)
+    if (b >= b0) st16<NT>(out + b, (v4u){(u32)b, 0u, 1u, 2u});
+}
+
 // grid-stride sweep: wave-instruction i of wave w writes KiB (i * nwaves + w)
 template <bool NT>
 __global__ void __launch_bounds__(256) k_sweep(uint8_t* out, u64 total) {
@@ -72,6 +83,21 @@ int main(int argc, char** argv) {
     }
     printf("%-44s %8.3f ms  %7.0f GB/s  frac %.3f\n", name, best, total / (best * 1e-3) / 1e9, total / (best * 1e-3) / 8e12);
   };
+  if (argc > 2) {  // alignment study only
+    for (u64 R : {140000ull, 140032ull, 140288ull, 139264ull}) {
+      const u64 nw = (total + R - 1) / R, nb = (nw + 3) / 4;
+      char nm[96];
+      snprintf(nm, sizeof nm, "region %llu B nt", (unsigned long long)R);
+      run(nm, [&] { hipLaunchKernelGGL((k_region<true, 1>), dim3(nb), dim3(256), 0, 0, out, total, R); });
+      for (u64 G : {128ull, 1024ull}) {
+        snprintf(nm, sizeof nm, "region %llu B nt, %llu-B instr grid", (unsigned long long)R, (unsigned long long)G);
+        run(nm, [&] { hipLaunchKernelGGL((k_region_grid<true>), dim3(nb), dim3(256), 0, 0, out, total, R, G); });
+        snprintf(nm, sizeof nm, "region %llu B plain, %llu-B instr grid", (unsigned long long)R, (unsigned long long)G);
+        run(nm, [&] { hipLaunchKernelGGL((k_region_grid<false>), dim3(nb), dim3(256), 0, 0, out, total, R, G); });
+      }
+    }
+    return 0;
+  }
   const u64 Rs[] = {140000, 32768, 8192, 524288};
   for (u64 R : Rs) {
     const u64 nw = (total + R - 1) / R, nb = (nw + 3) / 4;
