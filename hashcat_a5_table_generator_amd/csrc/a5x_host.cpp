@@ -835,6 +835,9 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
       K.vout_list = c->m_vl.p; K.vout_n = c->d_scalars + 15;
       K.vn = c->vn.p; K.vrsz = c->vrsz.p; K.vrec = c->vrec.p;
       K.vrec_n = (uint64_t*)(c->d_scalars + 10); K.vrec_cap = vcap;
+      if (!getenv("A5X_VSUB_LARGE_ONLY")) {  // (m_cl2 is free until k_mode_count_thread below)
+        K.vlong_list = c->m_cl2.p; K.vlong_n = c->d_scalars + 9;
+      }
       HIPCHK(c, a5x_launch_vsub(K, st));
     }
   }

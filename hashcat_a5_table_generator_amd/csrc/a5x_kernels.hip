@@ -221,6 +221,8 @@ struct KsArgs {
   u64 vrec_cap;
   uint16_t* vocc;  // per word 16 u16: the occurrence row of k_keyspace_thread's -s / -s -r words
                    // with a repeated pattern (null: none logged)
+  u32* vlong_list;  // k_keyspace_vsub small instantiation: the words for the large one
+  u32* vlong_n;
 };
 
 // -r / -s / -s -r on the FAST path (the mode-engine probe of k_keyspace_thread, rmode =
@@ -696,9 +698,18 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
 // cuts nothing: min <= 1 (the probe's condition) and #patterns <= max.
 // vrec per virtual word: its sub-words' records back to back, then one meta u64 per
 // sub-word (count | record u64 << 24 | bytes << 32); roff[w] = their base.
-#define VS_SLOT 92   // sub-word bytes per lane (sub-words <= VS_SLOT - 8 bytes; 23 dwords: lane
-                     // slots on distinct LDS banks)
+// Two instantiations by lane slot size (odd dword counts: lane slots on distinct LDS banks).
+// The small one takes words of <= VS_WSLOT_S - 4 bytes whose sub-words fit VS_SLOT_S - 8
+// and hands the rest to the large one (vlong_list); its smaller per-lane LDS admits more
+// waves per CU.  Both make the same decision for a word that fits both.
+#define VS_SLOT 92   // sub-word bytes per lane (sub-words <= VS_SLOT - 8 bytes; 23 dwords)
 #define VS_WSLOT 76  // word bytes per lane (words <= A5X_LMAX_A + over-read; 19 dwords)
+#ifndef VS_SLOT_S
+#define VS_SLOT_S 52   // small instantiation: sub-words <= 44 bytes (13 dwords)
+#endif
+#ifndef VS_WSLOT_S
+#define VS_WSLOT_S 36  // small instantiation: words <= 32 bytes (9 dwords)
+#endif
 #define VS_OCC 16    // pattern occurrences per word
 #define VS_SMAX 16   // sub-words per word
 #define VS_TMAX 4    // tied patterns per word
@@ -747,7 +758,7 @@ struct SubW {
 // occurrence goes to pl (and A) as a unit at its sub-word position.  occ: the word's
 // occurrences (q << 10 | key, strided by 256).  Returns the length, 0 when it does not
 // fit the slot.
-template <class PL>
+template <u32 SLOT, class PL>
 __device__ u32 vs_build(const Tab& T, const VsWord& V, const uint8_t* orig, uint8_t* sub, const uint16_t* occ, u32 s,
                         int rmode, PL& pl, CountAcc& A) {
   u32 ch[VS_TMAX];
@@ -767,7 +778,7 @@ __device__ u32 vs_build(const Tab& T, const VsWord& V, const uint8_t* orig, uint
   for (u32 j = 0; j < V.nocc; j++) {
     const u32 e = occ[j * VS_BLOCK];
     const u32 q = e >> 10, key = e & 1023u;
-    if (W.len() + (q - prev) + 16u > VS_SLOT - 8u) return 0;  // (values <= 15 bytes)
+    if (W.len() + (q - prev) + 16u > SLOT - 8u) return 0;  // (values <= 15 bytes)
     W.run(orig, prev, q);
     u32 ci = ~0u;
 #pragma unroll
@@ -799,7 +810,7 @@ __device__ u32 vs_build(const Tab& T, const VsWord& V, const uint8_t* orig, uint
     }
     prev = q + kl;
   }
-  if (W.len() + (V.L - prev) > VS_SLOT - 8u) return 0;
+  if (W.len() + (V.L - prev) > SLOT - 8u) return 0;
   W.run(orig, prev, V.L);
   W.sync();
   return W.len();
@@ -863,13 +874,14 @@ struct VsRecSink {
 #ifndef VS_WPE
 #define VS_WPE 3  // waves per SIMD the register budget is cut for (LDS admits ~7 one-wave workgroups per CU)
 #endif
+template <u32 WSLOT, u32 SLOT, bool SMALL>
 __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(VS_WPE))) k_keyspace_vsub(KsArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 tb = (a.table_bytes + 15u) & ~15u;
   u64* gbuf = (u64*)(smem + tb);                                 // VS_BLOCK x VS_GCAP open-group entries
-  uint8_t* wsl = smem + tb + VS_BLOCK * VS_GCAP * 8;             // VS_BLOCK x VS_WSLOT word bytes
-  uint8_t* ssl = wsl + VS_BLOCK * VS_WSLOT;                      // VS_BLOCK x VS_SLOT sub-word bytes
-  uint16_t* occ0 = (uint16_t*)(ssl + VS_BLOCK * VS_SLOT);        // VS_OCC x VS_BLOCK occurrences
+  uint8_t* wsl = smem + tb + VS_BLOCK * VS_GCAP * 8;             // VS_BLOCK x WSLOT word bytes
+  uint8_t* ssl = wsl + VS_BLOCK * WSLOT;                         // VS_BLOCK x SLOT sub-word bytes
+  uint16_t* occ0 = (uint16_t*)(ssl + VS_BLOCK * SLOT);           // VS_OCC x VS_BLOCK occurrences
   VsWave* wvs = (VsWave*)(occ0 + VS_BLOCK * VS_OCC);             // one per wave
   load_table(smem, a.table, a.table_bytes);
   __syncthreads();
@@ -878,11 +890,11 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
   VsWave& Q = wvs[wv];
   const u32 n = *a.defer_n;
   const u32 pbit = a.rmode == 2 ? 1u : 2u;
-  uint8_t* orig = wsl + tid * VS_WSLOT;
+  uint8_t* orig = wsl + tid * WSLOT;
   uint16_t* occ = occ0 + tid;
-  uint8_t* sub = ssl + tid * VS_SLOT;
+  uint8_t* sub = ssl + tid * SLOT;
   LWord lw;
-  lw.base = ssl; lw.off = tid * VS_SLOT;
+  lw.base = ssl; lw.off = tid * SLOT;
   for (u32 b0 = blockIdx.x * VS_BLOCK; b0 < n; b0 += gridDim.x * VS_BLOCK) {
     // ---- word lane: occurrences, tied patterns ----
     const u32 i = b0 + tid;
@@ -891,6 +903,8 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
     const u64 s0 = valid ? a.woff[w] : 0ull;
     const u64 L64 = valid ? a.woff[w + 1] - s0 : 0ull;
     bool ok = valid && L64 >= 1 && L64 <= A5X_LMAX_A;
+    const bool lngw = SMALL && ok && L64 > WSLOT - 4u;  // too long for this instantiation's slots
+    ok = ok && !lngw;
     VsWord V;
     V.L = ok ? (u32)L64 : 0u; V.nocc = 0; V.nt = 0; V.S = 1; V.tk = 0; V.tr = 0;
     {
@@ -900,7 +914,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
       const u32* src = (const u32*)(a.words + (s0 & ~3ull));
       const u32 sh = (u32)(s0 & 3u), nd = (V.L + 3u) / 4u;
       u32 lo = V.L ? src[0] : 0u;
-      for (u32 q = 0; q < VS_WSLOT / 4; q++) {
+      for (u32 q = 0; q < WSLOT / 4; q++) {
         const u32 hi = q < nd ? src[q + 1] : 0u;
         const u32 v = __builtin_amdgcn_alignbyte(hi, lo, sh);
         sl[q] = 4 * q + 4 <= V.L ? v : (4 * q < V.L ? keep_bytes(v, V.L - 4 * q) : 0u);
@@ -1018,7 +1032,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
         count_init(A, 0);
         NullSink ns;
         Planner<false, LWord, NullSink, VS_GCAP> pl(lw, T, ns);
-        const u32 Ls = vs_build(T, W, wsl + wl * VS_WSLOT, sub, occ0 + wl, s, a.rmode, pl, A);
+        const u32 Ls = vs_build<SLOT>(T, W, wsl + wl * WSLOT, sub, occ0 + wl, s, a.rmode, pl, A);
         u32 rs = 0;
         u64 cnt = 0, byt = 0;
         bool f = Ls != 0;
@@ -1032,7 +1046,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
           Q.u0[l] = pl.P.np | (min(rfull, 255u) << 8) | (Ls << 16);
           Q.uP[l] = (u32)min(A.P, (u64)0xFFFFFFFFu);
         }
-        if (!f) atomicOr(&Q.bad[l], 1u);
+        if (!f) atomicOr(&Q.bad[l], Ls ? 1u : 2u);  // (2: a sub-word past the lane slot)
         else {
           atomicAdd(&Q.ctot[l], (u32)min(cnt, (u64)0xFFFFFFFFu));
           atomicAdd(&Q.btot[l], (u32)min(byt, (u64)0xFFFFFFFFu));
@@ -1052,6 +1066,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
       rtot += (V.S - 1u) * rfull;
       for (u32 s = 1; s < V.S; s++) Q.tinfo[Q.tbase[lane] + s] = (uint16_t)(np | (rfull << 4));
     }
+    const bool lngs = SMALL && ok && (Q.bad[lane] & 2u);  // a sub-word past the small slot: the large one decides
     ok = ok && !Q.bad[lane] && ctot >= 1 && ctot <= a.rseg;  // (one mode-engine item, as the probe's -s words)
     const u32 mtot = ok ? rtot + V.S : 0u;
     const u32 minc = wave_incl_scan_u32(mtot);
@@ -1084,7 +1099,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
             Planner<true, LWord, VsRecSink, VS_GCAP> pb(lw, T, sk, 0u);
             CountAcc A;
             count_init(A, 0);
-            const u32 Ls = vs_build(T, W, wsl + wl * VS_WSLOT, sub, occ0 + wl, s, a.rmode, pb, A);
+            const u32 Ls = vs_build<SLOT>(T, W, wsl + wl * WSLOT, sub, occ0 + wl, s, a.rmode, pb, A);
             pb.finish(Ls);
             const Plan& P = pb.P;
             if (!Ls || !vs_fast(A, P, Ls, s == 0 ? cmin : 0u, rs, cnt, byt) || P.np != np || rs != rs0)
@@ -1105,9 +1120,14 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
       a.vn[w] = V.S - 1u;
       a.vrsz[w] = rtot;
     }
-    const bool left = valid && !ok;  // (ok without room: undecided, the host reruns)
+    const bool lng = lngw || lngs;
+    const bool left = valid && !ok && !lng;  // (ok without room: undecided, the host reruns)
     const u32 mi = wave_append(left, a.vout_n);
     if (left) a.vout_list[mi] = (u32)w;
+    if (SMALL) {
+      const u32 li = wave_append(lng, a.vlong_n);
+      if (lng) a.vlong_list[li] = (u32)w;
+    }
     WAVE_SYNC();  // (Q is rewritten by the next words)
   }
 }
@@ -2990,10 +3010,11 @@ size_t a5x_keyspace_rprobe_lds(u32 table_bytes) {
   return ((table_bytes + 15u) & ~15u) + 256 * KS_GCAP * 8 + 256 * RP_SLOT;
 }
 
-size_t a5x_keyspace_vsub_lds(u32 table_bytes) {
-  return ((table_bytes + 15u) & ~15u) + VS_BLOCK * (VS_GCAP * 8 + VS_WSLOT + VS_SLOT + VS_OCC * 2) +
+static size_t vsub_lds(u32 table_bytes, u32 wslot, u32 slot) {
+  return ((table_bytes + 15u) & ~15u) + VS_BLOCK * (VS_GCAP * 8 + wslot + slot + VS_OCC * 2) +
          (VS_BLOCK / 64) * sizeof(VsWave);
 }
+size_t a5x_keyspace_vsub_lds(u32 table_bytes) { return vsub_lds(table_bytes, VS_WSLOT, VS_SLOT); }
 
 hipError_t a5x_launch_vsub(const A5xKsLaunch& L, hipStream_t st) {
   KsArgs a;
@@ -3004,8 +3025,18 @@ hipError_t a5x_launch_vsub(const A5xKsLaunch& L, hipStream_t st) {
   a.rmode = L.rmode; a.rcmin = L.rcmin; a.rnseg = L.rnseg; a.rseg = L.rseg;
   a.vout_list = L.vout_list; a.vout_n = L.vout_n; a.vn = L.vn; a.vrsz = L.vrsz;
   a.vrec = L.vrec; a.vrec_n = (unsigned long long*)L.vrec_n; a.vrec_cap = L.vrec_cap; a.vocc = L.vocc;
-  hipLaunchKernelGGL(k_keyspace_vsub, dim3(L.defer_blocks * (256 / VS_BLOCK)), dim3(VS_BLOCK),
-                     a5x_keyspace_vsub_lds(L.table_bytes), st, a);
+  const dim3 grid(L.defer_blocks * (256 / VS_BLOCK));
+  if (L.vlong_list) {
+    // small lane slots first (more waves per CU); the words they cannot hold go to the
+    // large instantiation through vlong_list
+    a.vlong_list = L.vlong_list; a.vlong_n = L.vlong_n;
+    hipLaunchKernelGGL((k_keyspace_vsub<VS_WSLOT_S, VS_SLOT_S, true>), grid, dim3(VS_BLOCK),
+                       vsub_lds(L.table_bytes, VS_WSLOT_S, VS_SLOT_S), st, a);
+    a.defer_list = L.vlong_list; a.defer_n = L.vlong_n;
+    a.vlong_list = nullptr; a.vlong_n = nullptr;
+  }
+  hipLaunchKernelGGL((k_keyspace_vsub<VS_WSLOT, VS_SLOT, false>), grid, dim3(VS_BLOCK),
+                     vsub_lds(L.table_bytes, VS_WSLOT, VS_SLOT), st, a);
   return hipGetLastError();
 }
 
@@ -3198,7 +3229,9 @@ hipError_t a5x_set_kernel_attrs() {
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_keyspace_rprobe, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_keyspace_vsub, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  e = hipFuncSetAttribute((const void*)k_keyspace_vsub<VS_WSLOT, VS_SLOT, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_keyspace_vsub<VS_WSLOT_S, VS_SLOT_S, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_locate, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
