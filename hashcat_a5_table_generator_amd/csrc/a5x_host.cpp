@@ -148,7 +148,8 @@ struct a5x_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint64_t seg = 512;         // candidates per per-word-path segment (a radix round there costs ~64x a FAST one;
                               // C3 A/B: 512 / 256 -1 %, 4096 +8 %, 16384 +44 % -- the slow words run beside k_expand_fast)
-  uint64_t chunk = 8192;      // candidates per expand wave (sweep on C3: 8192 < 16384 < 32768 ms)
+  uint64_t chunk = 16384;     // candidates per expand wave (round-5 A/B, profiles/r05c_ab_chunk_16k.txt:
+                              // C3 expansion 8.49-8.53 vs 8.62-8.76 ms at 8192, 8.56 at 32768)
   uint32_t waves_per_block = 4;
   uint32_t waves_per_block_fast = 1;
 };
