@@ -1140,6 +1140,9 @@ int job_launch(a5x_ctx* c, const Job& J, const Range& R, uint8_t* d_out, uint64_
     if (!c->ev_join) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     HIPCHK(c, hipEventRecord(c->ev_fork, J.st));
     HIPCHK(c, hipStreamWaitEvent(c->sstream, c->ev_fork, 0));
+    // a few mode words among many FAST ones: a small grid filters the items beside k_expand_fast
+    // instead of one workgroup per 64 items (C5 -s A/B, profiles/r05g_ab_mode_items_grid_c5.txt)
+    M.grid_cap = J.B.nmode * 8 < J.nw ? 2048u : 0u;
     if (J.B.nmode) HIPCHK(c, a5x_launch_mode_items(M, 1, c->sstream));  // (every word FAST: none)
     A5xExpLaunch E = exp_launch_mode(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);
     E.cand_begin = R.cb;
@@ -1319,6 +1322,7 @@ int expand_digest(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, ui
       M.dg_hits = c->dg_hits.p; M.dg_hit_cap = (uint32_t)dev_hits; M.dg_nhits = c->d_scalars + 8;
       HIPCHK(c, hipMemsetAsync(c->d_scalars + 8, 0, 4, J.st));
       HIPCHK(c, hipEventRecord(c->ev[1], J.st));
+      M.grid_cap = J.B.nmode * 8 < J.nw ? 2048u : 0u;  // (as in job_launch)
       if (J.B.nmode && tc) HIPCHK(c, a5x_launch_mode_items(M, 2, J.st));
       if (J.B.rfast && tc) {  // -r FAST words: hashed in k_expand_fast_md5 / _ntlm's ring
         A5xExpLaunch E = exp_launch_mode(c, J.w, J.wo, J.nw, J.mn, J.mx, J.B);

@@ -1096,6 +1096,8 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
           if (np) {
             VsRecSink sk;
             sk.g = gbuf + tid; sk.rec = rb + ro; sk.np = np;
+            // (greedy big pieces: balanced ones as k_keyspace_thread builds measured +-0 here,
+            // profiles/r05g_ab_mode_items_grid_c5.txt -- sub-words rarely pass 64 combinations)
             Planner<true, LWord, VsRecSink, VS_GCAP> pb(lw, T, sk, 0u);
             CountAcc A;
             count_init(A, 0);

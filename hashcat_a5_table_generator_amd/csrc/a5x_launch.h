@@ -207,6 +207,8 @@ struct A5xModeLaunch {
   uint64_t dg_tmask;
   struct A5xHitRaw* dg_hits;
   uint32_t* dg_nhits;
+  uint32_t grid_cap;  // item kernels: workgroups at most (0: M_GRID_MAX); a few mode words among many
+                      // FAST ones are filtered by a small grid beside k_expand_fast
 };
 size_t a5x_mode_lds(uint32_t mtab_bytes);
 uint64_t a5x_mode_gslot_bytes();

@@ -2027,7 +2027,7 @@ hipError_t a5x_launch_mode_count_g(const A5xModeLaunch& L, hipStream_t st) {
 
 hipError_t a5x_launch_mode_items(const A5xModeLaunch& L, int op, hipStream_t st) {
   if (L.item_end <= L.item_begin) return hipSuccess;
-  const dim3 g(m_grid((L.item_end - L.item_begin + 63) / 64, M_GRID_MAX));  // (m_items: 64 items a step)
+  const dim3 g(m_grid((L.item_end - L.item_begin + 63) / 64, L.grid_cap ? L.grid_cap : M_GRID_MAX));  // (64 items a step)
   if (op == 0) {
     hipLaunchKernelGGL(k_mode_items_len, g, dim3(64), m_lds<MLdsC>(L.mtab_bytes), st, L);
     if (L.mode != A5X_MODE_REVERSE)
