@@ -35,6 +35,9 @@ struct A5xTableHdr {
   uint32_t off_kmatch;    // u64 kmatch[max(nkeys, 1)]: key k's first min(klen, 4) bytes | klen << 32
   uint32_t off_bucket2;   // u32 bucket2[256]: bucket[b] | bucket[b + 1] << 16 (one read per byte)
   uint32_t off_cval;      // u64 cval[nchoices]: choice's first min(len, 7) bytes | min(len, 255) << 56
+  uint32_t lead_only;     // no key starts with a UTF-8 continuation byte (0x80-0xBF): the keyspace
+                          // walk steps over them (k_keyspace_thread psk_walk)
+  uint32_t reserved[3];
 };
 
 struct A5xKey {
@@ -57,7 +60,7 @@ struct A5xChoice {
   uint16_t blob_off;      // offset in blob (valid for any len)
 };
 
-static_assert(sizeof(A5xTableHdr) == 64, "hdr");
+static_assert(sizeof(A5xTableHdr) == 80, "hdr");
 static_assert(sizeof(A5xKey) == 32, "key");
 static_assert(sizeof(A5xChoice) == 8, "choice");
 

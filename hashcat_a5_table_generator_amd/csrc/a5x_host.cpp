@@ -357,6 +357,8 @@ int compile_table(a5x_ctx* c) {
   h.max_vlen = max_vlen;
   h.has_empty_key = t.index.count(std::string()) ? 1u : 0u;
   for (int b = 0; b < 256; b++) h.max_bucket = std::max<uint32_t>(h.max_bucket, bucket[b + 1] - bucket[b]);
+  h.lead_only = 1;
+  for (int b = 0x80; b < 0xC0; b++) h.lead_only = bucket[b + 1] > bucket[b] ? 0u : h.lead_only;
   if (h.total_bytes > A5X_TABLE_LDS_MAX)
     return fail(c, A5X_E_UNSUPPORTED, "device table is %u bytes (LDS staging max %u)", h.total_bytes,
                 (unsigned)A5X_TABLE_LDS_MAX);
@@ -383,6 +385,12 @@ int compile_table(a5x_ctx* c) {
   }
   c->table_bytes = h.total_bytes;
   return A5X_OK;
+}
+
+// the compiled table's keys all start on UTF-8 lead (or ASCII) bytes (A5xTableHdr::lead_only)
+bool table_lead_only(const a5x_ctx* c) {
+  return c->blob.size() >= sizeof(A5xTableHdr) && ((const A5xTableHdr*)c->blob.data())->lead_only != 0 &&
+         !getenv("A5X_NO_UTF_WALK");
 }
 
 int upload_table(a5x_ctx* c) {
@@ -491,6 +499,7 @@ int run_keyspace(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff, uin
     K.table = c->d_table; K.table_bytes = c->table_bytes; K.words = d_words; K.woff = d_woff; K.nw = nw;
     K.mn = mn; K.mx = mx; K.count = c->count.p; K.bytes = c->bytes.p; K.flags = c->flags.p;
     K.defer_list = c->defer.p; K.defer_n = c->d_scalars; K.nbig = c->d_scalars + 1; K.err = c->d_scalars + 2;
+    K.hiflag = table_lead_only(c) ? c->d_scalars + 8 : nullptr;
     K.nslow = c->d_scalars + 3;
     K.slow_list = c->slow_list.p; K.big_list = c->big_list.p;
     K.rec = c->rec.p; K.roff = c->roff.p;
@@ -831,6 +840,7 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     K.cplx_list = c->cplx.p; K.cplx_n = c->d_scalars + 14; K.cplx_cap = (uint32_t)rcap; K.cplx_base = rtiles;
     K.defer_blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nw + 255) / 256, (uint64_t)c->cus * 2));
     K.vocc = vsub ? c->vocc.p : nullptr;
+    K.hiflag = table_lead_only(c) ? c->d_scalars + 8 : nullptr;
     HIPCHK(c, a5x_launch_keyspace(K, st));
     if (vsub) {
       K.vout_list = c->m_vl.p; K.vout_n = c->d_scalars + 15;

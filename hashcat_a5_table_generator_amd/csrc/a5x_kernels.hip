@@ -223,7 +223,20 @@ struct KsArgs {
                    // with a repeated pattern (null: none logged)
   u32* vlong_list;  // k_keyspace_vsub small instantiation: the words for the large one
   u32* vlong_n;
+  const u32* hiflag;  // k_keyspace_thread: the batch has bytes >= 0x80 (null: the byte walk only)
 };
+
+// Whether the batch's words hold bytes >= 0x80, judged on its first 256 KiB (the choice
+// only picks the faster of two exact walks: k_keyspace_thread<true> steps over UTF-8
+// continuation bytes, <false> walks every byte); one atomic per wave that saw one.
+__global__ void __launch_bounds__(256) k_hibytes(const uint8_t* words, const u64* woff, u64 nw, u32* flag) {
+  const uintptr_t b0 = (uintptr_t)(words + woff[0]) & ~(uintptr_t)3, b1 = (uintptr_t)(words + woff[nw]);
+  const u64 nd = min((u64)((b1 - b0 + 3) / 4), (u64)65536);  // (16 readable bytes past the batch)
+  const u32* d = (const u32*)b0;
+  u32 acc = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += (u64)gridDim.x * blockDim.x) acc |= d[i];
+  if (__builtin_amdgcn_ballot_w64((acc & 0x80808080u) != 0u) && lane_id() == 0) atomicOr(flag, 1u);
+}
 
 // -r / -s / -s -r on the FAST path (the mode-engine probe of k_keyspace_thread, rmode =
 // 1 / 2 / 3).  The lone units of the position-synchronous walk are the word's match
@@ -350,69 +363,87 @@ __device__ bool psk_norep;  // (psk_walk's rep when the caller does not track re
 #ifndef PSK_KB
 #define PSK_KB 2  // bucket keys read together per position (more: a loop)
 #endif
-template <bool COUNT, class PL>
+template <bool COUNT, bool UTF, class PL>
 __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 Lmax, u32 bmax, const Tab& T,
                                          PL& pl, CountAcc& A, bool& cplx, int rmode, uint16_t* ulog = nullptr,
                                          u32* nlog = nullptr, bool logrep = false, bool& rep = psk_norep) {
   u32 cur_end = 0;
   u64 seen = 0;
-  for (u32 q = 0; q < Lmax; q++) {
-    const bool act = act0 && q < L && !cplx;
-    if (act) {
-      // three dependent LDS trips per position: the word's 4 bytes, the byte's bucket, the
-      // bucket's keys (compact first-4-bytes | length records, read together)
-      const u32 w4 = lds_ld4(lw.base, lw.off + q);
-      const u32 bk = T.bucket2[w4 & 255u];
-      const u32 ks = bk & 0xFFFFu, ke = bk >> 16;
-      const u32 nk1 = T.hdr->nkeys ? T.hdr->nkeys - 1u : 0u;
-      u32 nm = 0, kk = 0;
-      u64 kmv[PSK_KB];
+  // one position q of the lane's word; returns the bytes to the next position that can
+  // start a key (UTF: the continuation bytes after q are passed over)
+  auto pos = [&](u32 q) -> u32 {
+    // three dependent LDS trips per position: the word's 4 bytes, the byte's bucket, the
+    // bucket's keys (compact first-4-bytes | length records, read together)
+    const u32 w4 = lds_ld4(lw.base, lw.off + q);
+    const u32 c1 = UTF && ((w4 >> 8) & 0xC0u) == 0x80u ? 1u : 0u;
+    const u32 c2 = c1 && ((w4 >> 16) & 0xC0u) == 0x80u ? 1u : 0u;
+    const u32 c3 = c2 && (w4 >> 30) == 2u ? 1u : 0u;
+    const u32 bk = T.bucket2[w4 & 255u];
+    const u32 ks = bk & 0xFFFFu, ke = bk >> 16;
+    const u32 nk1 = T.hdr->nkeys ? T.hdr->nkeys - 1u : 0u;
+    u32 nm = 0, kk = 0;
+    u64 kmv[PSK_KB];
 #pragma unroll
-      for (u32 i = 0; i < PSK_KB; i++) kmv[i] = T.kmatch[min(ks + i, nk1)];
-      auto test = [&](u32 k2, u64 km) {
-        const u32 kl = (u32)(km >> 32) & 0xFFFFu;
-        if (k2 < ke && q + kl <= L) {
-          if (kl > 4) {
-            cplx = true;
-          } else {
-            const u32 m = kl >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kl)) - 1u);
-            if ((w4 & m) == (u32)km) { nm++; kk = k2; }
-          }
-        }
-      };
-#pragma unroll
-      for (u32 i = 0; i < PSK_KB; i++) test(ks + i, kmv[i]);
-      for (u32 i = PSK_KB; i < bmax; i++) test(ks + i, T.kmatch[min(ks + i, nk1)]);
-      if (nm > 1 || (nm == 1 && q < cur_end)) {
-        cplx = true;
-      } else if (nm == 1 && !cplx) {
-        Unit U;
-        lone_unit(T, q, kk, U);
-        // -s / -s -r with rep: a positional pattern met again is a tied occurrence -- no
-        // unit (the word is not FAST); the walk goes on logging the occurrences for
-        // k_keyspace_vsub (seen holds key index mod 64: a collision is taken for a repeat)
-        const bool again = logrep && rmode >= 2 && ((seen >> (kk & 63u)) & 1u) &&
-                           (T.keys[kk].pad0 & (rmode == 2 ? 1u : 2u)) && T.keys[kk].nvals >= 1;
-        bool logit = again;
-        if (again) {
-          rep = true;
-          cur_end = U.e;
-        } else if (rmode && !mode_unit(T, U, rmode, seen, true)) {
-          cplx = true;
-        } else if (U.R > KS_GCAP) {
+    for (u32 i = 0; i < PSK_KB; i++) kmv[i] = T.kmatch[min(ks + i, nk1)];
+    auto test = [&](u32 k2, u64 km) {
+      const u32 kl = (u32)(km >> 32) & 0xFFFFu;
+      if (k2 < ke && q + kl <= L) {
+        if (kl > 4) {
           cplx = true;
         } else {
-          if (COUNT) count_unit(A, U);
-          if (!(KS_ABL & 2)) pl.unit(U);
-          cur_end = U.e;
-          logit = true;
-        }
-        if (COUNT && ulog && logit) {
-          const bool fits = *nlog < KS_ULOG && kk < 1024u && q < 64u;
-          if (fits) ulog[*nlog * 256u] = (uint16_t)((q << 10) | kk);
-          *nlog = fits ? *nlog + 1u : (u32)KS_ULOG + 1u;
+          const u32 m = kl >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kl)) - 1u);
+          if ((w4 & m) == (u32)km) { nm++; kk = k2; }
         }
       }
+    };
+#pragma unroll
+    for (u32 i = 0; i < PSK_KB; i++) test(ks + i, kmv[i]);
+    for (u32 i = PSK_KB; i < bmax; i++) test(ks + i, T.kmatch[min(ks + i, nk1)]);
+    if (nm > 1 || (nm == 1 && q < cur_end)) {
+      cplx = true;
+    } else if (nm == 1 && !cplx) {
+      Unit U;
+      lone_unit(T, q, kk, U);
+      // -s / -s -r with rep: a positional pattern met again is a tied occurrence -- no
+      // unit (the word is not FAST); the walk goes on logging the occurrences for
+      // k_keyspace_vsub (seen holds key index mod 64: a collision is taken for a repeat)
+      const bool again = logrep && rmode >= 2 && ((seen >> (kk & 63u)) & 1u) &&
+                         (T.keys[kk].pad0 & (rmode == 2 ? 1u : 2u)) && T.keys[kk].nvals >= 1;
+      bool logit = again;
+      if (again) {
+        rep = true;
+        cur_end = U.e;
+      } else if (rmode && !mode_unit(T, U, rmode, seen, true)) {
+        cplx = true;
+      } else if (U.R > KS_GCAP) {
+        cplx = true;
+      } else {
+        if (COUNT) count_unit(A, U);
+        if (!(KS_ABL & 2)) pl.unit(U);
+        cur_end = U.e;
+        logit = true;
+      }
+      if (COUNT && ulog && logit) {
+        const bool fits = *nlog < KS_ULOG && kk < 1024u && q < 64u;
+        if (fits) ulog[*nlog * 256u] = (uint16_t)((q << 10) | kk);
+        *nlog = fits ? *nlog + 1u : (u32)KS_ULOG + 1u;
+      }
+    }
+    return 1u + c1 + c2 + c3;
+  };
+  if constexpr (!UTF) {
+    // every lane at byte q together (q wave-uniform)
+    for (u32 q = 0; q < Lmax; q++)
+      if (act0 && q < L && !cplx) (void)pos(q);
+  } else {
+    // a batch with UTF-8 and a table whose keys start on lead bytes only (lead_only): every
+    // lane at its own position, continuation bytes passed over (2-byte letters: half the
+    // steps; the instantiation k_keyspace_thread<true>)
+    u32 q = 0;
+    for (u32 it = 0; it < Lmax; it++) {
+      const bool act = act0 && q < L && !cplx;
+      if (!__builtin_amdgcn_ballot_w64(act)) break;
+      if (act) q += pos(q);
     }
   }
 }
@@ -422,7 +453,10 @@ __device__ __forceinline__ void psk_walk(const LWord& lw, u32 L, bool act0, u32 
 // closed-form (count, bytes), and for FAST words the plan record, packed densely
 // in word order inside the tile's record region (workgroup scan of the sizes).
 // The tile's word bytes are staged in LDS with 16-B loads.
+template <bool UTF>
 __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
+  // (hiflag: the batch has bytes >= 0x80 -- k_hibytes; the other instantiation does nothing)
+  if (a.hiflag && (*a.hiflag != 0u) != UTF) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u32 tb = (a.table_bytes + 15u) & ~15u;
   u64* gbuf = (u64*)(smem + tb);                       // 256 x KS_GCAP open-group entries
@@ -477,7 +511,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
     u32 nlog = 0;
     const bool rm = a.rmode != 0;
     bool rep = false;  // (-s / -s -r with vocc: a repeated pattern; the occurrences logged)
-    psk_walk<true>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, a.rmode, ulog, &nlog, a.vocc != nullptr, rep);
+    psk_walk<true, UTF>(lw, L, psk, wave_max_u32(L), bmax, T, pl, A, cplx, a.rmode, ulog, &nlog, a.vocc != nullptr, rep);
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
     u32 f = 0;
@@ -533,7 +567,7 @@ __global__ void __launch_bounds__(256) k_keyspace_thread(KsArgs a) {
         }
       }
       const bool walk = build && !replay;
-      if (!(KS_ABL & 1)) psk_walk<false>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2, a.rmode);
+      if (!(KS_ABL & 1)) psk_walk<false, UTF>(lw, L, walk, wave_max_u32(walk ? L : 0u), bmax, T, pb, A2, c2, a.rmode);
       if (build && !(KS_ABL & 1)) {
         pb.finish(L);
         pb.pick_balanced();
@@ -640,7 +674,7 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
     NullSink ns;
     Planner<false, LWord, NullSink, KS_GCAP> pl(lw, T, ns);
     bool cplx = false;
-    psk_walk<true>(lw, L, valid, wave_max_u32(L), bmax, T, pl, A, cplx, a.rmode);
+    psk_walk<true, false>(lw, L, valid, wave_max_u32(L), bmax, T, pl, A, cplx, a.rmode);
     WordClass C;
     C.flags = 0; C.count = 0; C.bytes = 0; C.ovf = false; C.clusters = false;
     u32 f = 0;
@@ -661,7 +695,7 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
       Planner<true, LWord, DevRecSink, KS_GCAP> pb(lw, T, sk, rf ? fb_balanced_cap(C.count + 1) : 0u);
       CountAcc A2;
       bool c2 = false;
-      psk_walk<false>(lw, L, rf, wave_max_u32(rf ? L : 0u), bmax, T, pb, A2, c2, a.rmode);
+      psk_walk<false, false>(lw, L, rf, wave_max_u32(rf ? L : 0u), bmax, T, pb, A2, c2, a.rmode);
       if (rf) {
         pb.finish(L);
         pb.pick_balanced();
@@ -2974,7 +3008,15 @@ hipError_t a5x_launch_keyspace(const A5xKsLaunch& L, hipStream_t st) {
   a.cplx_list = L.cplx_list; a.cplx_n = L.cplx_n; a.cplx_cap = L.cplx_cap; a.cplx_base = L.cplx_base;
   a.glob_list = L.glob_list; a.glob_n = L.glob_n; a.gscr = L.gscr;
   a.rmode = L.rmode; a.rcmin = L.rcmin; a.rnseg = L.rnseg; a.rseg = L.rseg; a.vocc = L.vocc;
-  hipLaunchKernelGGL(k_keyspace_thread, dim3(blocks_for(L.nw, FW_TILE, 65536)), dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
+  a.hiflag = L.hiflag;
+  const dim3 kg(blocks_for(L.nw, FW_TILE, 65536));
+  if (L.hiflag) {  // the table's keys start on UTF-8 lead bytes only: the walk by the batch's bytes
+    hipLaunchKernelGGL(k_hibytes, dim3(256), dim3(256), 0, st, L.words, L.woff, L.nw, L.hiflag);
+    // (the full grid: a resident one striding over the tiles measured slower on C5 -s, 19.3 vs
+    // 17.9 ms keyspace; on an ASCII batch every workgroup returns at once)
+    hipLaunchKernelGGL(k_keyspace_thread<true>, kg, dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
+  }
+  hipLaunchKernelGGL(k_keyspace_thread<false>, kg, dim3(FW_TILE), a5x_keyspace_thread_lds(L.table_bytes), st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (L.rmode) {  // -r / -s / -s -r FAST probe: k_keyspace_thread + the words it listed
@@ -3225,7 +3267,9 @@ hipError_t a5x_set_kernel_attrs() {
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_keyspace_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_keyspace_thread, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  e = hipFuncSetAttribute((const void*)k_keyspace_thread<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_keyspace_thread<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_keyspace_cplx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;

@@ -50,6 +50,7 @@ struct A5xKsLaunch {
   uint16_t* vocc;  // per word 16 u16: k_keyspace_thread's occurrence rows for k_keyspace_vsub (null: none)
   uint32_t* vlong_list;  // k_keyspace_vsub: words the small-slot pass hands to the large one (null: large only)
   uint32_t* vlong_n;
+  uint32_t* hiflag;      // zeroed u32: k_keyspace_thread walks UTF-8 words by lead bytes (null: by bytes)
 };
 
 // the virtual word list of a batch with virtual words (k_vwords_fill)
