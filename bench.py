@@ -278,10 +278,11 @@ def cpu_baseline(tables, args):
     fd = os.open(os.devnull, os.O_WRONLY)
     runs = []
     for th in thread_counts():
-        # past 16 workers the one shared channel (the reference's) serialises them and every
-        # extra worker only adds contention: the sample shrinks with the worker count so the
-        # all-cores run stays a few seconds (the rate, not the sample, is reported)
-        nwords = max(2000, args.cpu_sample_words * 16 // max(16, th))
+        # with several workers the one shared channel (the reference's) serialises them and
+        # every extra worker only adds contention (16 workers: ~1/5 of the 1-worker rate on
+        # the GPU box): the pools get half the sample, shrinking further past 16 workers, so
+        # every run stays within ~10-30 s (the rate, not the sample, is reported)
+        nwords = args.cpu_sample_words if th == 1 else max(2000, args.cpu_sample_words * 8 // max(16, th))
         _, (data, offs) = synth.config_words(args.workload, nwords, seed=0xC0FFEE)
         t0 = time.perf_counter()
         c, b = t.run_pipeline(data, offs, args.mode, args.min, args.max, th, fd)
@@ -292,8 +293,8 @@ def cpu_baseline(tables, args):
     best = max(runs, key=lambda r: r["value"])
     return {"value": best["value"], "unit": "candidates/s", "cores": best["threads"], "kind": "port",
             "cpu_model": cpu_model(), "cpu_affinity": cpu_threads(), "cpu_quota": cpu_quota(), "runs": runs,
-            "sample": f"{args.cpu_sample_words} words of workload {args.workload} (seed 0xC0FFEE; past 16 workers "
-                      f"{args.cpu_sample_words} x 16 / workers) to /dev/null; "
+            "sample": f"{args.cpu_sample_words} words of workload {args.workload} (seed 0xC0FFEE; worker pools "
+                      f"{args.cpu_sample_words} x 8 / max(16, workers)) to /dev/null; "
                       f"C restatement of main.go (oracle/a5_oracle.c) with its goroutine pool, 1000-slot channel "
                       f"(lock-free ring; a blocked sender or receiver spins briefly, then parks on a futex like a "
                       f"goroutine) and one 4 KiB writer; runs at {[r['threads'] for r in runs]} worker thread(s), "
