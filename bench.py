@@ -136,8 +136,9 @@ def shard_for_rank(args, D, ctx, intra_word=True):
     the balanced split by output bytes comes from one all-gather of block totals + one
     all-reduce(MIN).  intra_word: the split points are candidates, found
     exactly on the device (a5x_split_device / a5x_locate_device), so a word larger than a
-    rank's share is cut inside (dist.candidate_split); else word boundaries
-    (dist.distributed_split, a5x_partition semantics: the fused-digest path).
+    rank's share is cut inside (dist.candidate_split) -- the expansion and the fused digest
+    alike (run_digest); else word boundaries (dist.distributed_split, a5x_partition
+    semantics: only --verify, which checks whole words per rank).
     Returns (tables, data, offs, (w0, w1), (cand_begin, cand_count, shard_bytes)) -- candidates
     of the local batch [w0, w1); (0, None, None) = all of them."""
     from hashcat_a5_table_generator_amd import DeviceBuffer, dist as hd, synth
@@ -684,13 +685,17 @@ def launch_ranks(n: int) -> int:
     initialise it, one process per GPU (main.go:70-95's data parallelism over words, here
     over devices)."""
     import subprocess
+    import tempfile
     port = _free_port()
     procs = []
+    # rank 0's stdout goes to a temporary file, read after the ranks exit: a PIPE read only
+    # then could fill (~64 KiB) and block rank 0 while the others wait at a collective
+    out0 = tempfile.TemporaryFile()
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+                                      stdout=out0 if r == 0 else sys.stderr.fileno()))
     log(f"launched {n} ranks (pids {[p.pid for p in procs]}, master 127.0.0.1:{port})")
     rc = 0
     live = list(procs)
@@ -705,7 +710,9 @@ def launch_ranks(n: int) -> int:
                         q.terminate()
         if live:
             time.sleep(0.2)
-    out = procs[0].stdout.read().decode(errors="replace")
+    out0.seek(0)
+    out = out0.read().decode(errors="replace")
+    out0.close()
     sys.stdout.write(out)
     sys.stdout.flush()
     return rc if rc > 0 else (1 if rc else 0)

@@ -23,7 +23,7 @@ E_CAPACITY = -8
 
 # the exported symbols of include/a5x.h (checked by tests/test_abi.py)
 EXPORTS = (
-    "a5x_abi_version", "a5x_create", "a5x_destroy", "a5x_last_error", "a5x_device_info",
+    "a5x_abi_version", "a5x_create", "a5x_create_error", "a5x_destroy", "a5x_last_error", "a5x_device_info",
     "a5x_load_table_file", "a5x_parse_table", "a5x_set_table", "a5x_clear_table", "a5x_table_export",
     "a5x_split_words", "a5x_keyspace", "a5x_expand", "a5x_expand_range", "a5x_expand_device", "a5x_keyspace_device",
     "a5x_digest_device", "a5x_partition", "a5x_dev_alloc", "a5x_dev_free", "a5x_memcpy_h2d",
@@ -79,6 +79,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     i = ctypes.c_int
     L.a5x_abi_version.restype = i
     L.a5x_create.argtypes = [i, ctypes.POINTER(vp)]
+    L.a5x_create_error.argtypes = []
+    L.a5x_create_error.restype = ctypes.c_char_p
     L.a5x_destroy.argtypes = [vp]
     L.a5x_destroy.restype = None
     L.a5x_last_error.argtypes = [vp]

@@ -207,8 +207,10 @@ static int load_targets(a5x_ctx* ctx, const char* path, int algo) {
 static bool parse_u64(const char* s, uint64_t* out) {
   char* e;
   errno = 0;
+  // digits only: strtoull would skip leading blanks and negate a '-' (" -3" -> 2^64 - 3)
+  if (*s < '0' || *s > '9') return false;
   const unsigned long long v = strtoull(s, &e, 10);
-  if (!*s || *e || *s == '-' || errno) return false;
+  if (*e || errno) return false;
   *out = v;
   return true;
 }

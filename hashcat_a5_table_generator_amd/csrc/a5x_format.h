@@ -4,7 +4,10 @@
 // The merged Go map[string][]string of main.go:40-50 is compiled into one flat
 // "device table" blob that every workgroup copies into LDS once:
 //
-//   A5xTableHdr                                   (64 B)
+//   A5xTableHdr                                   (80 B: static_assert below; the
+//                                                 lead_only flag + reserved[3] grew it
+//                                                 from 64 B, so A5X_TABLE_LDS_MAX holds
+//                                                 16 B less of keys / choices / blob)
 //   u16 bucket[257]  keys whose first byte is b are [bucket[b], bucket[b+1])
 //   A5xKey  keys[nkeys]                           (32 B each, 16-B aligned)
 //   A5xChoice choices[nchoices]                   (8 B each)

@@ -18,6 +18,12 @@
 #ifndef FX_HOLDNB
 #define FX_HOLDNB 2      // rounds of <= this many big pieces keep their entries in registers
 #endif
+#ifndef FX6_SWZ
+#define FX6_SWZ 0        // XOR-swizzled ring (FX_SWZ of the includer)
+#endif
+#ifndef FX6_ABL
+#define FX6_ABL 0        // timing ablations (FX_ABL of the includer)
+#endif
 #ifndef FX6_ZBE
 #define FX6_ZBE 255      // the window entry that holds the empty piece (set by the includer)
 #endif
@@ -94,6 +100,7 @@ template <int NB, int K, class FLUSH>
 __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], const u32* rb, const u32* re, u32 ring,
                                          u32 cap, FxRun& R, u32 rr, u32 j, bool act, FLUSH& flush, FxLaneRun& lr) {
   static_assert(K <= FX6_KMAX, "FxLaneRun holds FX6_KMAX candidates");
+  constexpr bool SWZ = FX6_SWZ && !FLUSH::DIGEST;  // (the digest reads its candidates linearly)
   const u32 lane = lane_id();
   const uint4 q0 = wq[j][0], q1 = wq[j][1];
   const u32 st = act ? (rr + lane - q1.w) * K + rb[j] : 0u;  // first rank of the run
@@ -129,12 +136,12 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
   const u32 nact = uniform((u32)__popcll(__ballot(fit)));
   const u32 tot = nact ? readlane_u32(incl, nact - 1u) : 0u;
   u32 P = ring + used + incl - len;
-  if (fit) {
+  if (fit && !(FX6_ABL & 64)) {  // (FX_ABL 64: no placement, timing ablation)
     if constexpr (HOLD) {
 #pragma unroll
       for (int c = 0; c < K; c++)
 #pragma unroll
-        for (int b = 0; b < NB; b++) fx7_put(ent[c][b], P);
+        for (int b = 0; b < NB; b++) fx7_put<SWZ>(ent[c][b], P);
     } else {
       // Entries read again here, one candidate ahead: candidate c + 1's NB reads are
       // issued before candidate c's ORs (in the same basic block, ahead of the puts'
@@ -151,7 +158,7 @@ __device__ __forceinline__ u32 fx7_round(const uint4* be, const uint4 (*wq)[2], 
           for (int b = 0; b < NB; b++) nxt[b] = be[idx[c + 1][b]];
         }
 #pragma unroll
-        for (int b = 0; b < NB; b++) fx7_put(cur[b], P);
+        for (int b = 0; b < NB; b++) fx7_put<SWZ>(cur[b], P);
         if (c + 1 < K) {
 #pragma unroll
           for (int b = 0; b < NB; b++) cur[b] = nxt[b];

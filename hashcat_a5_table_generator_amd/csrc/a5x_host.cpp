@@ -1578,8 +1578,24 @@ extern "C" {
 
 int a5x_abi_version(void) { return A5X_ABI_VERSION; }
 
+// Why the calling thread's last a5x_create failed (no context exists to carry
+// a5x_last_error): the failing HIP call and hipGetErrorString, or the argument problem.
+static thread_local std::string g_create_err;
+
+static int create_fail(int rc, const char* call, hipError_t e, int device) {
+  char buf[256];
+  if (e != hipSuccess)
+    snprintf(buf, sizeof buf, "a5x_create(device=%d): %s failed: %s (hipError_t %d)", device, call,
+             hipGetErrorString(e), (int)e);
+  else
+    snprintf(buf, sizeof buf, "a5x_create(device=%d): %s", device, call);
+  g_create_err = buf;
+  return rc;
+}
+
 int a5x_create(int device, a5x_ctx** out) {
-  if (!out) return A5X_E_ARG;
+  g_create_err.clear();
+  if (!out) return create_fail(A5X_E_ARG, "null output pointer", hipSuccess, device);
   *out = nullptr;
   if (device == -1) {  // host-only context: tables, splitting, export (no GPU needed)
     a5x_ctx* c = new a5x_ctx();
@@ -1588,13 +1604,23 @@ int a5x_create(int device, a5x_ctx** out) {
     return A5X_OK;
   }
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return A5X_E_HIP;
-  if (device < 0 || device >= n) return A5X_E_ARG;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) return create_fail(A5X_E_HIP, "hipGetDeviceCount", e, device);
+  if (n <= 0) return create_fail(A5X_E_HIP, "hipGetDeviceCount found no device", hipSuccess, device);
+  if (device < 0 || device >= n) {
+    char msg[96];
+    snprintf(msg, sizeof msg, "device out of range (%d visible)", n);
+    return create_fail(A5X_E_ARG, msg, hipSuccess, device);
+  }
   a5x_ctx* c = new a5x_ctx();
   c->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if ((e = hipSetDevice(device)) != hipSuccess) {
     delete c;
-    return A5X_E_HIP;
+    return create_fail(A5X_E_HIP, "hipSetDevice", e, device);
+  }
+  if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+    delete c;
+    return create_fail(A5X_E_HIP, "hipStreamCreateWithFlags", e, device);
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
@@ -1602,14 +1628,18 @@ int a5x_create(int device, a5x_ctx** out) {
     c->cus = prop.multiProcessorCount;
   }
   if (c->cus <= 0) c->cus = 256;
-  bool ok = hipMalloc((void**)&c->d_scalars, 256) == hipSuccess &&
-            hipHostMalloc((void**)&c->h_scalars, 256, 0) == hipSuccess &&
-            hipHostMalloc((void**)&c->h_totals, 64, 0) == hipSuccess && a5x_set_kernel_attrs() == hipSuccess;
-  for (int i = 0; i < 4 && ok; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
-  for (int i = 0; i < 2 && ok; i++) ok = hipEventCreate(&c->dev_ev[i]) == hipSuccess;
-  if (!ok) {
+  const char* what = nullptr;
+  if ((e = hipMalloc((void**)&c->d_scalars, 256)) != hipSuccess) what = "hipMalloc";
+  else if ((e = hipHostMalloc((void**)&c->h_scalars, 256, 0)) != hipSuccess) what = "hipHostMalloc";
+  else if ((e = hipHostMalloc((void**)&c->h_totals, 64, 0)) != hipSuccess) what = "hipHostMalloc";
+  else if ((e = a5x_set_kernel_attrs()) != hipSuccess) what = "hipFuncSetAttribute";
+  for (int i = 0; i < 4 && !what; i++)
+    if ((e = hipEventCreate(&c->ev[i])) != hipSuccess) what = "hipEventCreate";
+  for (int i = 0; i < 2 && !what; i++)
+    if ((e = hipEventCreate(&c->dev_ev[i])) != hipSuccess) what = "hipEventCreate";
+  if (what) {
     a5x_destroy(c);
-    return A5X_E_HIP;
+    return create_fail(A5X_E_HIP, what, e, device);
   }
   if (const char* e = getenv("A5X_CHUNK")) c->chunk = std::max<uint64_t>(64, strtoull(e, nullptr, 10));
   // (< 2^24: k_keyspace_vsub packs a sub-word count <= mseg into 24 bits)
@@ -1668,6 +1698,8 @@ void a5x_destroy(a5x_ctx* c) {
 }
 
 const char* a5x_last_error(const a5x_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+const char* a5x_create_error(void) { return g_create_err.c_str(); }
 
 int a5x_device_info(a5x_ctx* c, char* name, size_t cap, int* cu_count) {
   if (!c) return A5X_E_ARG;

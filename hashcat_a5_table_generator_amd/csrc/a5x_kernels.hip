@@ -2129,9 +2129,27 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #endif
                       // during the window setup bytes [16, 16 + 8 FX_WREC) hold the window's
                       // small records (ring block 0 keeps the run's partial block)
+#ifndef FX_SWZ
+#define FX_SWZ 0      // ring stored XOR-swizzled at 16-B-block granularity inside 128-B bank rows
+#endif                // (a5x_ring.h fx7_swz; A/B variant, the ring then starts 1 KiB aligned)
+#ifndef FX_BATCH
+#define FX_BATCH 0    // flush: all ring reads issued before the stores (A/B variant)
+#endif
+#ifndef FX_DRAIN
+#define FX_DRAIN 0    // diagnostic: s_waitcnt vmcnt(0) after every flush (A/B variant)
+#endif
+#ifndef FX_GRID
+#define FX_GRID 0     // flush store instructions on the output's 128-B line grid (A/B variant)
+#endif
 #ifndef FX_TRASH
+#if FX_SWZ
+#define FX_TRASH 0
+#else
 #define FX_TRASH 256  // (unused gap in front of the ring; keeps the measured LDS layout)
 #endif
+#endif
+// physical ring block of logical block b (FX_SWZ: fx7_swz on a 1 KiB-aligned ring)
+__device__ __forceinline__ u32 fx_pb(u32 b) { return FX_SWZ ? b ^ ((b >> 3) & 7u) : b; }
 #ifndef FX_WW
 #define FX_WW 32      // window words
 #endif
@@ -2141,14 +2159,20 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #define FX_ZBE (FX_NBE - 1)
 #define FX6_ZBE FX_ZBE
 // window records: ring bytes [16, FX_RING) during the setup; the last u64 is the zero slot
-#define FX_RZ ((FX_RING - 16) / 8 - 1)
+#ifndef FX_LALIGN
+#define FX_LALIGN 0   // flush whole 128-B output lines only, the rest carried to the ring front (A/B)
+#endif
+// first ring block of the window records during the setup: behind the carried partial
+// block (FX_LALIGN: behind up to 8 carried blocks + the partial one)
+#define FX_RBLK (FX_LALIGN ? 9 : 1)
+#define FX_RZ ((FX_RING - 16 * FX_RBLK) / 8 - 1)
 #ifndef FX_K
 #define FX_K 4        // candidates per lane run (a5x_fx6.h)
 #endif
 #ifndef FX_ABL
 #define FX_ABL 0      // timing ablations (variant builds only; output is garbage when set):
                       // 4 no global stores, 8 no rounds, 16 no big entries, 32 no prefix,
-                      // 128 no ring re-zeroing
+                      // 64 no placement ORs, 128 no ring re-zeroing
 #endif
 #ifndef FX_DABL
 #define FX_DABL 0     // fused-digest ablations (variant builds, wrong hits): 1 no MD rounds, 2 no probe
@@ -2212,12 +2236,56 @@ struct FxRun {
 // ring block 0.  The first block of a run may start before lo: byte-exact.
 // (nontemporal: the stream is written once; plain stores measured +4-8 % expansion time,
 // profiles/r05ce_ab_chunk_stores_occupancy_c3.txt)
+#ifndef FX_ST
+#define FX_ST 0  // output stores: 0 nontemporal, 1 plain (write-back), 2 sc1 (write-through) -- A/B variants
+#endif
 __device__ __forceinline__ void fx_store16(uint8_t* p, const uint4 v) {
   typedef u32 v4u __attribute__((ext_vector_type(4)));
   v4u x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, (v4u*)p);
+  if (FX_ST == 1) *(v4u*)p = x;
+  else if (FX_ST == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+  else __builtin_nontemporal_store(x, (v4u*)p);
 }
 
+#if FX_LALIGN
+// Whole 128-B output lines only: the complete blocks up to the last line boundary are
+// stored (every store instruction then starts on a line once the run's first flush has
+// reached one) and the rest -- up to 8 blocks + the partial one -- moves to the ring front.
+// ALL: every complete block (the run's end).
+template <bool ALL = false>
+__device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) {
+  const u32 lane = lane_id();
+  const u32 nb = uniform((u32)((R.pos - R.B) >> 4));
+  if (nb == 0) return;
+  const u64 B = uniform64(R.B);
+  const u32 nf = ALL ? nb : (u32)(((((B + 16ull * nb) & ~127ull) > B ? ((B + 16ull * nb) & ~127ull) : B) - B) >> 4);
+  if (nf == 0) return;
+  if (B + 16ull * nf > a.out_cap) { guard_trip(a, 1, B, R.lo, R.pos, a.out_cap); R.B = B + 16ull * nf; return; }
+  uint4* r4 = (uint4*)ring;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  if (B >= R.lo) {
+    for (u32 b = lane; b < nf; b += 64) {
+      if (!(FX_ABL & 4)) fx_store16(a.out + B + 16ull * b, r4[b]);
+      r4[b] = z;
+    }
+  } else {
+    for (u32 b = lane; b < nf; b += 64) {
+      if (!(FX_ABL & 4)) store_block(a, B + 16ull * b, r4[b], R.lo, R.pos);
+      r4[b] = z;
+    }
+  }
+  // carry blocks [nf, nb] to [0, nc): all reads before the writes (one instruction each)
+  const u32 nc = nb - nf + 1u;  // <= 9
+  uint4 t = z;
+  if (lane < nc) t = r4[nf + lane];
+  WAVE_SYNC();
+  if (lane < nc) r4[lane] = t;
+  if (lane < nc && nf + lane >= nc) r4[nf + lane] = z;  // sources not overwritten by the carry
+  R.B = B + 16ull * nf;
+  WAVE_SYNC();
+}
+#else
+template <bool ALL = false>
 __device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) {
   const u32 lane = lane_id();
   const u32 nb = uniform((u32)((R.pos - R.B) >> 4));
@@ -2227,30 +2295,77 @@ __device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) 
   uint4* r4 = (uint4*)ring;
   // (OR placement: every flushed block is zeroed again behind its read)
   if (B >= R.lo) {
-    for (u32 b = lane; b < nb; b += 64) {
-      if (!(FX_ABL & 4)) fx_store16(a.out + B + 16ull * b, r4[b]);
-      if (!(FX_ABL & 128)) r4[b] = make_uint4(0, 0, 0, 0);
+#if FX_GRID
+    // store instructions on the 128-B line grid of the output: instruction i covers the
+    // 64 blocks from line (B & ~127) + 1 KiB i; lanes before B or past the flush idle
+    const u32 d = (u32)(B >> 4) & 7u;
+    for (u32 i = lane; i < nb + d; i += 64) {
+      if (i >= d) {
+        const u32 b = i - d;
+        if (!(FX_ABL & 4)) fx_store16(a.out + B + 16ull * b, r4[fx_pb(b)]);
+        if (!(FX_ABL & 128)) r4[fx_pb(b)] = make_uint4(0, 0, 0, 0);
+      }
     }
+#elif FX_BATCH
+    // every ring read of the flush (and the partial block nb) issued before the first wait:
+    // one LDS round trip per flush instead of one per KiB (the loop below waits for each
+    // read before its store)
+    static_assert(FX_RING <= 4096, "batched flush: at most 4 blocks per lane");
+    const u32 nq = (nb + 63u) >> 6;  // uniform, 1..4
+    uint4 v0, v1 = make_uint4(0, 0, 0, 0), v2 = v1, v3 = v1;
+    v0 = r4[fx_pb(min(lane, nb))];  // (clamped: lanes past the flush re-read block nb)
+    if (nq > 1) v1 = r4[fx_pb(min(lane + 64u, nb))];
+    if (nq > 2) v2 = r4[fx_pb(min(lane + 128u, nb))];
+    if (nq > 3) v3 = r4[fx_pb(min(lane + 192u, nb))];
+    const uint4 t = r4[fx_pb(nb)];
+    uint8_t* o = a.out + B + 16ull * lane;
+    if (!(FX_ABL & 4)) {
+      if (lane < nb) fx_store16(o, v0);
+      if (nq > 1 && lane + 64u < nb) fx_store16(o + 1024, v1);
+      if (nq > 2 && lane + 128u < nb) fx_store16(o + 2048, v2);
+      if (nq > 3 && lane + 192u < nb) fx_store16(o + 3072, v3);
+    }
+    // blocks [0, nb] back to zero (nb: the partial block, moved to block 0)
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const u32 nz = (nb >> 6) + 1u;  // uniform, 1..4 (nb < FX_RING / 16)
+    if (lane <= nb) r4[fx_pb(lane)] = z;
+    if (nz > 1 && lane + 64u <= nb) r4[fx_pb(lane + 64u)] = z;
+    if (nz > 2 && lane + 128u <= nb) r4[fx_pb(lane + 128u)] = z;
+    if (nz > 3 && lane + 192u <= nb) r4[fx_pb(lane + 192u)] = z;
+    if (lane == 0) r4[0] = t;  // after lane 0's own zero write of block 0 (a lane's LDS ops stay in order)
+    R.B = B + 16ull * nb;
+    WAVE_SYNC();
+    return;
+#else
+    for (u32 b = lane; b < nb; b += 64) {
+      if (!(FX_ABL & 4)) fx_store16(a.out + B + 16ull * b, r4[fx_pb(b)]);
+      if (!(FX_ABL & 128)) r4[fx_pb(b)] = make_uint4(0, 0, 0, 0);
+    }
+#endif
   } else {
     for (u32 b = lane; b < nb; b += 64) {
-      if (!(FX_ABL & 4)) store_block(a, B + 16ull * b, r4[b], R.lo, R.pos);
-      if (!(FX_ABL & 128)) r4[b] = make_uint4(0, 0, 0, 0);
+      if (!(FX_ABL & 4)) store_block(a, B + 16ull * b, r4[fx_pb(b)], R.lo, R.pos);
+      if (!(FX_ABL & 128)) r4[fx_pb(b)] = make_uint4(0, 0, 0, 0);
     }
   }
   if (lane == 0) {
-    const uint4 t = r4[nb];
-    r4[nb] = make_uint4(0, 0, 0, 0);
+    const uint4 t = r4[fx_pb(nb)];
+    r4[fx_pb(nb)] = make_uint4(0, 0, 0, 0);
     r4[0] = t;
   }
+#if FX_DRAIN  // (diagnostic A/B: wait for every store of the flush, as the window setup's loads do)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   R.B = B + 16ull * nb;
   WAVE_SYNC();
 }
+#endif
 
 // flush everything up to pos (tail block byte-exact)
 __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) {
   if (!R.open) return;
-  fx_flush(R, ring, a);
-  if (R.pos > R.B && lane_id() == 0) {
+  fx_flush<true>(R, ring, a);
+  if (R.pos > R.B && lane_id() == 0) {  // (block 0 is physical block 0 under FX_SWZ too)
     store_block(a, R.B, ((const uint4*)ring)[0], max(R.lo, R.B), R.pos);
     ((uint4*)ring)[0] = make_uint4(0, 0, 0, 0);
   }
@@ -2259,6 +2374,8 @@ __device__ __forceinline__ void fx_close(FxRun& R, u32* ring, const ExpArgs& a) 
 }
 
 #define FX6_KMAX FX_K
+#define FX6_SWZ FX_SWZ
+#define FX6_ABL FX_ABL
 #include "a5x_fx6.h"
 #include "a5x_md.h"
 
@@ -2582,7 +2699,7 @@ __device__ __forceinline__ uint4 fx_entry(const u64* rec, u32 d0, u32 wbe, u32 s
 template <int DIG>
 __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const ExpArgs& a, u64 chunk) {
   const u32 lane = lane_id();
-  u64* const rec = (u64*)(ring + 4);  // ring bytes [16, 16 + 8 FX_WREC)
+  u64* const rec = (u64*)(ring + 4 * FX_RBLK);  // ring bytes [16 FX_RBLK, 16 FX_RBLK + 8 FX_WREC)
   const u64 g0 = max(a.cand_begin, chunk * a.CH);
   const u64 g1 = min(a.cand_end, (chunk + 1) * a.CH);
   if (g0 >= g1) return;
@@ -2781,7 +2898,7 @@ __device__ __forceinline__ void expand_chunk_fast(FXWin& F, u32* ring, const Exp
     }
     fl.wbase = w;
     // the records' ring bytes [16, 16 + 8 ntot) back to zero for the OR rounds
-    for (u32 i = 1 + lane; i <= (ntot + sh + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+    for (u32 i = FX_RBLK + lane; i < FX_RBLK + (ntot + sh + 2) / 2; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
     WAVE_SYNC();
     STAMP(2);
     // the next window's metadata, loaded under this window's rounds (the window's own
@@ -2822,6 +2939,7 @@ __device__ __forceinline__ void expand_fast_body(const ExpArgs& a) {
   FXWin& F = *(FXWin*)(mine + FX_TRASH + FX_RING);
   const u64 chunk = a.cand_begin / a.CH + (u64)blockIdx.x * nwv + wv;
   if (chunk * a.CH >= a.cand_end) return;
+  if (FX_SWZ && DIG == 0 && (fx6_addr(ring) & 1023u)) { guard_trip(a, 7, fx6_addr(ring), 0, 0, 0); return; }
   expand_chunk_fast<DIG>(F, ring, a, chunk);
 }
 

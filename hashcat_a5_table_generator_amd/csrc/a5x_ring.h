@@ -45,18 +45,26 @@ __device__ __forceinline__ void fx7_or(uint32_t a, uint32_t v) {
   __hip_atomic_fetch_or((fx6_lds32*)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// XOR swizzle of a ring byte address at 16-B-block granularity: block bits 4-6 ^= row bits
+// 7-9, so each 128-B bank row (ds_write banks (a/4) mod 32) keeps its bytes and the 16-B
+// blocks stay whole (the flush's ds_read_b128 / ds_write_b128 stay conflict-free).  The
+// ring must start 1 KiB aligned so that logical block 0 is physical block 0.
+__device__ __forceinline__ uint32_t fx7_swz(uint32_t a) { return a ^ ((a >> 3) & 0x70u); }
+
+template <bool SWZ = false>
 __device__ __forceinline__ void fx7_put(const uint4 e, uint32_t& P) {
   const uint32_t n = P & 3u, base = P - n;
   const uint32_t l = e.w >> 24, e3 = e.w & 0xFFFFFFu;
   const uint32_t sel = fx6_sel(n);
   const uint32_t t = n + l;
-  fx7_or(base, __builtin_amdgcn_perm(e.x, 0u, sel));
-  fx7_or(base + 4u, __builtin_amdgcn_perm(e.y, e.x, sel));
+  auto at = [&](uint32_t o) { return SWZ ? fx7_swz(base + o) : base + o; };
+  fx7_or(at(0u), __builtin_amdgcn_perm(e.x, 0u, sel));
+  fx7_or(at(4u), __builtin_amdgcn_perm(e.y, e.x, sel));
   if (__builtin_amdgcn_ballot_w64(t > 8u)) {  // pieces reaching a third dword (wave-uniform)
-    fx7_or(base + 8u, __builtin_amdgcn_perm(e.z, e.y, sel));
+    fx7_or(at(8u), __builtin_amdgcn_perm(e.z, e.y, sel));
     if (__builtin_amdgcn_ballot_w64(t > 12u)) {
-      fx7_or(base + 12u, __builtin_amdgcn_perm(e3, e.z, sel));
-      if (__builtin_amdgcn_ballot_w64(t > 16u)) fx7_or(base + 16u, __builtin_amdgcn_perm(0u, e3, sel));
+      fx7_or(at(12u), __builtin_amdgcn_perm(e3, e.z, sel));
+      if (__builtin_amdgcn_ballot_w64(t > 16u)) fx7_or(at(16u), __builtin_amdgcn_perm(0u, e3, sel));
     }
   }
   P += l;

@@ -73,7 +73,8 @@ class Context:
         h = ctypes.c_void_p()
         rc = self._L.a5x_create(device, ctypes.byref(h))
         if rc != 0:
-            raise A5xError(rc, f"a5x_create(device={device}) failed (no usable GPU?)")
+            why = (self._L.a5x_create_error() or b"").decode(errors="replace")
+            raise A5xError(rc, why or f"a5x_create(device={device}) failed")
         self.h = h
         self.device = device
 
@@ -361,24 +362,21 @@ def _ctx() -> Context:
 
 
 def read_substitution_table(path: str) -> SubMap:
-    """``readSubstitutionTable`` (``main.go:108-144``) via the library's Go-exact parser."""
-    c = _ctx()
-    c.clear_table()
-    c.load_tables([path])
-    return c.table()
+    """``readSubstitutionTable`` (``main.go:108-144``) via the library's Go-exact parser
+    (a private host-only context: the shared default context's table is left alone)."""
+    with Context(-1) as c:
+        c.load_tables([path])
+        return c.table()
 
 
 def decode_hex_notation(value: bytes) -> bytes:
-    """``decodeHexNotation`` (``main.go:147-162``); raises ``ValueError`` like the Go error."""
+    """``decodeHexNotation`` (``main.go:147-162``); raises ``ValueError`` like the Go error.
+    Parsed in a private host-only context (no GPU, the default context untouched)."""
     if len(value) < 7 or not value.startswith(b"$HEX[") or not value.endswith(b"]"):
         return value
-    c = _ctx()
-    c.clear_table()
-    try:
+    with Context(-1) as c:
         c.parse_table(b"k=" + value + b"\n")
-    finally:
-        pass
-    t = c.table()
+        t = c.table()
     if b"k" not in t:
         raise ValueError(f"invalid hex string {value[5:-1]!r}")
     return t[b"k"][0]

@@ -98,6 +98,9 @@ A5X_API int a5x_abi_version(void);
 A5X_API int a5x_create(int device, a5x_ctx** out);
 A5X_API void a5x_destroy(a5x_ctx* ctx);
 A5X_API const char* a5x_last_error(const a5x_ctx* ctx);
+/* Why the calling thread's last a5x_create failed ("" after a success): the failing HIP
+   call with hipGetErrorString, or the argument problem (no context exists to carry it). */
+A5X_API const char* a5x_create_error(void);
 /* device name / gfx arch of the context's GPU */
 A5X_API int a5x_device_info(a5x_ctx* ctx, char* name, size_t name_cap, int* cu_count);
 

@@ -89,3 +89,30 @@ def test_cli_replica_usage():
     assert r.returncode == 0 and "--table-files" in r.stdout
     r = subprocess.run([build.CLI], capture_output=True, text=True)
     assert r.returncode != 0 and "table-files" in r.stderr
+
+
+def test_create_failure_names_the_hip_call():
+    """a5x_create with no visible device: the exception carries the failing HIP call and
+    hipGetErrorString (a5x_create_error), not a bare A5X_E_HIP.  A child process, so that
+    HIP_VISIBLE_DEVICES=-1 is seen before the HIP runtime initialises."""
+    import subprocess
+    import sys
+    code = ("from hashcat_a5_table_generator_amd import Context, A5xError\n"
+            "try:\n    Context(0)\nexcept A5xError as e:\n    print('ERR', e)\nelse:\n    print('OK')\n")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    out = r.stdout.strip()
+    assert out.startswith("ERR"), (out, r.stderr[-2000:])
+    assert "A5X_E_HIP" in out and "a5x_create(device=0)" in out, out
+    assert "hipGetDeviceCount" in out, out
+
+
+def test_create_error_is_empty_after_success():
+    from hashcat_a5_table_generator_amd import _lib
+    L = _lib.load()
+    h = ctypes.c_void_p()
+    assert L.a5x_create(-7, ctypes.byref(h)) != 0
+    assert L.a5x_create_error()  # the argument problem is named
+    assert L.a5x_create(-1, ctypes.byref(h)) == 0
+    assert L.a5x_create_error() == b""
+    L.a5x_destroy(h)

@@ -18,7 +18,9 @@ typedef u32 v4u __attribute__((ext_vector_type(4)));
 typedef v4u v4ua __attribute__((aligned(1)));
 typedef u32 u32a __attribute__((aligned(1)));
 
-#define CH 8192u
+#ifndef CH
+#define CH 16384u  // candidates per wave (k_expand_fast's chunk, A5X_CHUNK default)
+#endif
 #define K 4u
 
 __device__ __forceinline__ u32 clen(u64 c) {  // 8..26 bytes, mean 17
@@ -57,6 +59,13 @@ __device__ __forceinline__ u32 incl_scan(u32 x) {
 // MODE 3: as 1 with nontemporal unaligned stores
 // MODE 4: runs assembled in a per-lane LDS slot (two unaligned ds_write_b128 pieces per
 //         candidate), read back with unaligned ds_read_b128, unaligned global stores
+// MODE 5: as 0 with plain (write-back) stores
+// MODE 6 / 7: as 0 (nt) / 5 (plain) with the store instructions on the 128-B line grid
+// MODE 8 / 9: k_expand_fast's flush pattern: per round of 64 runs of K candidates, the
+//         complete 16-B blocks written so far (nt), instructions from the round's first
+//         block (8) or on the 128-B line grid (9); the partial block waits for the next round
+// MODE 10 / 11: as 8 / 9 with plain stores
+// MODE 12 / 13: as 8 / 9 with sc1 (write-through) stores
 template <int MODE>
 __global__ void __launch_bounds__(256) k_store(uint8_t* out, const u64* boff, u64 n) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 64 * 144];
@@ -65,11 +74,38 @@ __global__ void __launch_bounds__(256) k_store(uint8_t* out, const u64* boff, u6
   if (ch * CH >= n) return;
   const u64 c0 = ch * CH, c1 = min(n, c0 + CH);
   u64 pos = boff[ch];
-  if (MODE == 0) {
+  if (MODE == 0 || MODE == 5 || MODE == 6 || MODE == 7) {
     const u64 end = boff[ch + 1];
-    for (u64 b = (pos & ~15ull) + 16ull * lane; b < end; b += 1024) {
+    const u64 b0 = (MODE == 6 || MODE == 7) ? (pos & ~127ull) : (pos & ~15ull);
+    for (u64 b = b0 + 16ull * lane; b < end; b += 1024) {
+      if (b + 16 <= (pos & ~15ull)) continue;
       v4u v = {(u32)b, (u32)(b >> 32), 0x0a0a0a0au, (u32)ch};
-      __builtin_nontemporal_store(v, (v4u*)(out + b));
+      if (MODE == 0 || MODE == 6) __builtin_nontemporal_store(v, (v4u*)(out + b));
+      else *(v4u*)(out + b) = v;
+    }
+    return;
+  }
+  if (MODE >= 8) {
+    constexpr bool NT = MODE == 8 || MODE == 9, GRID = MODE == 9 || MODE == 11 || MODE == 13;
+    constexpr bool SC1 = MODE >= 12;
+    u64 B = pos & ~15ull;  // first unwritten block
+    for (u64 c = c0; c < c1; c += 64 * K) {
+      const u64 cs = c + (u64)lane * K;
+      u32 rl = 0;
+#pragma unroll
+      for (u32 i = 0; i < K; i++) rl += cs + i < c1 ? clen(cs + i) : 0u;
+      const u32 inc = incl_scan(rl);
+      pos += __shfl(inc, 63);
+      const u64 E = (c + 64 * K >= c1) ? ((pos + 15) & ~15ull) : (pos & ~15ull);  // complete blocks (all at the end)
+      const u64 G = GRID ? (B & ~127ull) : B;
+      for (u64 b = G + 16ull * lane; b < E; b += 1024) {
+        if (b < B) continue;
+        v4u v = {(u32)b, (u32)(b >> 32), 0x0a0a0a0au, (u32)ch};
+        if (SC1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(out + b), "v"(v) : "memory");
+        else if (NT) __builtin_nontemporal_store(v, (v4u*)(out + b));
+        else *(v4u*)(out + b) = v;
+      }
+      B = E;
     }
     return;
   }
@@ -138,13 +174,19 @@ int main(int argc, char** argv) {
   CHK(hipMemcpy(dboff, bo.data(), (nch + 1) * 8, hipMemcpyHostToDevice));
   uint8_t* out;
   CHK(hipMalloc(&out, total + 64));
-  printf("candidates %llu, bytes %.3f GB, chunks %llu\n", (unsigned long long)n, total / 1e9, (unsigned long long)nch);
+  printf("candidates %llu, bytes %.3f GB, chunks %llu (%u candidates per wave)\n", (unsigned long long)n, total / 1e9, (unsigned long long)nch, CH);
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));
   const char* names[] = {"aligned nt dwordx4 (ceiling)", "unaligned runs, reg content", "unaligned runs, const content",
-                         "unaligned runs, nt", "LDS-slot runs, unaligned"};
-  for (int m = 0; m < 5; m++) {
+                         "unaligned runs, nt", "LDS-slot runs, unaligned", "aligned plain dwordx4",
+                         "aligned nt, 128-B instr grid", "aligned plain, 128-B instr grid",
+                         "round flushes nt (kernel pattern)", "round flushes nt, 128-B grid",
+                         "round flushes plain", "round flushes plain, 128-B grid",
+                         "round flushes sc1", "round flushes sc1, 128-B grid"};
+  const int only = argc > 2 ? atoi(argv[2]) : 0;  // 1: the aligned / flush-pattern modes only
+  for (int m = 0; m < 14; m++) {
+    if (only && (m >= 1 && m <= 4)) continue;
     for (int rep = 0; rep < 3; rep++) {
       CHK(hipMemset(out, 0, total + 64));
       CHK(hipEventRecord(e0));
@@ -154,6 +196,15 @@ int main(int argc, char** argv) {
         case 2: hipLaunchKernelGGL(k_store<2>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
         case 3: hipLaunchKernelGGL(k_store<3>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
         case 4: hipLaunchKernelGGL(k_store<4>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 5: hipLaunchKernelGGL(k_store<5>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 6: hipLaunchKernelGGL(k_store<6>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 7: hipLaunchKernelGGL(k_store<7>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 8: hipLaunchKernelGGL(k_store<8>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 9: hipLaunchKernelGGL(k_store<9>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 10: hipLaunchKernelGGL(k_store<10>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 11: hipLaunchKernelGGL(k_store<11>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 12: hipLaunchKernelGGL(k_store<12>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 13: hipLaunchKernelGGL(k_store<13>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
       }
       CHK(hipEventRecord(e1));
       CHK(hipEventSynchronize(e1));
