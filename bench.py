@@ -334,18 +334,36 @@ def digest_cpu_baseline(tables, args, targets):
                       f" thread(s), the best reported"}
 
 
+def digest_mix_cycles(algo: str):
+    """Mean SIMD issue cycles per VALU wave-instruction of the MD5 / MD4 compression
+    (profiles/r06_digest_isa_mix.json: tools/isa_mix.py prices every opcode of md5_block /
+    md4_block by the issue costs measured in profiles/r06_mb_valu.txt -- 2 cycles for
+    v_add_u32 / v_xor_b32 / v_bitop3_b32, 4 for v_add3_u32 / v_alignbit_b32 / v_bfi_b32 /
+    v_perm_b32 ...).  None when the file is absent."""
+    f = os.path.join(ROOT, "profiles", "r06_digest_isa_mix.json")
+    try:
+        d = json.load(open(f))
+        return d["md5_block" if algo == "md5" else "md4_block"]["mean_issue_cycles"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
     """Digest stage: VALU-bound.  achieved = integer lane-ops/s of the digest kernel (int
-    ops per candidate from the PMC profile (tools/gpu.sh digestprof) x candidates / stage
-    time); peak = 256 CUs x 4 SIMDs x 16 lanes/cycle x 2.4 GHz = 39.3 T int32 lane-ops/s:
-    the issue rate of the VOP3 instructions the MD5 / MD4 rounds are made of (v_add3_u32,
-    v_bfi_b32, v_alignbit_b32, v_xor3_b32), 4 cycles per wave64 instruction -- measured on
-    MI355X (tools/mb_valu.hip, profiles/r05_mb_valu.txt: v_perm / v_alignbyte 1.93 ns per
-    wave-instruction per SIMD, twice v_add_u32's 1.13 ns: VOP2 ops issue in 2 cycles, VOP3
-    in 4).  Round 4 priced every op at the VOP2 rate (78.6 T), which halved frac against the
-    PMC's VALUBusy; peak_vop2 keeps that figure.  Fused path (default mode): k_expand_fast_md5 / k_expand_fast_ntlm
-    expand, hash and probe in one kernel, so the stage time is the expansion time.  The
-    step's time is accounted as keyspace + stage (+ two-pass digest) + the rest (host)."""
+    ops per candidate from the PMC profile (tools/gpu.sh digestprof: SQ_INSTS_VALU x 64 /
+    candidates) x candidates / stage time).  Three peaks, all 256 CUs x 4 SIMDs at 2.4 GHz:
+      * peak (frac): the nominal VALU rate, one wave64 instruction per 2 cycles per SIMD
+        (32 lanes / cycle, MI355X_MICROARCH.md) = 78.6 T int32 lane-ops/s;
+      * peak_vop3 (frac_vop3): every instruction at the half rate (4 cycles) of the VOP3
+        integer ops the rounds lean on = 39.3 T;
+      * peak_mix (frac_mix): the MD core's own mix, 64 lanes per (mean issue cycles) per SIMD
+        (digest_mix_cycles: 2.80 cycles for MD5, 2.94 for MD4; profiles/r06_mb_valu.txt has the
+        per-opcode costs, measured with every line live).
+    SQ_ACTIVE_INST_VALU is in quad-cycles per wave: ACTIVE / INSTS is a wave's residency per
+    instruction (~1 quad-cycle = 4 cycles), not the SIMD's issue cost.  Fused path (default
+    mode): k_expand_fast_md5 / k_expand_fast_ntlm expand, hash and probe in one kernel, so the
+    stage time is the expansion time.  The step's time is accounted as keyspace + stage
+    (+ two-pass digest) + the rest (host)."""
     fused = ms_dig < 1e-3
     # (-r / -s / -s -r: the FAST-probe and virtual words hash in k_expand_fast_<algo>, the
     # rest in the mode engine's k_mode_digest_* beside it -- ops summed over both)
@@ -353,9 +371,12 @@ def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
               if fused else "k_digest_stream")
     ms_stage = ms_exp if fused else ms_dig
     prof = digest_profile(args.digest, args.words, kernel, args.mode, args.min)
-    peak = 256 * 4 * 16 * 2.4e9 / 1e12  # Tops/s at the VOP3 issue rate
+    peak = 256 * 4 * 32 * 2.4e9 / 1e12  # Tops/s: the nominal VALU rate (2 cycles per wave64 instruction)
+    mixc = digest_mix_cycles(args.digest)
+    peak_mix = 256 * 4 * 64 * 2.4e9 / mixc / 1e12 if mixc else None
     r = {"bound": "valu", "kernel": kernel + ("" if fused else f"<{args.digest}>"), "fused": fused,
-         "unit": "Tops/s (int32 lane ops)", "peak": peak, "peak_vop2": 2 * peak,
+         "unit": "Tops/s (int32 lane ops)", "peak": peak, "peak_vop3": peak / 2, "peak_mix": peak_mix,
+         "mix_issue_cycles_per_inst": mixc,
          "ms_digest_per_step": ms_stage if not fused else 0.0,
          "ms_expand_per_step": ms_exp, "ms_keyspace_per_step": ms_ks, "ms_step": ms_step,
          "ms_step_unaccounted": ms_step - ms_ks - ms_exp - (0.0 if fused else ms_dig),
@@ -365,12 +386,15 @@ def digest_roofline(args, tc, ms_dig, ms_exp, ms_ks, ms_step):
                          f"{'' if prof['_sha_match'] else ', an earlier source revision'})")
         if prof["_sha_match"]:  # int ops per candidate count only for the sources they were measured on
             ach = prof["int_ops_per_cand"] * tc / (ms_stage * 1e-3) / 1e12
-            r.update(achieved=ach, frac=ach / peak, int_ops_per_cand=prof["int_ops_per_cand"],
+            r.update(achieved=ach, frac=ach / peak, frac_vop3=ach / (peak / 2),
+                     frac_mix=(ach / peak_mix) if peak_mix else None, int_ops_per_cand=prof["int_ops_per_cand"],
                      valu_busy_pct=prof.get("valu_busy_pct"), valu_utilization_pct=prof.get("valu_utilization_pct"),
-                     valu_cycles_per_inst=prof.get("valu_cycles_per_inst"), eff_clock_ghz=prof.get("eff_clock_ghz"))
-            if prof.get("eff_clock_ghz"):  # the same VOP3 issue rate at the clock the chip held
-                pk = 256 * 4 * 16 * prof["eff_clock_ghz"] * 1e9 / 1e12
-                r.update(peak_at_eff_clock=pk, frac_at_eff_clock=ach / pk)
+                     active_valu_quad_cycles_per_inst=prof.get("active_valu_quad_cycles_per_inst",
+                                                               (prof.get("valu_cycles_per_inst") or 0) / 4 or None),
+                     eff_clock_ghz=prof.get("eff_clock_ghz"))
+            if prof.get("eff_clock_ghz") and peak_mix:  # the mix peak at the clock the chip held
+                pk = peak_mix * prof["eff_clock_ghz"] / 2.4
+                r.update(peak_mix_at_eff_clock=pk, frac_mix_at_eff_clock=ach / pk)
         else:
             r.update(frac_from_stale_profile=True, stale_int_ops_per_cand=prof["int_ops_per_cand"])
     return r

@@ -78,9 +78,10 @@ res = {
     "active_valu_per_wave_cycle": sum(c1.get("SQ_ACTIVE_INST_VALU", [0])) / max(1.0, sum(c1.get("SQ_WAVE_CYCLES", [1]))),
     "kernel_avg_us": float(dig["AverageNs"]) / 1e3 if dig else None,
     "kernel_calls": int(dig["Calls"]) if dig else None,
-    # SQ_ACTIVE_INST_VALU counts quad-cycles: x 4 / instructions = issue cycles per wave64
-    # VALU instruction (2 for VOP2 ops, 4 for VOP3: profiles/r05_mb_valu.txt)
-    "valu_cycles_per_inst": 4.0 * sum(c1.get("SQ_ACTIVE_INST_VALU", [0])) / max(1.0, valu),
+    # SQ_ACTIVE_INST_VALU counts quad-cycles per wave (MI355X_MICROARCH.md): / instructions =
+    # a wave's residency per VALU instruction (~1 quad-cycle: one wave alone issues every 4
+    # cycles), NOT the SIMD's issue cost (2 or 4 cycles by opcode: profiles/r06_mb_valu.txt)
+    "active_valu_quad_cycles_per_inst": sum(c1.get("SQ_ACTIVE_INST_VALU", [0])) / max(1.0, valu),
     # effective shader clock over the profiled dispatches (GRBM_GUI_ACTIVE sums the 8 XCDs;
     # MI355X_MICROARCH.md 'DVFS give-back'), from the kernel's average duration in the
     # kernel-trace pass of the same workload
