@@ -2241,8 +2241,8 @@ int a5x_set_targets(a5x_ctx* c, int algo, const uint8_t* dig, uint64_t n) {
     memcpy(d, dig + 16 * i, 16);
     if ((d[0] | d[1] | d[2] | d[3]) == 0) { has_zero = 1; continue; }
     const uint32_t bi = d[0] & (uint32_t)((1ull << bm_log2) - 1);
-    if (MD_BLOOM2) {  // (a5x_md.h md_probe: the 64-bit word of bi, two bits from word 1)
-      const uint64_t m = md_bloom_bits(d[1]);
+    if (MD_BLOOM2) {  // (a5x_md.h md_prefilter: the 64-bit word of bi, two bits from word 3)
+      const uint64_t m = md_bloom_bits(d[3]);
       bm[(bi >> 6) * 2] |= (uint32_t)m;
       bm[(bi >> 6) * 2 + 1] |= (uint32_t)(m >> 32);
     } else {

@@ -2578,6 +2578,11 @@ __device__ __forceinline__ void fxd_round(const uint4* be, const uint4 (*wq)[2],
 #pragma unroll
   for (int q = 0; q < NQ; q++) fx6_st16(slot + 16u * q, make_uint4(0, 0, 0, 0));  // zero again for the next round
   u32 h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+#if FX_DABL == 0
+  // (early rejection: a wave whose candidates all miss the prefilter on digest words 0 / 3
+  // skips the last two MD steps and the table probe -- md_block_probe)
+  const bool hit = md_block_probe<MD5>(M, on, a.dg_bitmap, a.dg_bm_mask, a.dg_table, a.dg_tmask, a.dg_has_zero != 0, h);
+#else
 #if FX_DABL & 1
   h[0] ^= M[0] + M[14]; h[1] ^= M[1]; h[2] ^= M[2]; h[3] ^= M[3];
 #else
@@ -2588,6 +2593,7 @@ __device__ __forceinline__ void fxd_round(const uint4* be, const uint4 (*wq)[2],
   const bool hit = (h[0] ^ h[1] ^ h[2] ^ h[3]) == 0x7A5A5A5Au && h[0] == 0x13579BDFu;
 #else
   const bool hit = md_probe(a.dg_bitmap, a.dg_bm_mask, a.dg_table, a.dg_tmask, a.dg_has_zero != 0, h);
+#endif
 #endif
   if (on && hit) {
     const u32 k = atomicAdd(a.dg_nhits, 1u);

@@ -17,8 +17,9 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t s) { return __buil
 #define MD5_H(x, y, z) ((x) ^ (y) ^ (z))
 #define MD5_I(x, y, z) ((y) ^ ((x) | ~(z)))
 
-__device__ __forceinline__ void md5_block(uint32_t* st, const uint32_t* M) {
-  uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+// steps 1-62: after them a and d hold their final values (digest words 0 and 3 = IV + a, d),
+// so the target prefilter (md_prefilter) can reject before steps 63-64 (md_block_probe)
+__device__ __forceinline__ void md5_steps62(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, const uint32_t* M) {
   MD5_STEP(MD5_F, a, b, c, d, M[0], 0xd76aa478u, 7) MD5_STEP(MD5_F, d, a, b, c, M[1], 0xe8c7b756u, 12)
   MD5_STEP(MD5_F, c, d, a, b, M[2], 0x242070dbu, 17) MD5_STEP(MD5_F, b, c, d, a, M[3], 0xc1bdceeeu, 22)
   MD5_STEP(MD5_F, a, b, c, d, M[4], 0xf57c0fafu, 7) MD5_STEP(MD5_F, d, a, b, c, M[5], 0x4787c62au, 12)
@@ -50,7 +51,14 @@ __device__ __forceinline__ void md5_block(uint32_t* st, const uint32_t* M) {
   MD5_STEP(MD5_I, a, b, c, d, M[8], 0x6fa87e4fu, 6) MD5_STEP(MD5_I, d, a, b, c, M[15], 0xfe2ce6e0u, 10)
   MD5_STEP(MD5_I, c, d, a, b, M[6], 0xa3014314u, 15) MD5_STEP(MD5_I, b, c, d, a, M[13], 0x4e0811a1u, 21)
   MD5_STEP(MD5_I, a, b, c, d, M[4], 0xf7537e82u, 6) MD5_STEP(MD5_I, d, a, b, c, M[11], 0xbd3af235u, 10)
+}
+__device__ __forceinline__ void md5_steps63_64(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, const uint32_t* M) {
   MD5_STEP(MD5_I, c, d, a, b, M[2], 0x2ad7d2bbu, 15) MD5_STEP(MD5_I, b, c, d, a, M[9], 0xeb86d391u, 21)
+}
+__device__ __forceinline__ void md5_block(uint32_t* st, const uint32_t* M) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+  md5_steps62(a, b, c, d, M);
+  md5_steps63_64(a, b, c, d, M);
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
 }
 
@@ -61,8 +69,8 @@ __device__ __forceinline__ void md5_block(uint32_t* st, const uint32_t* M) {
 #define MD4_R2(a, b, c, d, k, s) a = rotl(a + MD4_G(b, c, d) + M[k] + 0x5a827999u, s);
 #define MD4_R3(a, b, c, d, k, s) a = rotl(a + MD4_H(b, c, d) + M[k] + 0x6ed9eba1u, s);
 
-__device__ __forceinline__ void md4_block(uint32_t* st, const uint32_t* M) {
-  uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+// steps 1-46: a and d final (digest words 0 and 3), as md5_steps62
+__device__ __forceinline__ void md4_steps46(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, const uint32_t* M) {
   MD4_R1(a, b, c, d, 0, 3) MD4_R1(d, a, b, c, 1, 7) MD4_R1(c, d, a, b, 2, 11) MD4_R1(b, c, d, a, 3, 19)
   MD4_R1(a, b, c, d, 4, 3) MD4_R1(d, a, b, c, 5, 7) MD4_R1(c, d, a, b, 6, 11) MD4_R1(b, c, d, a, 7, 19)
   MD4_R1(a, b, c, d, 8, 3) MD4_R1(d, a, b, c, 9, 7) MD4_R1(c, d, a, b, 10, 11) MD4_R1(b, c, d, a, 11, 19)
@@ -74,7 +82,15 @@ __device__ __forceinline__ void md4_block(uint32_t* st, const uint32_t* M) {
   MD4_R3(a, b, c, d, 0, 3) MD4_R3(d, a, b, c, 8, 9) MD4_R3(c, d, a, b, 4, 11) MD4_R3(b, c, d, a, 12, 15)
   MD4_R3(a, b, c, d, 2, 3) MD4_R3(d, a, b, c, 10, 9) MD4_R3(c, d, a, b, 6, 11) MD4_R3(b, c, d, a, 14, 15)
   MD4_R3(a, b, c, d, 1, 3) MD4_R3(d, a, b, c, 9, 9) MD4_R3(c, d, a, b, 5, 11) MD4_R3(b, c, d, a, 13, 15)
-  MD4_R3(a, b, c, d, 3, 3) MD4_R3(d, a, b, c, 11, 9) MD4_R3(c, d, a, b, 7, 11) MD4_R3(b, c, d, a, 15, 15)
+  MD4_R3(a, b, c, d, 3, 3) MD4_R3(d, a, b, c, 11, 9)
+}
+__device__ __forceinline__ void md4_steps47_48(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, const uint32_t* M) {
+  MD4_R3(c, d, a, b, 7, 11) MD4_R3(b, c, d, a, 15, 15)
+}
+__device__ __forceinline__ void md4_block(uint32_t* st, const uint32_t* M) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+  md4_steps46(a, b, c, d, M);
+  md4_steps47_48(a, b, c, d, M);
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
 }
 
@@ -86,26 +102,33 @@ __device__ __forceinline__ uint32_t lds4(const uint8_t* base, uint32_t off) {
 
 // Target set: a 2^k-bit prefilter, then an open-addressing table of 16-B digests
 // (all-zero slot = empty; the all-zero digest is a flag).  The prefilter is a blocked
-// Bloom filter: digest word 0 picks a 64-bit word, word 1 two bits in it (one load, both
+// Bloom filter: digest word 0 picks a 64-bit word, word 3 two bits in it (one load, both
 // bits tested): at 64 bits per target a false positive is ~1/1000 instead of 1/64, so a
 // wave of 64 candidates reaches the table probe in ~6 % of its rounds instead of ~63 %
-// (MD_BLOOM2=0: one bit, the round-4 filter; the host builds the same layout).
+// (MD_BLOOM2=0: one bit, the round-4 filter; the host builds the same layout).  Words 0
+// and 3 are final two MD5 steps (MD4: two steps) before the end of the last block, so a
+// wave whose candidates all miss the filter skips those steps (md_block_probe).
 #ifndef MD_BLOOM2
 #define MD_BLOOM2 1
 #endif
-__host__ __device__ __forceinline__ uint64_t md_bloom_bits(uint32_t d1) {
-  return MD_BLOOM2 ? (1ull << (d1 & 63u)) | (1ull << ((d1 >> 6) & 63u)) : 0ull;
+__host__ __device__ __forceinline__ uint64_t md_bloom_bits(uint32_t d3) {
+  return MD_BLOOM2 ? (1ull << (d3 & 63u)) | (1ull << ((d3 >> 6) & 63u)) : 0ull;
+}
+// the prefilter alone, on digest words 0 and 3 (a possible all-zero target passes)
+__device__ __forceinline__ bool md_prefilter(const uint32_t* bitmap, uint32_t bm_mask, bool has_zero, uint32_t d0,
+                                             uint32_t d3) {
+  if (has_zero && (d0 | d3) == 0u) return true;
+  const uint32_t bi = d0 & bm_mask;
+  if (MD_BLOOM2) {
+    const uint64_t m = md_bloom_bits(d3);
+    return (((const uint64_t*)bitmap)[bi >> 6] & m) == m;
+  }
+  return (bitmap[bi >> 5] >> (bi & 31u)) & 1u;
 }
 __device__ __forceinline__ bool md_probe(const uint32_t* bitmap, uint32_t bm_mask, const uint4* table, uint64_t tmask,
                                          bool has_zero, const uint32_t* d) {
   if ((d[0] | d[1] | d[2] | d[3]) == 0u) return has_zero;
-  const uint32_t bi = d[0] & bm_mask;
-  if (MD_BLOOM2) {
-    const uint64_t m = md_bloom_bits(d[1]);
-    if ((((const uint64_t*)bitmap)[bi >> 6] & m) != m) return false;
-  } else if (!((bitmap[bi >> 5] >> (bi & 31u)) & 1u)) {
-    return false;
-  }
+  if (!md_prefilter(bitmap, bm_mask, false, d[0], d[3])) return false;
   const uint64_t h = ((uint64_t)d[1] | ((uint64_t)d[2] << 32)) * 0x9E3779B97F4A7C15ull;
   uint64_t slot = (h >> 20) & tmask;
   for (uint64_t n = 0; n <= tmask; n++) {
@@ -115,6 +138,24 @@ __device__ __forceinline__ bool md_probe(const uint32_t* bitmap, uint32_t bm_mas
     slot = (slot + 1) & tmask;
   }
   return false;
+}
+
+// One-block digest + probe with early rejection: steps 1-62 (MD4: 1-46) give digest words 0
+// and 3; when no lane of the wave passes the prefilter on them the last two steps and the
+// table probe are skipped (no hit is possible).  h = the digest (words 1, 2 only when the
+// wave went on).  Wave-collective (the ballot): call with every lane of the wave.
+template <bool MD5>
+__device__ __forceinline__ bool md_block_probe(const uint32_t* M, bool on, const uint32_t* bitmap, uint32_t bm_mask,
+                                               const uint4* table, uint64_t tmask, bool has_zero, uint32_t* h) {
+  uint32_t a = 0x67452301u, b = 0xefcdab89u, c = 0x98badcfeu, d = 0x10325476u;
+  if (MD5) md5_steps62(a, b, c, d, M); else md4_steps46(a, b, c, d, M);
+  h[0] = 0x67452301u + a; h[3] = 0x10325476u + d;
+  h[1] = h[2] = 0u;
+  const bool pass = on && md_prefilter(bitmap, bm_mask, has_zero, h[0], h[3]);
+  if (!__builtin_amdgcn_ballot_w64(pass)) return false;
+  if (MD5) md5_steps63_64(a, b, c, d, M); else md4_steps47_48(a, b, c, d, M);
+  h[1] = 0xefcdab89u + b; h[2] = 0x98badcfeu + c;
+  return pass && md_probe(bitmap, bm_mask, table, tmask, has_zero, h);
 }
 
 // Merkle-Damgard over message bytes [off, off + len) of an LDS buffer (readable 8 bytes

@@ -1247,9 +1247,8 @@ __device__ __forceinline__ void m_slot_md5_probe(const A5xModeLaunch& a, u32 slo
   }
   M[14] = on ? len << 3 : 0u;
   M[15] = 0u;
-  u32 d[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-  md5_block(d, M);
-  if (on && md_probe(a.dg_bitmap, a.dg_bm_mask, a.dg_table, a.dg_tmask, a.dg_has_zero != 0, d)) {
+  u32 d[4];
+  if (md_block_probe<true>(M, on, a.dg_bitmap, a.dg_bm_mask, a.dg_table, a.dg_tmask, a.dg_has_zero != 0, d)) {
     const u32 h = atomicAdd(a.dg_nhits, 1u);
     if (h < a.dg_hit_cap) {
       A5xHitRaw r;
