@@ -2135,6 +2135,9 @@ __device__ bool expand_word(WaveLds<LMAX, MLMAX, DPENT>& S, u32* ring, const Tab
 #ifndef FX_BATCH
 #define FX_BATCH 0    // flush: all ring reads issued before the stores (A/B variant)
 #endif
+#ifndef FX_SADDR
+#define FX_SADDR 0    // flush stores addressed as scalar base + 32-bit lane offset (A/B variant)
+#endif
 #ifndef FX_DRAIN
 #define FX_DRAIN 0    // diagnostic: s_waitcnt vmcnt(0) after every flush (A/B variant)
 #endif
@@ -2336,6 +2339,19 @@ __device__ __forceinline__ void fx_flush(FxRun& R, u32* ring, const ExpArgs& a) 
     R.B = B + 16ull * nb;
     WAVE_SYNC();
     return;
+#elif FX_SADDR
+    // scalar base + 32-bit lane offset (global_store ... saddr): 4 B of address per lane to
+    // the vector memory pipeline instead of 8
+    typedef u32 gv4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) gv4u gv4;
+    typedef __attribute__((address_space(1))) uint8_t gu8;
+    gu8* const ob = (gu8*)(uintptr_t)uniform64((u64)(uintptr_t)(a.out + B));
+    for (u32 b = lane; b < nb; b += 64) {
+      const uint4 v = r4[fx_pb(b)];
+      const gv4u x = {v.x, v.y, v.z, v.w};
+      if (!(FX_ABL & 4)) __builtin_nontemporal_store(x, (gv4*)(ob + 16u * b));
+      if (!(FX_ABL & 128)) r4[fx_pb(b)] = make_uint4(0, 0, 0, 0);
+    }
 #else
     for (u32 b = lane; b < nb; b += 64) {
       if (!(FX_ABL & 4)) fx_store16(a.out + B + 16ull * b, r4[fx_pb(b)]);
