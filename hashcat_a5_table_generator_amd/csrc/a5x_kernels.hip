@@ -2240,13 +2240,17 @@ struct FxRun {
 // (nontemporal: the stream is written once; plain stores measured +4-8 % expansion time,
 // profiles/r05ce_ab_chunk_stores_occupancy_c3.txt)
 #ifndef FX_ST
-#define FX_ST 0  // output stores: 0 nontemporal, 1 plain (write-back), 2 sc1 (write-through) -- A/B variants
+#define FX_ST 0  // output stores: 0 nontemporal, 1 plain (write-back), 2 sc1 (write-through), 3 the cache-policy
+#endif           // bits FX_STPOL ("sc0 nt", ...) -- A/B variants
+#ifndef FX_STPOL
+#define FX_STPOL "nt"
 #endif
 __device__ __forceinline__ void fx_store16(uint8_t* p, const uint4 v) {
   typedef u32 v4u __attribute__((ext_vector_type(4)));
   v4u x = {v.x, v.y, v.z, v.w};
   if (FX_ST == 1) *(v4u*)p = x;
   else if (FX_ST == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+  else if (FX_ST == 3) asm volatile("global_store_dwordx4 %0, %1, off " FX_STPOL ::"v"(p), "v"(x) : "memory");
   else __builtin_nontemporal_store(x, (v4u*)p);
 }
 

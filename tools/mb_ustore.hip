@@ -66,6 +66,7 @@ __device__ __forceinline__ u32 incl_scan(u32 x) {
 //         block (8) or on the 128-B line grid (9); the partial block waits for the next round
 // MODE 10 / 11: as 8 / 9 with plain stores
 // MODE 12 / 13: as 8 / 9 with sc1 (write-through) stores
+// MODE 14..18: as 8 with the cache-policy bits sc0 / sc0 nt / sc1 nt / sc0 sc1 / sc0 sc1 nt
 template <int MODE>
 __global__ void __launch_bounds__(256) k_store(uint8_t* out, const u64* boff, u64 n) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 64 * 144];
@@ -87,7 +88,7 @@ __global__ void __launch_bounds__(256) k_store(uint8_t* out, const u64* boff, u6
   }
   if (MODE >= 8) {
     constexpr bool NT = MODE == 8 || MODE == 9, GRID = MODE == 9 || MODE == 11 || MODE == 13;
-    constexpr bool SC1 = MODE >= 12;
+    constexpr bool SC1 = MODE == 12 || MODE == 13;
     u64 B = pos & ~15ull;  // first unwritten block
     for (u64 c = c0; c < c1; c += 64 * K) {
       const u64 cs = c + (u64)lane * K;
@@ -101,7 +102,12 @@ __global__ void __launch_bounds__(256) k_store(uint8_t* out, const u64* boff, u6
       for (u64 b = G + 16ull * lane; b < E; b += 1024) {
         if (b < B) continue;
         v4u v = {(u32)b, (u32)(b >> 32), 0x0a0a0a0au, (u32)ch};
-        if (SC1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(out + b), "v"(v) : "memory");
+        if (MODE == 14) asm volatile("global_store_dwordx4 %0, %1, off sc0" ::"v"(out + b), "v"(v) : "memory");
+        else if (MODE == 15) asm volatile("global_store_dwordx4 %0, %1, off sc0 nt" ::"v"(out + b), "v"(v) : "memory");
+        else if (MODE == 16) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(out + b), "v"(v) : "memory");
+        else if (MODE == 17) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(out + b), "v"(v) : "memory");
+        else if (MODE == 18) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(out + b), "v"(v) : "memory");
+        else if (SC1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(out + b), "v"(v) : "memory");
         else if (NT) __builtin_nontemporal_store(v, (v4u*)(out + b));
         else *(v4u*)(out + b) = v;
       }
@@ -183,10 +189,12 @@ int main(int argc, char** argv) {
                          "aligned nt, 128-B instr grid", "aligned plain, 128-B instr grid",
                          "round flushes nt (kernel pattern)", "round flushes nt, 128-B grid",
                          "round flushes plain", "round flushes plain, 128-B grid",
-                         "round flushes sc1", "round flushes sc1, 128-B grid"};
+                         "round flushes sc1", "round flushes sc1, 128-B grid", "round flushes sc0", "round flushes sc0 nt",
+                         "round flushes sc1 nt", "round flushes sc0 sc1", "round flushes sc0 sc1 nt"};
   const int only = argc > 2 ? atoi(argv[2]) : 0;  // 1: the aligned / flush-pattern modes only
-  for (int m = 0; m < 14; m++) {
+  for (int m = 0; m < 19; m++) {
     if (only && (m >= 1 && m <= 4)) continue;
+    if (only == 2 && m < 8) continue;
     for (int rep = 0; rep < 3; rep++) {
       CHK(hipMemset(out, 0, total + 64));
       CHK(hipEventRecord(e0));
@@ -205,6 +213,11 @@ int main(int argc, char** argv) {
         case 11: hipLaunchKernelGGL(k_store<11>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
         case 12: hipLaunchKernelGGL(k_store<12>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
         case 13: hipLaunchKernelGGL(k_store<13>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 14: hipLaunchKernelGGL(k_store<14>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 15: hipLaunchKernelGGL(k_store<15>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 16: hipLaunchKernelGGL(k_store<16>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 17: hipLaunchKernelGGL(k_store<17>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
+        case 18: hipLaunchKernelGGL(k_store<18>, dim3((nch + 3) / 4), dim3(256), 0, 0, out, dboff, n); break;
       }
       CHK(hipEventRecord(e1));
       CHK(hipEventSynchronize(e1));
