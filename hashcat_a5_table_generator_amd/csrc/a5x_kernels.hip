@@ -756,6 +756,10 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
                      // keyspace 27.1 vs 29.2 ms, the same words split, expansion unchanged; 2: most
                      // words past 8 pieces)
 #endif
+#ifndef VS_PATCH
+#define VS_PATCH 1   // sub-words 1.. of a fixed-width uniform word patched from sub-word 0's record
+                     // (0: every sub-word planned, the A/B baseline)
+#endif
 #ifndef VS_BLOCK
 #define VS_BLOCK 128 // k_keyspace_vsub workgroup: two waves share the table copy (C5 -s A/B, profiles/r05r_ab_vsub_block_c5.txt:
                      // 16.98 ms vs 17.85 ms at 64, 17.19 at 256)
@@ -889,6 +893,10 @@ struct VsWave {  // per-wave LDS state
   u32 ctot[64], btot[64], rtot[64], bad[64];
   uint4 info[64];                     // word: L | nocc << 8 | nt << 16 | S << 24, tr, tk
   unsigned long long base[64];
+  uint16_t tbb[65];                   // first build task (the planner) of each lane's word (+ total)
+  uint16_t tpb[65];                   // first patch task (sub-words 1.. of a patched word) (+ total)
+  u64 upst[64];                       // uniform word: sub-word 0's piece starts (Planner::pst)
+  u32 ub0[64];                        // ... and the bytes of each other sub-word
 };
 
 // Record sink of the build pass: the open group in LDS (lane-strided by VS_BLOCK),
@@ -1030,6 +1038,15 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
         uni = uni && (a.rmode == 2 ? key.minclen == key.maxclen : T.ch[key.choice_base + 1].len == key.klen);
       }
     }
+    // fixed width: every pattern of the word (units and tied) has all its choices as long as
+    // itself, so an entry's byte j is word byte (piece start + j) in every sub-word and
+    // sub-word s's record is sub-word 0's with the tied bytes changed (the patch tasks)
+    bool fixed = VS_PATCH && ok && uni;
+    for (u32 j = 0; fixed && j < V.nocc; j++) {
+      const A5xKey key = T.keys[occ[j * VS_BLOCK] & 1023u];
+      fixed = key.nvals >= 1 &&
+              (a.rmode == 2 ? key.minclen == key.maxclen : T.ch[key.choice_base + 1].len == key.klen);
+    }
     // ---- the wave's task lists: word lane l owns tasks [tbase[l], tbase[l] + S) ----
     const u32 Sl = ok ? V.S : 0u, Sc = ok ? (uni ? 1u : V.S) : 0u;
     const u32 tinc = wave_incl_scan_u32(Sl), tcinc = wave_incl_scan_u32(Sc);
@@ -1079,6 +1096,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
           const u32 rfull = 1u + pl.P.np + pl.P.ne;  // (the record of a sub-word with candidates)
           Q.u0[l] = pl.P.np | (min(rfull, 255u) << 8) | (Ls << 16);
           Q.uP[l] = (u32)min(A.P, (u64)0xFFFFFFFFu);
+          Q.upst[l] = pl.pst;
         }
         if (!f) atomicOr(&Q.bad[l], Ls ? 1u : 2u);  // (2: a sub-word past the lane slot)
         else {
@@ -1091,6 +1109,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
     WAVE_SYNC();
     // ---- word lane: the decision, one bump allocation per wave ----
     u32 ctot = Q.ctot[lane], btot = Q.btot[lane], rtot = Q.rtot[lane];
+    bool patch = false;
     if (ok && uni && V.S > 1 && !Q.bad[lane]) {
       // sub-words 1 .. S-1 of a uniform word: sub-word 0's layout with every combination
       const u32 u0 = Q.u0[lane], P = Q.uP[lane], np = u0 & 255u, rfull = (u0 >> 8) & 255u, Ls = u0 >> 16;
@@ -1099,6 +1118,8 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
       btot += (V.S - 1u) * b0;
       rtot += (V.S - 1u) * rfull;
       for (u32 s = 1; s < V.S; s++) Q.tinfo[Q.tbase[lane] + s] = (uint16_t)(np | (rfull << 4));
+      Q.ub0[lane] = b0;
+      patch = fixed && (Q.tinfo[Q.tbase[lane]] >> 4) == rfull;  // (sub-word 0 has its record)
     }
     const bool lngs = SMALL && ok && (Q.bad[lane] & 2u);  // a sub-word past the small slot: the large one decides
     ok = ok && !Q.bad[lane] && ctot >= 1 && ctot <= a.rseg;  // (one mode-engine item, as the probe's -s words)
@@ -1110,20 +1131,31 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
     const bool room = ok && base + mtot <= a.vrec_cap;
     Q.base[lane] = room ? base : ~0ull;
     Q.rtot[lane] = rtot;
+    // the build tasks (the planner: every sub-word, or sub-word 0 of a patched word) and the
+    // patch tasks (its sub-words 1 ..)
+    patch = patch && room;
+    const u32 Sb = room ? (patch ? 1u : V.S) : 0u, Sp = patch ? V.S - 1u : 0u;
+    const u32 binc = wave_incl_scan_u32(Sb), pinc = wave_incl_scan_u32(Sp);
+    const u32 nbtask = readlane_u32(binc, 63), nptask = readlane_u32(pinc, 63);
+    Q.tbb[lane] = (uint16_t)(binc - Sb);
+    Q.tpb[lane] = (uint16_t)(pinc - Sp);
+    if (lane == 63) { Q.tbb[64] = (uint16_t)nbtask; Q.tpb[64] = (uint16_t)nptask; }
     WAVE_SYNC();
+    (void)ntask;
     // ---- build pass: records and metas at the word's base ----
-    for (u32 t0 = 0; t0 < ntask; t0 += 64) {
+    for (u32 t0 = 0; t0 < nbtask; t0 += 64) {
       const u32 t = t0 + lane;
-      if (t < ntask) {
+      if (t < nbtask) {
         VsWord W;
         u32 l, s;
-        task_word(Q.tbase, t, W, l, s);
+        task_word(Q.tbb, t, W, l, s);
+        const u32 ts = Q.tbase[l] + s;  // (the sub-word's task in the record layout)
         const unsigned long long wb = Q.base[l];
         if (wb != ~0ull && !(VS_ABL & 1)) {
           const u32 wl = wv * 64 + l;
           u32 ro = 0;
-          for (u32 t2 = Q.tbase[l]; t2 < t; t2++) ro += Q.tinfo[t2] >> 4;
-          const u32 ti = Q.tinfo[t], np = ti & 15u, rs0 = ti >> 4;
+          for (u32 t2 = Q.tbase[l]; t2 < ts; t2++) ro += Q.tinfo[t2] >> 4;
+          const u32 ti = Q.tinfo[ts], np = ti & 15u, rs0 = ti >> 4;
           u64* rb = a.vrec + wb;
           u32 rs = 0;
           u64 cnt = 0, byt = 0;
@@ -1143,6 +1175,90 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
             rb[ro] = fr_hdr(P.np, P.ng, P.ne, P.maxl, P.nbig, P.bstarts, P.bRp);
           }
           rb[Q.rtot[l] + s] = cnt | ((u64)rs << 24) | (byt << 32);
+        }
+      }
+    }
+    // ---- patch pass: sub-word s >= 1 of a patched word = sub-word 0's record (written above by
+    // this wave) with every entry XORed by its piece's bytes of delta = sub-word s ^ sub-word 0
+    // (nonzero only on the tied occurrences); header and piece descriptors unchanged ----
+    if (nptask && !(VS_ABL & 1)) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (the wave's record stores before its loads)
+      for (u32 t0 = 0; t0 < nptask; t0 += 64) {
+        const u32 t = t0 + lane;
+        if (t < nptask) {
+          VsWord W;
+          u32 l, s;
+          task_word(Q.tpb, t, W, l, s);
+          s += 1u;
+          const u32 wl = wv * 64 + l;
+          const uint8_t* worig = wsl + wl * WSLOT;
+          const uint16_t* wocc = occ0 + wl;
+          // delta in the lane's sub-word slot: zero through byte L (the last byte a piece holds)
+          u32* dd = (u32*)sub;
+          for (u32 q = 0; q <= W.L / 4u; q++) dd[q] = 0u;
+          u32 ch[VS_TMAX];
+          u32 x = s;
+#pragma unroll
+          for (u32 tt = 0; tt < VS_TMAX; tt++) {
+            const u32 R = (W.tr >> (5 * tt)) & 31u;
+            const u32 key = (u32)(W.tk >> (10 * tt)) & 1023u;
+            const bool on = tt < W.nt;
+            const u32 d = on ? x % R : 0u;
+            x = on ? x / R : x;
+            ch[tt] = on ? T.keys[key].choice_base + d : 0u;
+          }
+          for (u32 j = 0; j < W.nocc; j++) {
+            const u32 e = wocc[j * VS_BLOCK];
+            const u32 q = e >> 10, key = e & 1023u;
+            u32 ci = ~0u;
+#pragma unroll
+            for (u32 tt = 0; tt < VS_TMAX; tt++)
+              if (tt < W.nt && ((u32)(W.tk >> (10 * tt)) & 1023u) == key) ci = ch[tt];
+            if (ci == ~0u) continue;
+            const u32 dv = lds_ld4(worig, q) ^ (u32)T.cval[ci], kl = T.keys[key].klen;  // (kl <= 4)
+            for (u32 b = 0; b < kl; b++) sub[q + b] = (uint8_t)(dv >> (8 * b));
+          }
+          const u32 u0 = Q.u0[l], np = u0 & 255u, rfull = (u0 >> 8) & 255u;
+          const u64 pst = Q.upst[l];
+          const unsigned long long wb = Q.base[l];
+          const u64* r0 = a.vrec + wb;
+          u64* rd = a.vrec + wb + (u64)s * rfull;
+          // header and descriptors; pe = end entry of each piece (8 bits each)
+          rd[0] = r0[0];
+          u64 pe = 0;
+#pragma unroll
+          for (u32 p = 0; p < FW_PMAX; p++) {
+            if (p < np) {
+              const u64 G = r0[1 + p];
+              rd[1 + p] = G;
+              pe |= (u64)((frd_ebase(G) + frd_R(G)) & 255u) << (8 * p);
+            }
+          }
+          auto pmask = [&](u32 p) -> u64 {
+            const u32 ps = (u32)(pst >> (7 * p)) & 127u;
+            return (u64)lds_ld4(sub, ps) | ((u64)lds_ld4(sub, ps + 4u) << 32);
+          };
+          u32 p = 0, pend = (u32)pe & 255u;
+          u64 m = pmask(0);
+          const u32 e0 = 1u + np;
+          for (u32 i0 = e0; i0 < rfull; i0 += 8) {
+            u64 v[8];
+#pragma unroll
+            for (u32 k = 0; k < 8; k++) v[k] = i0 + k < rfull ? r0[i0 + k] : 0ull;
+#pragma unroll
+            for (u32 k = 0; k < 8; k++) {
+              const u32 i = i0 + k;
+              if (i < rfull) {
+                if (i - e0 == pend) {  // (pieces' entries are contiguous, each piece >= 1)
+                  p++;
+                  pend = (u32)(pe >> (8 * p)) & 255u;
+                  m = pmask(p);
+                }
+                rd[i] = v[k] ^ (m & ((1ull << (8 * fw_len(v[k]))) - 1ull));
+              }
+            }
+          }
+          a.vrec[wb + Q.rtot[l] + s] = (u64)Q.uP[l] | ((u64)rfull << 24) | ((u64)Q.ub0[l] << 32);
         }
       }
     }

@@ -399,11 +399,14 @@ struct Planner {
   // window setup.  pick_balanced() takes it when it has as many big pieces as the greedy.
   u32 acap, aR, al, aspan;
   Plan A;
+  // first word byte of pieces 0..7 (7 bits each; k_keyspace_vsub's patched sub-words --
+  // dead code for every other user)
+  u64 pst;
 
   A5X_HD Planner(const W& w, const Tab& t, S& s, u32 balanced_cap = 0) : wd(w), T(t), sk(s) {
     P.np = 0; P.ng = 0; P.ne = 0; P.lconst = 0; P.maxl = 0; P.minl = 0; P.ok = true;
     P.nbig = 0; P.bstarts = 0; P.bent = 0; P.bRp = 0;
-    open = false; bR = 1; bl = 0; bspan = 0; cR = 1; cmax = 0; cmin = 0; cpi = 0; prev = 0;
+    open = false; bR = 1; bl = 0; bspan = 0; cR = 1; cmax = 0; cmin = 0; cpi = 0; prev = 0; pst = 0;
     acap = balanced_cap; aR = 1; al = 0; aspan = 0;
     A.nbig = 0; A.bstarts = 0; A.bent = 0; A.bRp = 0;
   }
@@ -441,7 +444,11 @@ struct Planner {
     P.ne += cR; P.ng++; P.maxl += cmax; P.minl += cmin;
     open = false;
   }
+  A5X_HD void piece_at(u32 pi, u32 off) {
+    if (pi < 8) pst |= (u64)(off & 127u) << (7 * pi);
+  }
   A5X_HD void literal(u32 off, u32 n, bool nl_last) {  // one literal piece of n bytes
+    piece_at(P.np, off);
     if constexpr (BUILD) {
       const u32 nb = nl_last ? n - 1 : n;
       u64 v = nb ? wd.ld(off, nb) : 0ull;
@@ -515,6 +522,7 @@ struct Planner {
         off += n; rem -= n;
       }
       open = true; cR = Ru; cmax = rem + ml; cmin = rem + U.mnl; cpi = P.np;
+      piece_at(cpi, off);
       P.np++;
       if constexpr (BUILD && CAP <= PL_SPLIT_CAP) {  // (read every choice, then write)
         const u64 rb = rem ? wd.ld(off, rem) : 0ull;
