@@ -749,7 +749,8 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
 #define VS_TMAX 4    // tied patterns per word
 #ifndef VS_ABL
 #define VS_ABL 0     // k_keyspace_vsub timing ablations (variant builds only, wrong output): 1 no build
-                     // pass, 2 no count pass, 4 no tasks (walk + pattern analysis only)
+                     // pass, 2 no count pass, 4 no tasks (walk + pattern analysis only), 16 fixed pass
+                     // without its record stores
 #endif
 #ifndef VS_GCAP
 #define VS_GCAP 4    // entries per open group of the sub-word planner (C5 -s A/B, 4 vs 8 = KS_GCAP:
@@ -757,7 +758,7 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
                      // words past 8 pieces)
 #endif
 #ifndef VS_PATCH
-#define VS_PATCH 1   // sub-words 1.. of a fixed-width uniform word patched from sub-word 0's record
+#define VS_PATCH 1   // the sub-words of a fixed-width uniform word written without the planner
                      // (0: every sub-word planned, the A/B baseline)
 #endif
 #ifndef VS_BLOCK
@@ -894,9 +895,11 @@ struct VsWave {  // per-wave LDS state
   uint4 info[64];                     // word: L | nocc << 8 | nt << 16 | S << 24, tr, tk
   unsigned long long base[64];
   uint16_t tbb[65];                   // first build task (the planner) of each lane's word (+ total)
-  uint16_t tpb[65];                   // first patch task (sub-words 1.. of a patched word) (+ total)
+  uint16_t tpb[65];                   // first fixed task (the sub-words of a fixed-width word) (+ total)
   u64 upst[64];                       // uniform word: sub-word 0's piece starts (Planner::pst)
+  u64 uhdr[64];                       // ... its record header
   u32 ub0[64];                        // ... and the bytes of each other sub-word
+  u32 tbits[64], tsel[64];            // fixed-width word: its tied occurrences (bit j), their pattern (2 bits each)
 };
 
 // Record sink of the build pass: the open group in LDS (lane-strided by VS_BLOCK),
@@ -1039,8 +1042,8 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
       }
     }
     // fixed width: every pattern of the word (units and tied) has all its choices as long as
-    // itself, so an entry's byte j is word byte (piece start + j) in every sub-word and
-    // sub-word s's record is sub-word 0's with the tied bytes changed (the patch tasks)
+    // itself, so an entry's byte j is word byte (piece start + j) in every sub-word, and every
+    // sub-word's record follows from sub-word 0's pieces (the fixed pass)
     bool fixed = VS_PATCH && ok && uni;
     for (u32 j = 0; fixed && j < V.nocc; j++) {
       const A5xKey key = T.keys[occ[j * VS_BLOCK] & 1023u];
@@ -1097,6 +1100,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
           Q.u0[l] = pl.P.np | (min(rfull, 255u) << 8) | (Ls << 16);
           Q.uP[l] = (u32)min(A.P, (u64)0xFFFFFFFFu);
           Q.upst[l] = pl.pst;
+          Q.uhdr[l] = fr_hdr(pl.P.np, pl.P.ng, pl.P.ne, pl.P.maxl, pl.P.nbig, pl.P.bstarts, pl.P.bRp);
         }
         if (!f) atomicOr(&Q.bad[l], Ls ? 1u : 2u);  // (2: a sub-word past the lane slot)
         else {
@@ -1119,7 +1123,18 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
       rtot += (V.S - 1u) * rfull;
       for (u32 s = 1; s < V.S; s++) Q.tinfo[Q.tbase[lane] + s] = (uint16_t)(np | (rfull << 4));
       Q.ub0[lane] = b0;
-      patch = fixed && (Q.tinfo[Q.tbase[lane]] >> 4) == rfull;  // (sub-word 0 has its record)
+      patch = fixed && (Q.tinfo[Q.tbase[lane]] >> 4) == rfull;  // (sub-word 0 has candidates)
+    }
+    if (patch) {
+      u32 tb = 0, ts = 0;
+      for (u32 j = 0; j < V.nocc; j++) {
+        const u32 key = occ[j * VS_BLOCK] & 1023u;
+#pragma unroll
+        for (u32 tt = 0; tt < VS_TMAX; tt++)
+          if (tt < V.nt && ((u32)(V.tk >> (10 * tt)) & 1023u) == key) { tb |= 1u << j; ts |= tt << (2 * j); }
+      }
+      Q.tbits[lane] = tb;
+      Q.tsel[lane] = ts;
     }
     const bool lngs = SMALL && ok && (Q.bad[lane] & 2u);  // a sub-word past the small slot: the large one decides
     ok = ok && !Q.bad[lane] && ctot >= 1 && ctot <= a.rseg;  // (one mode-engine item, as the probe's -s words)
@@ -1131,10 +1146,9 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
     const bool room = ok && base + mtot <= a.vrec_cap;
     Q.base[lane] = room ? base : ~0ull;
     Q.rtot[lane] = rtot;
-    // the build tasks (the planner: every sub-word, or sub-word 0 of a patched word) and the
-    // patch tasks (its sub-words 1 ..)
+    // the build tasks (the planner) and the fixed tasks (the sub-words of a fixed-width word)
     patch = patch && room;
-    const u32 Sb = room ? (patch ? 1u : V.S) : 0u, Sp = patch ? V.S - 1u : 0u;
+    const u32 Sb = room && !patch ? V.S : 0u, Sp = patch ? V.S : 0u;
     const u32 binc = wave_incl_scan_u32(Sb), pinc = wave_incl_scan_u32(Sp);
     const u32 nbtask = readlane_u32(binc, 63), nptask = readlane_u32(pinc, 63);
     Q.tbb[lane] = (uint16_t)(binc - Sb);
@@ -1178,88 +1192,92 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
         }
       }
     }
-    // ---- patch pass: sub-word s >= 1 of a patched word = sub-word 0's record (written above by
-    // this wave) with every entry XORed by its piece's bytes of delta = sub-word s ^ sub-word 0
-    // (nonzero only on the tied occurrences); header and piece descriptors unchanged ----
-    if (nptask && !(VS_ABL & 1)) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (the wave's record stores before its loads)
-      for (u32 t0 = 0; t0 < nptask; t0 += 64) {
-        const u32 t = t0 + lane;
-        if (t < nptask) {
-          VsWord W;
-          u32 l, s;
-          task_word(Q.tpb, t, W, l, s);
-          s += 1u;
-          const u32 wl = wv * 64 + l;
-          const uint8_t* worig = wsl + wl * WSLOT;
-          const uint16_t* wocc = occ0 + wl;
-          // delta in the lane's sub-word slot: zero through byte L (the last byte a piece holds)
-          u32* dd = (u32*)sub;
-          for (u32 q = 0; q <= W.L / 4u; q++) dd[q] = 0u;
-          u32 ch[VS_TMAX];
+    // ---- fixed pass: every sub-word of a fixed-width uniform word written without the planner.
+    // Its pieces are sub-word 0's (count pass: Q.upst, Q.uhdr) and every choice is as long as its
+    // pattern, so piece p's entry a is the sub-word's bytes [pst_p, pst_p + len_p) (tied choices
+    // in, '\n' at L) with each of the piece's units (at most two: R_p <= VS_GCAP) at a nonzero
+    // digit of a (first unit least significant) XORed from its key to that choice -- exactly the
+    // planner's entry, descriptor and meta ----
+    static_assert(VS_GCAP <= 4, "fixed pass: at most two units per piece");
+    for (u32 t0 = 0; t0 < nptask && !(VS_ABL & 1); t0 += 64) {
+      const u32 t = t0 + lane;
+      if (t < nptask) {
+        VsWord W;
+        u32 l, s;
+        task_word(Q.tpb, t, W, l, s);
+        const u32 wl = wv * 64 + l;
+        const uint16_t* wocc = occ0 + wl;
+        const u32 tbits = Q.tbits[l], tsel = Q.tsel[l];
+        // the tied patterns' choices (digits of s, first tied pattern least significant; s < 16)
+        u32 ch0 = 0, ch1 = 0, ch2 = 0, ch3 = 0;
+        {
           u32 x = s;
 #pragma unroll
           for (u32 tt = 0; tt < VS_TMAX; tt++) {
-            const u32 R = (W.tr >> (5 * tt)) & 31u;
-            const u32 key = (u32)(W.tk >> (10 * tt)) & 1023u;
-            const bool on = tt < W.nt;
-            const u32 d = on ? x % R : 0u;
-            x = on ? x / R : x;
-            ch[tt] = on ? T.keys[key].choice_base + d : 0u;
+            const u32 R = tt < W.nt ? (W.tr >> (5 * tt)) & 31u : 1u;
+            const u32 q = (u32)((float)x * __builtin_amdgcn_rcpf((float)R) + 0.03125f);  // (x < 16: exact)
+            const u32 c = T.keys[(u32)(W.tk >> (10 * tt)) & 1023u].choice_base + (x - q * R);
+            x = q;
+            if (tt == 0) ch0 = c; else if (tt == 1) ch1 = c; else if (tt == 2) ch2 = c; else ch3 = c;
           }
-          for (u32 j = 0; j < W.nocc; j++) {
-            const u32 e = wocc[j * VS_BLOCK];
-            const u32 q = e >> 10, key = e & 1023u;
-            u32 ci = ~0u;
-#pragma unroll
-            for (u32 tt = 0; tt < VS_TMAX; tt++)
-              if (tt < W.nt && ((u32)(W.tk >> (10 * tt)) & 1023u) == key) ci = ch[tt];
-            if (ci == ~0u) continue;
-            const u32 dv = lds_ld4(worig, q) ^ (u32)T.cval[ci], kl = T.keys[key].klen;  // (kl <= 4)
-            for (u32 b = 0; b < kl; b++) sub[q + b] = (uint8_t)(dv >> (8 * b));
-          }
-          const u32 u0 = Q.u0[l], np = u0 & 255u, rfull = (u0 >> 8) & 255u;
-          const u64 pst = Q.upst[l];
-          const unsigned long long wb = Q.base[l];
-          const u64* r0 = a.vrec + wb;
-          u64* rd = a.vrec + wb + (u64)s * rfull;
-          // header and descriptors; pe = end entry of each piece (8 bits each)
-          rd[0] = r0[0];
-          u64 pe = 0;
-#pragma unroll
-          for (u32 p = 0; p < FW_PMAX; p++) {
-            if (p < np) {
-              const u64 G = r0[1 + p];
-              rd[1 + p] = G;
-              pe |= (u64)((frd_ebase(G) + frd_R(G)) & 255u) << (8 * p);
-            }
-          }
-          auto pmask = [&](u32 p) -> u64 {
-            const u32 ps = (u32)(pst >> (7 * p)) & 127u;
-            return (u64)lds_ld4(sub, ps) | ((u64)lds_ld4(sub, ps + 4u) << 32);
-          };
-          u32 p = 0, pend = (u32)pe & 255u;
-          u64 m = pmask(0);
-          const u32 e0 = 1u + np;
-          for (u32 i0 = e0; i0 < rfull; i0 += 8) {
-            u64 v[8];
-#pragma unroll
-            for (u32 k = 0; k < 8; k++) v[k] = i0 + k < rfull ? r0[i0 + k] : 0ull;
-#pragma unroll
-            for (u32 k = 0; k < 8; k++) {
-              const u32 i = i0 + k;
-              if (i < rfull) {
-                if (i - e0 == pend) {  // (pieces' entries are contiguous, each piece >= 1)
-                  p++;
-                  pend = (u32)(pe >> (8 * p)) & 255u;
-                  m = pmask(p);
-                }
-                rd[i] = v[k] ^ (m & ((1ull << (8 * fw_len(v[k]))) - 1ull));
-              }
-            }
-          }
-          a.vrec[wb + Q.rtot[l] + s] = (u64)Q.uP[l] | ((u64)rfull << 24) | ((u64)Q.ub0[l] << 32);
         }
+        // the sub-word's bytes + '\n' in the lane's slot (the word slot is zero past L)
+        u32* sd = (u32*)sub;
+        const u32* od = (const u32*)(wsl + wl * WSLOT);
+        for (u32 q = 0; q <= W.L / 4u; q++) sd[q] = od[q];
+        for (u32 tb = tbits; tb; tb &= tb - 1u) {
+          const u32 j = __builtin_ctz(tb), tt = (tsel >> (2 * j)) & 3u;
+          const u32 e = wocc[j * VS_BLOCK], q = e >> 10, key = e & 1023u;
+          const u32 ci = tt == 0 ? ch0 : tt == 1 ? ch1 : tt == 2 ? ch2 : ch3;
+          if (ci == T.keys[key].choice_base) continue;  // (choice 0: the pattern itself)
+          const u32 kl = T.keys[key].klen, sh = 8u * (q & 3u);  // (kl <= 4)
+          const u64 msk = (((1ull << (8 * kl)) - 1ull) << sh), cv = (u64)(u32)T.cval[ci] << sh;
+          const u32 w0 = sd[q / 4u], w1 = sd[q / 4u + 1u];
+          const u64 nv = ((((u64)w1 << 32) | w0) & ~msk) | (cv & msk);
+          sd[q / 4u] = (u32)nv;
+          sd[q / 4u + 1u] = (u32)(nv >> 32);
+        }
+        sub[W.L] = (uint8_t)10;
+        const u32 u0 = Q.u0[l], np = u0 & 255u, rfull = (u0 >> 8) & 255u;
+        const u64 pst = Q.upst[l];
+        const unsigned long long wb = Q.base[l];
+        u64* rd = a.vrec + wb + (u64)s * rfull;  // (sub-word 0's record has rfull u64 too)
+        rd[0] = Q.uhdr[l];
+        u32 j = 0, eb = 0;
+        for (u32 p = 0; p < np; p++) {
+          const u32 ps = (u32)(pst >> (7 * p)) & 127u;
+          const u32 pe = p + 1 < np ? (u32)(pst >> (7 * (p + 1))) & 127u : W.L + 1u;
+          const u64 lm = (1ull << (8 * (pe - ps))) - 1ull;  // (len <= 7)
+          const u64 base = ((u64)lds_ld4(sub, ps) | ((u64)lds_ld4(sub, ps + 4u) << 32)) & lm;
+          // the piece's units: the untied occurrences in [ps, pe)
+          u32 nu = 0, R0 = 1, R1 = 1, o0 = 0, o1 = 0, c0 = 0, c1 = 0;
+          for (; j < W.nocc; j++) {
+            const u32 e = wocc[j * VS_BLOCK], q = e >> 10;
+            if (q >= pe) break;
+            if ((tbits >> j) & 1u) continue;
+            const A5xKey K = T.keys[e & 1023u];
+            const u32 R = a.rmode == 2 ? (u32)K.nvals + 1u : 2u;
+            if (nu == 0) { R0 = R; o0 = 8u * (q - ps); c0 = K.choice_base; }
+            else { R1 = R; o1 = 8u * (q - ps); c1 = K.choice_base; }
+            nu++;
+          }
+          const u32 R = R0 * R1;
+          rd[1 + p] = fr_desc(R, eb);
+          const u64 meta = fw_meta(pe - ps, R);
+          const u32 k0 = (u32)T.cval[c0], k1 = (u32)T.cval[c1];
+          u64* re = rd + 1 + np + eb;
+          for (u32 d1 = 0; d1 < R1; d1++) {
+            const u64 v1 = d1 ? base ^ ((u64)(k1 ^ (u32)T.cval[c1 + d1]) << o1) : base;
+            for (u32 d0 = 0; d0 < R0; d0++) {
+              const u64 v = d0 ? v1 ^ ((u64)(k0 ^ (u32)T.cval[c0 + d0]) << o0) : v1;
+              if (!(VS_ABL & 16) || v == 0x0123456789abcdefull) re[d1 * R0 + d0] = (v & lm) | meta;
+            }
+          }
+          eb += R;
+        }
+        const u32 cmin0 = s == 0 ? cmin : 0u, Ls1 = W.L + 1u;
+        const u32 cnt = Q.uP[l] - cmin0, byt = Q.ub0[l] - (cmin0 ? Ls1 : 0u);
+        a.vrec[wb + Q.rtot[l] + s] = (u64)cnt | ((u64)rfull << 24) | ((u64)byt << 32);
       }
     }
     // ---- word lane: results ----

@@ -136,7 +136,7 @@ A5X_HD u32 frh_R(u64 h, u32 b) { return ((u32)(h >> (40 + 6 * b)) & 63u) + 1u; }
 // to the entries) << 32 | (R-1) << 40 | (R == 1) << 63.  The digit of n is
 // d = n - q R with q = umulhi(n, magic) (+ n when R = 1): exact for n (R - 1) <
 // 2^32 (FW_PMAX_CNT bound).
-A5X_HD u32 fr_magic(u32 R) { return R > 1 ? (u32)((((u64)1 << 32) + R - 1) / R) : 0u; }
+A5X_HD u32 fr_magic(u32 R) { return R > 1 ? 0xFFFFFFFFu / R + 1u : 0u; }  // (= ceil(2^32 / R): a 32-bit division)
 A5X_HD u64 fr_desc(u32 R, u32 ebase) {
   return (u64)fr_magic(R) | ((u64)(ebase & 255u) << 32) | ((u64)(R - 1) << 40) | ((u64)(R == 1) << 63);
 }
