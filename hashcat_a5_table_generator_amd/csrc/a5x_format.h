@@ -82,7 +82,11 @@ enum : uint32_t {
 };
 
 // FAST words: bits 10..14 = group pieces, 16..23 = piece entries, 24..28 = pieces
-// (plan_word in a5x_kernels.hip).
+// (plan_word in a5x_kernels.hip).  Virtual words: bit 29 = A5X_WF_VFIX (below).
+enum : uint32_t {
+  A5X_WF_VFIX = 1u << 29,  // (with VIRT) fixed-width word: k_keyspace_vsub left a descriptor, k_vwords_fill writes
+                           // its sub-words' records
+};
 
 // Limits of the expansion passes (documented in DESIGN.md).
 #define A5X_WAVE 64

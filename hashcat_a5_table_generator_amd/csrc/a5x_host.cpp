@@ -698,11 +698,11 @@ A5xModeLaunch mode_launch(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_
 }
 
 // The virtual word list of a -s / -s -r batch with virtual words (k_keyspace_vsub): every
-// word one entry, a virtual word one per sub-word, records copied in list order; the
-// chunk -> first entry map of k_expand_fast over it.  byte_off null: no output layout
-// (fused digest).  Synchronises once.
-int build_virtual(a5x_ctx* c, uint64_t nw, const uint64_t* d_cand_off, const uint64_t* d_byte_off, hipStream_t st,
-                  Batch* B) {
+// word one entry, a virtual word one per sub-word, records in list order (copied, or written
+// from a fixed-width word's descriptor); the chunk -> first entry map of k_expand_fast over it.
+// byte_off null: no output layout (fused digest).  Synchronises once.
+int build_virtual(a5x_ctx* c, uint64_t nw, const uint8_t* d_words, const uint64_t* d_woff, int mode, int mn,
+                  const uint64_t* d_cand_off, const uint64_t* d_byte_off, hipStream_t st, Batch* B) {
   int rc;
   if ((rc = grow(c, c->vpre, nw + 1)) || (rc = grow(c, c->vrpre, nw + 1))) return rc;
   HIPCHK(c, a5x_launch_vwords_sizes(c->flags.p, d_cand_off, nw, c->vn.p, c->vrsz.p, st));
@@ -723,6 +723,8 @@ int build_virtual(a5x_ctx* c, uint64_t nw, const uint64_t* d_cand_off, const uin
   V.vrec = c->vrec.p; V.vpre = c->vpre.p; V.vrpre = c->vrpre.p; V.nw = nw;
   V.vcand_off = c->vcand_off.p; V.vbyte_off = c->vbyte_off.p; V.vflags = c->vflags.p; V.vroff = c->vroff.p;
   V.vmap = c->vmap.p; V.vobase = c->vobase.p; V.vrec2 = c->vrec2.p;
+  V.table = c->d_table; V.table_bytes = c->table_bytes; V.rmode = mode; V.rcmin = mn > 0 ? 1u : 0u;
+  V.words = d_words; V.woff = d_woff;
   HIPCHK(c, a5x_launch_vwords_fill(V, st));
   if (B->total_cands) {
     const uint64_t nchunks = (B->total_cands + c->chunk - 1) / c->chunk;
@@ -961,7 +963,7 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
     HIPCHK(c, hipStreamSynchronize(st));
     if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
     B->total_bytes = 0;
-    return vused ? build_virtual(c, nw, d_cand_off, nullptr, st, B) : A5X_OK;
+    return vused ? build_virtual(c, nw, d_words, d_woff, mode, mn, d_cand_off, nullptr, st, B) : A5X_OK;
   }
   if (items) HIPCHK(c, a5x_launch_mode_items(M, 0, st));
   if (items)
@@ -975,7 +977,7 @@ int run_keyspace_mode(a5x_ctx* c, const uint8_t* d_words, const uint64_t* d_woff
   HIPCHK(c, hipStreamSynchronize(st));
   if ((rc = decode_dev_err(c, c->h_scalars[2]))) return rc;
   B->total_bytes = c->h_totals[1];
-  return vused ? build_virtual(c, nw, d_cand_off, d_byte_off, st, B) : A5X_OK;
+  return vused ? build_virtual(c, nw, d_words, d_woff, mode, mn, d_cand_off, d_byte_off, st, B) : A5X_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -761,6 +761,7 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
 #define VS_PATCH 1   // the sub-words of a fixed-width uniform word written without the planner
                      // (0: every sub-word planned, the A/B baseline)
 #endif
+#define VS_DESC 10   // u64 descriptor of a fixed-width virtual word (k_keyspace_vsub -> k_vwords_fill, FvWord)
 #ifndef VS_BLOCK
 #define VS_BLOCK 128 // k_keyspace_vsub workgroup: two waves share the table copy (C5 -s A/B, profiles/r05r_ab_vsub_block_c5.txt:
                      // 16.98 ms vs 17.85 ms at 64, 17.19 at 256)
@@ -895,11 +896,9 @@ struct VsWave {  // per-wave LDS state
   uint4 info[64];                     // word: L | nocc << 8 | nt << 16 | S << 24, tr, tk
   unsigned long long base[64];
   uint16_t tbb[65];                   // first build task (the planner) of each lane's word (+ total)
-  uint16_t tpb[65];                   // first fixed task (the sub-words of a fixed-width word) (+ total)
   u64 upst[64];                       // uniform word: sub-word 0's piece starts (Planner::pst)
   u64 uhdr[64];                       // ... its record header
   u32 ub0[64];                        // ... and the bytes of each other sub-word
-  u32 tbits[64], tsel[64];            // fixed-width word: its tied occurrences (bit j), their pattern (2 bits each)
 };
 
 // Record sink of the build pass: the open group in LDS (lane-strided by VS_BLOCK),
@@ -1125,20 +1124,11 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
       Q.ub0[lane] = b0;
       patch = fixed && (Q.tinfo[Q.tbase[lane]] >> 4) == rfull;  // (sub-word 0 has candidates)
     }
-    if (patch) {
-      u32 tb = 0, ts = 0;
-      for (u32 j = 0; j < V.nocc; j++) {
-        const u32 key = occ[j * VS_BLOCK] & 1023u;
-#pragma unroll
-        for (u32 tt = 0; tt < VS_TMAX; tt++)
-          if (tt < V.nt && ((u32)(V.tk >> (10 * tt)) & 1023u) == key) { tb |= 1u << j; ts |= tt << (2 * j); }
-      }
-      Q.tbits[lane] = tb;
-      Q.tsel[lane] = ts;
-    }
+
     const bool lngs = SMALL && ok && (Q.bad[lane] & 2u);  // a sub-word past the small slot: the large one decides
     ok = ok && !Q.bad[lane] && ctot >= 1 && ctot <= a.rseg;  // (one mode-engine item, as the probe's -s words)
-    const u32 mtot = ok ? rtot + V.S : 0u;
+    patch = patch && ok;
+    const u32 mtot = ok ? (patch ? VS_DESC : rtot + V.S) : 0u;  // (a fixed-width word: its descriptor)
     const u32 minc = wave_incl_scan_u32(mtot);
     unsigned long long wbase = 0;
     if (lane == 63 && minc) wbase = atomicAdd(a.vrec_n, (unsigned long long)minc);
@@ -1146,14 +1136,37 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
     const bool room = ok && base + mtot <= a.vrec_cap;
     Q.base[lane] = room ? base : ~0ull;
     Q.rtot[lane] = rtot;
-    // the build tasks (the planner) and the fixed tasks (the sub-words of a fixed-width word)
+    // the build tasks (the planner); a fixed-width word's sub-words are written by k_vwords_fill
+    // from its descriptor, straight into the virtual word list's record area
     patch = patch && room;
-    const u32 Sb = room && !patch ? V.S : 0u, Sp = patch ? V.S : 0u;
-    const u32 binc = wave_incl_scan_u32(Sb), pinc = wave_incl_scan_u32(Sp);
-    const u32 nbtask = readlane_u32(binc, 63), nptask = readlane_u32(pinc, 63);
+    const u32 Sb = room && !patch ? V.S : 0u;
+    const u32 binc = wave_incl_scan_u32(Sb);
+    const u32 nbtask = readlane_u32(binc, 63);
     Q.tbb[lane] = (uint16_t)(binc - Sb);
-    Q.tpb[lane] = (uint16_t)(pinc - Sp);
-    if (lane == 63) { Q.tbb[64] = (uint16_t)nbtask; Q.tpb[64] = (uint16_t)nptask; }
+    if (lane == 63) Q.tbb[64] = (uint16_t)nbtask;
+    if (patch) {
+      u32 tb = 0, ts = 0;
+      u64 oc[4] = {0, 0, 0, 0};
+      for (u32 j = 0; j < V.nocc; j++) {
+        const u32 e = occ[j * VS_BLOCK], key = e & 1023u;
+#pragma unroll
+        for (u32 tt = 0; tt < VS_TMAX; tt++)
+          if (tt < V.nt && ((u32)(V.tk >> (10 * tt)) & 1023u) == key) { tb |= 1u << j; ts |= tt << (2 * j); }
+#pragma unroll
+        for (u32 k = 0; k < 4; k++)
+          if (j / 4u == k) oc[k] |= (u64)e << (16 * (j & 3u));
+      }
+      const u32 u0 = Q.u0[lane];
+      u64* d = a.vrec + base;
+      d[0] = Q.uhdr[lane];
+      d[1] = Q.upst[lane];
+      d[2] = V.tk | ((u64)V.nt << 40) | ((u64)V.S << 44) | ((u64)V.L << 49) | ((u64)(u0 & 15u) << 56);
+      d[3] = (u64)V.tr | ((u64)((u0 >> 8) & 255u) << 20) | ((u64)V.nocc << 28);
+      d[4] = (u64)Q.uP[lane] | ((u64)Q.ub0[lane] << 32);
+      d[5] = (u64)tb | ((u64)ts << 16);
+#pragma unroll
+      for (u32 k = 0; k < 4; k++) d[6 + k] = oc[k];
+    }
     WAVE_SYNC();
     (void)ntask;
     // ---- build pass: records and metas at the word's base ----
@@ -1192,99 +1205,11 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
         }
       }
     }
-    // ---- fixed pass: every sub-word of a fixed-width uniform word written without the planner.
-    // Its pieces are sub-word 0's (count pass: Q.upst, Q.uhdr) and every choice is as long as its
-    // pattern, so piece p's entry a is the sub-word's bytes [pst_p, pst_p + len_p) (tied choices
-    // in, '\n' at L) with each of the piece's units (at most two: R_p <= VS_GCAP) at a nonzero
-    // digit of a (first unit least significant) XORed from its key to that choice -- exactly the
-    // planner's entry, descriptor and meta ----
-    static_assert(VS_GCAP <= 4, "fixed pass: at most two units per piece");
-    for (u32 t0 = 0; t0 < nptask && !(VS_ABL & 1); t0 += 64) {
-      const u32 t = t0 + lane;
-      if (t < nptask) {
-        VsWord W;
-        u32 l, s;
-        task_word(Q.tpb, t, W, l, s);
-        const u32 wl = wv * 64 + l;
-        const uint16_t* wocc = occ0 + wl;
-        const u32 tbits = Q.tbits[l], tsel = Q.tsel[l];
-        // the tied patterns' choices (digits of s, first tied pattern least significant; s < 16)
-        u32 ch0 = 0, ch1 = 0, ch2 = 0, ch3 = 0;
-        {
-          u32 x = s;
-#pragma unroll
-          for (u32 tt = 0; tt < VS_TMAX; tt++) {
-            const u32 R = tt < W.nt ? (W.tr >> (5 * tt)) & 31u : 1u;
-            const u32 q = (u32)((float)x * __builtin_amdgcn_rcpf((float)R) + 0.03125f);  // (x < 16: exact)
-            const u32 c = T.keys[(u32)(W.tk >> (10 * tt)) & 1023u].choice_base + (x - q * R);
-            x = q;
-            if (tt == 0) ch0 = c; else if (tt == 1) ch1 = c; else if (tt == 2) ch2 = c; else ch3 = c;
-          }
-        }
-        // the sub-word's bytes + '\n' in the lane's slot (the word slot is zero past L)
-        u32* sd = (u32*)sub;
-        const u32* od = (const u32*)(wsl + wl * WSLOT);
-        for (u32 q = 0; q <= W.L / 4u; q++) sd[q] = od[q];
-        for (u32 tb = tbits; tb; tb &= tb - 1u) {
-          const u32 j = __builtin_ctz(tb), tt = (tsel >> (2 * j)) & 3u;
-          const u32 e = wocc[j * VS_BLOCK], q = e >> 10, key = e & 1023u;
-          const u32 ci = tt == 0 ? ch0 : tt == 1 ? ch1 : tt == 2 ? ch2 : ch3;
-          if (ci == T.keys[key].choice_base) continue;  // (choice 0: the pattern itself)
-          const u32 kl = T.keys[key].klen, sh = 8u * (q & 3u);  // (kl <= 4)
-          const u64 msk = (((1ull << (8 * kl)) - 1ull) << sh), cv = (u64)(u32)T.cval[ci] << sh;
-          const u32 w0 = sd[q / 4u], w1 = sd[q / 4u + 1u];
-          const u64 nv = ((((u64)w1 << 32) | w0) & ~msk) | (cv & msk);
-          sd[q / 4u] = (u32)nv;
-          sd[q / 4u + 1u] = (u32)(nv >> 32);
-        }
-        sub[W.L] = (uint8_t)10;
-        const u32 u0 = Q.u0[l], np = u0 & 255u, rfull = (u0 >> 8) & 255u;
-        const u64 pst = Q.upst[l];
-        const unsigned long long wb = Q.base[l];
-        u64* rd = a.vrec + wb + (u64)s * rfull;  // (sub-word 0's record has rfull u64 too)
-        rd[0] = Q.uhdr[l];
-        u32 j = 0, eb = 0;
-        for (u32 p = 0; p < np; p++) {
-          const u32 ps = (u32)(pst >> (7 * p)) & 127u;
-          const u32 pe = p + 1 < np ? (u32)(pst >> (7 * (p + 1))) & 127u : W.L + 1u;
-          const u64 lm = (1ull << (8 * (pe - ps))) - 1ull;  // (len <= 7)
-          const u64 base = ((u64)lds_ld4(sub, ps) | ((u64)lds_ld4(sub, ps + 4u) << 32)) & lm;
-          // the piece's units: the untied occurrences in [ps, pe)
-          u32 nu = 0, R0 = 1, R1 = 1, o0 = 0, o1 = 0, c0 = 0, c1 = 0;
-          for (; j < W.nocc; j++) {
-            const u32 e = wocc[j * VS_BLOCK], q = e >> 10;
-            if (q >= pe) break;
-            if ((tbits >> j) & 1u) continue;
-            const A5xKey K = T.keys[e & 1023u];
-            const u32 R = a.rmode == 2 ? (u32)K.nvals + 1u : 2u;
-            if (nu == 0) { R0 = R; o0 = 8u * (q - ps); c0 = K.choice_base; }
-            else { R1 = R; o1 = 8u * (q - ps); c1 = K.choice_base; }
-            nu++;
-          }
-          const u32 R = R0 * R1;
-          rd[1 + p] = fr_desc(R, eb);
-          const u64 meta = fw_meta(pe - ps, R);
-          const u32 k0 = (u32)T.cval[c0], k1 = (u32)T.cval[c1];
-          u64* re = rd + 1 + np + eb;
-          for (u32 d1 = 0; d1 < R1; d1++) {
-            const u64 v1 = d1 ? base ^ ((u64)(k1 ^ (u32)T.cval[c1 + d1]) << o1) : base;
-            for (u32 d0 = 0; d0 < R0; d0++) {
-              const u64 v = d0 ? v1 ^ ((u64)(k0 ^ (u32)T.cval[c0 + d0]) << o0) : v1;
-              if (!(VS_ABL & 16) || v == 0x0123456789abcdefull) re[d1 * R0 + d0] = (v & lm) | meta;
-            }
-          }
-          eb += R;
-        }
-        const u32 cmin0 = s == 0 ? cmin : 0u, Ls1 = W.L + 1u;
-        const u32 cnt = Q.uP[l] - cmin0, byt = Q.ub0[l] - (cmin0 ? Ls1 : 0u);
-        a.vrec[wb + Q.rtot[l] + s] = (u64)cnt | ((u64)rfull << 24) | ((u64)byt << 32);
-      }
-    }
     // ---- word lane: results ----
     if (room) {
       a.count[w] = ctot;
       a.bytes[w] = btot;
-      a.flags[w] = A5X_WF_FAST | A5X_WF_VIRT;
+      a.flags[w] = A5X_WF_FAST | A5X_WF_VIRT | (patch ? A5X_WF_VFIX : 0u);
       a.rnseg[w] = 1;
       a.roff[w] = (u32)base;
       a.vn[w] = V.S - 1u;
@@ -1304,7 +1229,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
 
 // k_expand_fast over a batch with virtual words runs on the virtual word list: every word
 // one entry (mode-engine words as holes, flags 0), a virtual word one entry per sub-word;
-// records copied into one area in list order (each window one contiguous copy).
+// records in one area in list order (each window one contiguous copy).
 struct VwArgs {
   const u32* flags;
   const u64* cand_off;
@@ -1322,6 +1247,13 @@ struct VwArgs {
   u32* vmap;    // entry -> word
   u32* vobase;  // entry -> its first candidate's index in the word
   u64* vrec2;
+  // fixed-width virtual words (A5X_WF_VFIX): the table and the words
+  const uint8_t* table;
+  u32 table_bytes;
+  int rmode;
+  u32 rcmin;
+  const uint8_t* words;
+  const u64* woff;
 };
 
 // record u64 of the words that are not virtual (virtual words: k_keyspace_vsub)
@@ -1336,7 +1268,132 @@ __global__ void __launch_bounds__(256) k_vwords_sizes(const u32* flags, const u6
   }
 }
 
+// A fixed-width virtual word (k_keyspace_vsub's descriptor d, VS_DESC u64): d0 the sub-words'
+// record header, d1 their piece starts (7 bits each), d2 tk | nt << 40 | S << 44 | L << 49 |
+// np << 56, d3 tr | rfull << 20 | nocc << 28, d4 P | (bytes of a sub-word s >= 1) << 32, d5 tied
+// occurrences (bit j) | their tied pattern << 16 (2 bits each), d6..d9 the occurrences (u16 q << 10 | key).
+struct FvWord {
+  u64 hdr, pst, tk;
+  u32 nt, S, L, np, tr, rfull, nocc, P, b0, tbits, tsel;
+  u64 oc0, oc1, oc2, oc3;  // (named, not an array: a dynamic index would put the struct in scratch)
+  __device__ __forceinline__ void load(const u64* d) {
+    hdr = d[0]; pst = d[1];
+    const u64 d2 = d[2], d3 = d[3], d4 = d[4], d5 = d[5];
+    tk = d2 & 0xFFFFFFFFFFull; nt = (u32)(d2 >> 40) & 7u; S = (u32)(d2 >> 44) & 31u; L = (u32)(d2 >> 49) & 127u;
+    np = (u32)(d2 >> 56) & 15u;
+    tr = (u32)d3 & 0xFFFFFu; rfull = (u32)(d3 >> 20) & 255u; nocc = (u32)(d3 >> 28) & 31u;
+    P = (u32)d4; b0 = (u32)(d4 >> 32);
+    tbits = (u32)d5 & 0xFFFFu; tsel = (u32)(d5 >> 16);
+    oc0 = d[6]; oc1 = d[7]; oc2 = d[8]; oc3 = d[9];
+  }
+  __device__ __forceinline__ u32 oc(u32 j) const {
+    const u32 k = j >> 2;  // (value masks, not a select of members: that becomes a dynamic index)
+    const u64 o = (oc0 & (0ull - (u64)(k == 0))) | (oc1 & (0ull - (u64)(k == 1))) | (oc2 & (0ull - (u64)(k == 2))) |
+                  (oc3 & (0ull - (u64)(k == 3)));
+    return (u32)(o >> (16 * (j & 3u))) & 0xFFFFu;
+  }
+};
+
+// Sub-word s's record of a fixed-width word at rd.  Its pieces are sub-word 0's (the count pass
+// planned it) and every choice is as long as its pattern, so piece p's entry a is the sub-word's
+// bytes [pst_p, pst_p + len_p) (tied choices in, '\n' at L) with each of the piece's units (at
+// most two: R_p <= VS_GCAP) at a nonzero digit of a (first unit least significant) XORed from
+// its key to that choice -- the planner's entry, descriptor and meta.  sub: FV_SLOT bytes of LDS;
+// wd: the word's bytes (global).
+static_assert(VS_GCAP <= 4, "fixed-width sub-words: at most two units per piece");
+__device__ __forceinline__ void fv_subword(const Tab& T, const FvWord& F, const uint8_t* wd, u32 s, int rmode, uint8_t* sub, u64* rd) {
+  // the tied patterns' choices (digits of s, first tied pattern least significant; s < 16)
+  u32 ch0 = 0, ch1 = 0, ch2 = 0, ch3 = 0;
+  {
+    u32 x = s;
+#pragma unroll
+    for (u32 tt = 0; tt < VS_TMAX; tt++) {
+      const u32 R = tt < F.nt ? (F.tr >> (5 * tt)) & 31u : 1u;
+      const u32 q = (u32)((float)x * __builtin_amdgcn_rcpf((float)R) + 0.03125f);  // (x < 16: exact)
+      const u32 c = T.keys[(u32)(F.tk >> (10 * tt)) & 1023u].choice_base + (x - q * R);
+      x = q;
+      if (tt == 0) ch0 = c; else if (tt == 1) ch1 = c; else if (tt == 2) ch2 = c; else ch3 = c;
+    }
+  }
+  // the word's bytes (aligned dwords, shifted into place; the words buffer has 16 readable
+  // bytes past the last word), tied choices written over their occurrences, '\n' at L
+  u32* sd = (u32*)sub;
+  {
+    const u64 a0 = (u64)wd;
+    const u32* src = (const u32*)(a0 & ~3ull);
+    const u32 sh = (u32)(a0 & 3u), nd = F.L / 4u + 1u;
+    u32 lo = src[0];
+    for (u32 q = 0; q < nd; q++) {
+      const u32 hi = src[q + 1];
+      sd[q] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+      lo = hi;
+    }
+  }
+  for (u32 tb = F.tbits; tb; tb &= tb - 1u) {
+    const u32 j = __builtin_ctz(tb), tt = (F.tsel >> (2 * j)) & 3u;
+    const u32 e = F.oc(j), q = e >> 10, key = e & 1023u;
+    const u32 ci = tt == 0 ? ch0 : tt == 1 ? ch1 : tt == 2 ? ch2 : ch3;
+    if (ci == T.keys[key].choice_base) continue;  // (choice 0: the pattern itself)
+    const u32 kl = T.keys[key].klen, sh = 8u * (q & 3u);  // (kl <= 4)
+    const u64 msk = (((1ull << (8 * kl)) - 1ull) << sh), cv = (u64)(u32)T.cval[ci] << sh;
+    const u32 w0 = sd[q / 4u], w1 = sd[q / 4u + 1u];
+    const u64 nv = ((((u64)w1 << 32) | w0) & ~msk) | (cv & msk);
+    sd[q / 4u] = (u32)nv;
+    sd[q / 4u + 1u] = (u32)(nv >> 32);
+  }
+  sub[F.L] = (uint8_t)10;
+  rd[0] = F.hdr;
+  u32 j = 0, eb = 0;
+  for (u32 p = 0; p < F.np; p++) {
+    const u32 ps = (u32)(F.pst >> (7 * p)) & 127u;
+    const u32 pe = p + 1 < F.np ? (u32)(F.pst >> (7 * (p + 1))) & 127u : F.L + 1u;
+    const u64 lm = (1ull << (8 * (pe - ps))) - 1ull;  // (len <= 7)
+    const u64 base = ((u64)lds_ld4(sub, ps) | ((u64)lds_ld4(sub, ps + 4u) << 32)) & lm;
+    // the piece's units: the untied occurrences in [ps, pe)
+    u32 nu = 0, R0 = 1, R1 = 1, o0 = 0, o1 = 0, c0 = 0, c1 = 0;
+    for (; j < F.nocc; j++) {
+      const u32 e = F.oc(j), q = e >> 10;
+      if (q >= pe) break;
+      if ((F.tbits >> j) & 1u) continue;
+      const A5xKey K = T.keys[e & 1023u];
+      const u32 R = rmode == 2 ? (u32)K.nvals + 1u : 2u;
+      if (nu == 0) { R0 = R; o0 = 8u * (q - ps); c0 = K.choice_base; }
+      else { R1 = R; o1 = 8u * (q - ps); c1 = K.choice_base; }
+      nu++;
+    }
+    const u32 R = R0 * R1;
+    rd[1 + p] = fr_desc(R, eb);
+    const u64 meta = fw_meta(pe - ps, R);
+    const u32 k0 = (u32)T.cval[c0], k1 = (u32)T.cval[c1];
+    u64* re = rd + 1 + F.np + eb;
+    for (u32 d1 = 0; d1 < R1; d1++) {
+      const u64 v1 = d1 ? base ^ ((u64)(k1 ^ (u32)T.cval[c1 + d1]) << o1) : base;
+      for (u32 d0 = 0; d0 < R0; d0++) {
+        const u64 v = d0 ? v1 ^ ((u64)(k0 ^ (u32)T.cval[c0 + d0]) << o0) : v1;
+        re[d1 * R0 + d0] = (v & lm) | meta;
+      }
+    }
+    eb += R;
+  }
+}
+
+#define FV_SLOT 96  // k_vwords_fill: per-lane sub-word bytes (+ '\n' + read slack; words <= VS_SLOT - 8)
+struct FvWave {
+  uint16_t tb[65];  // first fixed-width sub-word task of each lane's word (+ total)
+  u32 w[64];        // the lane's word
+  u32 d[64];        // its descriptor (vrec offset)
+  unsigned long long r0[64];  // its first record u64 in vrec2
+};
+static size_t vwords_fill_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + 256 * FV_SLOT + 4 * sizeof(FvWave); }
+
 __global__ void __launch_bounds__(256) k_vwords_fill(VwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const u32 tbytes = (a.table_bytes + 15u) & ~15u;
+  if (a.table) load_table(smem, a.table, a.table_bytes);
+  __syncthreads();
+  const Tab T = tab_view(smem);
+  uint8_t* sub = smem + tbytes + threadIdx.x * FV_SLOT;
+  FvWave& Q = ((FvWave*)(smem + tbytes + 256 * FV_SLOT))[threadIdx.x / 64];
   const u32 lane = lane_id();
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 wb = (u64)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); wb < a.nw; wb += stride) {
@@ -1345,12 +1402,29 @@ __global__ void __launch_bounds__(256) k_vwords_fill(VwArgs a) {
     const u32 f = valid ? a.flags[w] : 0u;
     const u64 v0 = valid ? w + a.vpre[w] : 0ull, r0 = valid ? a.vrpre[w] : 0ull;
     const u64 c0 = valid ? a.cand_off[w] : 0ull, b0 = valid && a.byte_off ? a.byte_off[w] : 0ull;
-    const u32 nrec = valid ? (u32)(a.vrpre[w + 1] - r0) : 0u;
+    u32 nrec = valid ? (u32)(a.vrpre[w + 1] - r0) : 0u;
+    const bool fix = valid && (f & A5X_WF_VFIX);
     u64 src = 0;  // (address of the word's records)
     if (valid && !(f & A5X_WF_VIRT)) {
       a.vcand_off[v0] = c0; a.vbyte_off[v0] = b0; a.vflags[v0] = nrec ? f : 0u; a.vroff[v0] = (u32)r0;
       a.vmap[v0] = (u32)w; a.vobase[v0] = 0;
       if (nrec) src = (u64)(a.rec + a.roff[w]);
+    } else if (fix) {
+      // every sub-word: the same layout; sub-word 0 without the all-keep word when min >= 1
+      const u64* d = a.vrec + a.roff[w];
+      const u64 hdr = d[0], d2 = d[2], d3 = d[3], d4 = d[4];
+      const u32 S = (u32)(d2 >> 44) & 31u, Ls1 = ((u32)(d2 >> 49) & 127u) + 1u, rs = (u32)(d3 >> 20) & 255u;
+      const u32 P = (u32)d4, bs = (u32)(d4 >> 32);
+      const u32 vf = A5X_WF_FAST | A5X_WF_RADIX | (frh_ng(hdr) << 10) | (frh_ne(hdr) << 16) | (frh_np(hdr) << 24);
+      u64 co = 0, bo = 0;
+      for (u32 s = 0; s < S; s++) {
+        const u64 v = v0 + s;
+        a.vcand_off[v] = c0 + co; a.vbyte_off[v] = b0 + bo; a.vflags[v] = vf; a.vroff[v] = (u32)(r0 + (u64)s * rs);
+        a.vmap[v] = (u32)w; a.vobase[v] = (u32)co;
+        const u32 cut = s == 0 ? a.rcmin : 0u;
+        co += P - cut; bo += bs - (cut ? Ls1 : 0u);
+      }
+      nrec = 0;  // (written below, not copied)
     } else if (valid) {
       const u64* vr = a.vrec + a.roff[w];
       src = (u64)vr;
@@ -1376,7 +1450,29 @@ __global__ void __launch_bounds__(256) k_vwords_fill(VwArgs a) {
       a.vcand_off[ve] = a.cand_off[a.nw];
       a.vbyte_off[ve] = a.byte_off ? a.byte_off[a.nw] : 0ull;
     }
-    // the records: the wave copies its lanes' ranges in lane order (contiguous ones merged)
+    // the fixed-width words' sub-words as tasks over the wave's lanes
+    const u32 Sf = fix ? (u32)(a.vpre[w + 1] - a.vpre[w]) + 1u : 0u;
+    const u32 finc = wave_incl_scan_u32(Sf), nft = readlane_u32(finc, 63);
+    if (nft) {
+      Q.tb[lane] = (uint16_t)(finc - Sf);
+      if (lane == 63) Q.tb[64] = (uint16_t)nft;
+      Q.w[lane] = (u32)w;
+      Q.d[lane] = valid ? a.roff[w] : 0u;
+      Q.r0[lane] = r0;
+      WAVE_SYNC();
+      for (u32 t0 = 0; t0 < nft; t0 += 64) {
+        const u32 t = t0 + lane;
+        if (t < nft) {
+          const u32 l = vs_owner(Q.tb, t), s = t - Q.tb[l];
+          FvWord F;
+          F.load(a.vrec + Q.d[l]);
+          const u64 ww = Q.w[l];
+          fv_subword(T, F, a.words + a.woff[ww], s, a.rmode, sub, a.vrec2 + Q.r0[l] + (u64)s * F.rfull);
+        }
+      }
+      WAVE_SYNC();  // (Q is rewritten by the next words)
+    }
+    // the other records: the wave copies its lanes' ranges in lane order (contiguous ones merged)
     u64 cs = 0, cd = 0;
     u32 cn = 0;
     auto copy = [&]() {
@@ -3374,7 +3470,9 @@ hipError_t a5x_launch_vwords_fill(const A5xVwLaunch& L, hipStream_t st) {
   a.vrec = L.vrec; a.vpre = L.vpre; a.vrpre = L.vrpre; a.nw = L.nw;
   a.vcand_off = L.vcand_off; a.vbyte_off = L.vbyte_off; a.vflags = L.vflags; a.vroff = L.vroff;
   a.vmap = L.vmap; a.vobase = L.vobase; a.vrec2 = L.vrec2;
-  hipLaunchKernelGGL(k_vwords_fill, dim3(blocks_for(L.nw, 256, 8192)), dim3(256), 0, st, a);
+  a.table = L.table; a.table_bytes = L.table_bytes; a.rmode = L.rmode; a.rcmin = L.rcmin; a.words = L.words;
+  a.woff = L.woff;
+  hipLaunchKernelGGL(k_vwords_fill, dim3(blocks_for(L.nw, 256, 8192)), dim3(256), vwords_fill_lds(L.table_bytes), st, a);
   return hipGetLastError();
 }
 
@@ -3556,6 +3654,8 @@ hipError_t a5x_set_kernel_attrs() {
   e = hipFuncSetAttribute((const void*)k_keyspace_vsub<VS_WSLOT, VS_SLOT, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_keyspace_vsub<VS_WSLOT_S, VS_SLOT_S, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_vwords_fill, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_locate, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;

@@ -71,6 +71,14 @@ struct A5xVwLaunch {
   uint32_t* vmap;
   uint32_t* vobase;
   uint64_t* vrec2;
+  // fixed-width virtual words (A5X_WF_VFIX): their sub-words' records are written here from the
+  // descriptors k_keyspace_vsub left
+  const uint8_t* table;
+  uint32_t table_bytes;
+  int rmode;
+  uint32_t rcmin;
+  const uint8_t* words;
+  const uint64_t* woff;
 };
 size_t a5x_keyspace_vsub_lds(uint32_t table_bytes);
 hipError_t a5x_launch_vsub(const A5xKsLaunch& L, hipStream_t st);
