@@ -762,6 +762,10 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
                      // (0: every sub-word planned, the A/B baseline)
 #endif
 #define VS_DESC 10   // u64 descriptor of a fixed-width virtual word (k_keyspace_vsub -> k_vwords_fill, FvWord)
+#ifndef FV_SLOT
+#define FV_SLOT 100  // k_vwords_fill: per-lane sub-word bytes (25 dwords: an odd stride keeps lanes on distinct
+                     // banks; 64 / 68 / 100: 5.08 / 4.04 / 3.87 ms on C5 -s); fixed-width words up to FV_SLOT - 8 bytes
+#endif
 #ifndef VS_BLOCK
 #define VS_BLOCK 128 // k_keyspace_vsub workgroup: two waves share the table copy (C5 -s A/B, profiles/r05r_ab_vsub_block_c5.txt:
                      // 16.98 ms vs 17.85 ms at 64, 17.19 at 256)
@@ -1043,7 +1047,7 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
     // fixed width: every pattern of the word (units and tied) has all its choices as long as
     // itself, so an entry's byte j is word byte (piece start + j) in every sub-word, and every
     // sub-word's record follows from sub-word 0's pieces (the fixed pass)
-    bool fixed = VS_PATCH && ok && uni;
+    bool fixed = VS_PATCH && ok && uni && V.L + 8u <= FV_SLOT;
     for (u32 j = 0; fixed && j < V.nocc; j++) {
       const A5xKey key = T.keys[occ[j * VS_BLOCK] & 1023u];
       fixed = key.nvals >= 1 &&
@@ -1377,12 +1381,11 @@ __device__ __forceinline__ void fv_subword(const Tab& T, const FvWord& F, const 
   }
 }
 
-#define FV_SLOT 96  // k_vwords_fill: per-lane sub-word bytes (+ '\n' + read slack; words <= VS_SLOT - 8)
 struct FvWave {
   uint16_t tb[65];  // first fixed-width sub-word task of each lane's word (+ total)
-  u32 w[64];        // the lane's word
   u32 d[64];        // its descriptor (vrec offset)
   unsigned long long r0[64];  // its first record u64 in vrec2
+  unsigned long long ws[64];  // its first byte in the words buffer
 };
 static size_t vwords_fill_lds(u32 table_bytes) { return ((table_bytes + 15u) & ~15u) + 256 * FV_SLOT + 4 * sizeof(FvWave); }
 
@@ -1456,9 +1459,9 @@ __global__ void __launch_bounds__(256) k_vwords_fill(VwArgs a) {
     if (nft) {
       Q.tb[lane] = (uint16_t)(finc - Sf);
       if (lane == 63) Q.tb[64] = (uint16_t)nft;
-      Q.w[lane] = (u32)w;
       Q.d[lane] = valid ? a.roff[w] : 0u;
       Q.r0[lane] = r0;
+      Q.ws[lane] = fix ? a.woff[w] : 0ull;
       WAVE_SYNC();
       for (u32 t0 = 0; t0 < nft; t0 += 64) {
         const u32 t = t0 + lane;
@@ -1466,8 +1469,7 @@ __global__ void __launch_bounds__(256) k_vwords_fill(VwArgs a) {
           const u32 l = vs_owner(Q.tb, t), s = t - Q.tb[l];
           FvWord F;
           F.load(a.vrec + Q.d[l]);
-          const u64 ww = Q.w[l];
-          fv_subword(T, F, a.words + a.woff[ww], s, a.rmode, sub, a.vrec2 + Q.r0[l] + (u64)s * F.rfull);
+          fv_subword(T, F, a.words + Q.ws[l], s, a.rmode, sub, a.vrec2 + Q.r0[l] + (u64)s * F.rfull);
         }
       }
       WAVE_SYNC();  // (Q is rewritten by the next words)
