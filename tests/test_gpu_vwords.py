@@ -214,3 +214,40 @@ def test_virtual_fused_ntlm_every_candidate(mode, mn):
         got.setdefault(d, set()).add((w, c))
     assert sum(len(v) for v in got.values()) == len(hits)
     assert got == want
+
+
+@pytest.mark.parametrize("mode,mn", [(2, 0), (2, 1), (3, 0), (3, 1)])
+def test_virtual_fixed_width_long_words(tmp_path, mode, mn):
+    """Fixed-width words (every key and value of a word the same length: k_keyspace_vsub's
+    descriptor, records written by k_vwords_fill without the planner) up to 64 bytes, with up
+    to four tied patterns, units of 2 and 3 choices (one or two per piece), literal runs cut at
+    7 bytes and tied occurrences straddling pieces; 1- and 2-byte keys -- against the C oracle,
+    counts and bytes included, and each word's order equal to its order in a 16-word batch."""
+    from hashcat_a5_table_generator_amd import Context, pack_words
+    p = tmp_path / "fixed.table"
+    p.write_bytes("a=4\na=@\ns=$\ne=3\no=0\nt=7\nt=+\nα=ש\nβ=נ\nγ=ע\nγ=ק\n".encode())
+    rng = np.random.default_rng(300 + 10 * mode + mn)
+    alpha = ["a", "s", "e", "o", "t", "x", "y", "α", "β", "γ", "z"]
+    words = []
+    for _ in range(1200):
+        w = ""
+        target = int(rng.integers(8, 65))
+        while len(w.encode()) < target:
+            w += alpha[int(rng.integers(0, len(alpha)))]
+        while len(w.encode()) > 64:
+            w = w[:-1]
+        words.append(w.encode())
+    words += [("xyzxyzx" * 9)[:n].encode() + b"aa" for n in range(5, 62, 7)]
+    words += ["αxxxxxxβxxxxxxαxxxxxxβ".encode(), "γγγγ".encode(), ("aseot" * 12).encode()]
+    want = _oracle(str(p), words, mode, mn, 15)
+    with Context(0) as c:
+        c.load_tables([str(p)])
+        cnt, byt = c.keyspace(*pack_words(words), mode, mn, 15)
+        got = c.expand_words(words, mode, mn, 15)
+        small = []
+        for i in range(0, len(words), 16):
+            small += c.expand_words(words[i:i + 16], mode, mn, 15)
+    for w, k, b, g, s, e in zip(words, cnt, byt, got, small, want):
+        assert sorted(g) == e, (mode, mn, w.decode(), len(g), len(e))
+        assert int(k) == len(e) and int(b) == sum(len(x) + 1 for x in e), (mode, mn, w.decode())
+        assert g == s, (mode, mn, w.decode(), "candidate order differs between batches")
