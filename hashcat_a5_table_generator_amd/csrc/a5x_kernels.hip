@@ -749,8 +749,7 @@ __global__ void __launch_bounds__(256) k_keyspace_rprobe(KsArgs a) {
 #define VS_TMAX 4    // tied patterns per word
 #ifndef VS_ABL
 #define VS_ABL 0     // k_keyspace_vsub timing ablations (variant builds only, wrong output): 1 no build
-                     // pass, 2 no count pass, 4 no tasks (walk + pattern analysis only), 16 fixed pass
-                     // without its record stores
+                     // pass, 2 no count pass, 4 no tasks (walk + pattern analysis only)
 #endif
 #ifndef VS_GCAP
 #define VS_GCAP 4    // entries per open group of the sub-word planner (C5 -s A/B, 4 vs 8 = KS_GCAP:
@@ -1172,7 +1171,6 @@ __global__ void __launch_bounds__(VS_BLOCK) __attribute__((amdgpu_waves_per_eu(V
       for (u32 k = 0; k < 4; k++) d[6 + k] = oc[k];
     }
     WAVE_SYNC();
-    (void)ntask;
     // ---- build pass: records and metas at the word's base ----
     for (u32 t0 = 0; t0 < nbtask; t0 += 64) {
       const u32 t = t0 + lane;

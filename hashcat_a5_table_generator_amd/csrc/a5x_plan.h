@@ -374,7 +374,9 @@ struct ArraySink {  // host replay / tests: rec[0..] as laid out in HBM
 };
 
 #ifndef PL_SPLIT_CAP
-#define PL_SPLIT_CAP 8   // groups of <= this many entries merge read-all-then-write-all (registers)
+#define PL_SPLIT_CAP 4   // groups of <= this many entries merge read-all-then-write-all (registers); larger
+                         // ones in place (k_keyspace_thread's 8-entry groups: C3 keyspace 2.19 vs 2.25 ms at 8,
+                         // profiles/r06u_ab_vwords_fixed_width_c5.txt)
 #endif
 
 
